@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST MLP (784-128-64-10, SGD, batch 64 per GPU) training
+throughput in samples/s, data-parallel over N MI355X GPUs.
+
+BASELINE.json metric: "MNIST MLP samples/sec at 1/2/4/8 MI355X" on the config
+"MLP 784-128-64-10 SGD" (reference: ~819 samples/s, README.md:199-203,
+derived in BASELINE.md).  Synthetic 28x28 data (no dataset on the box) and
+random-init weights of the same architecture; fp32 compute like the reference.
+
+Weak scaling: each rank trains batch 64 on its own shard; global batch = 64*N.
+Every timed step is a full optimizer step: fused forward/backward HIP kernels,
+gradient all-reduce over RCCL (N>1), SGD update.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_SAMPLES_PER_S = 819.0  # 599,680 samples / 732 s
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--model", default="784-128-64-10")
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--sync", default="rccl", choices=["rccl", "ring", "torch"])
+    ap.add_argument("--graph-steps", type=int, default=50,
+                    help="steps captured per hipGraph (0 = eager launches)")
+    ap.add_argument("--samples-per-rank", type=int, default=60032)
+    a = ap.parse_args()
+
+    import torch
+
+    from hipdsml.data.mnist import synthetic_mnist
+    from hipdsml.engine.trainer import MlpTrainer
+    from hipdsml.models.mlp import MlpSpec
+    from hipdsml.parallel.dist import DistContext
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE",
+              file=sys.stderr)
+    ctx = DistContext.from_env(device="cuda")
+    spec = MlpSpec.parse(a.model)
+    ds = synthetic_mnist(a.samples_per_rank, seed=1000 + ctx.rank, dim=spec.dims[0])
+    tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,
+                    graph_steps=a.graph_steps)
+    tr.train_steps(a.warmup)
+    tr.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.train_steps(a.steps)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    elapsed = t1 - t0
+    elapsed = ctx.all_reduce_scalars(elapsed, op="max")[0] if ctx.is_distributed else elapsed
+    st = tr.read_stats(global_=True)
+    n = ctx.world_size
+    samples = a.batch * n * a.steps
+    value = samples / elapsed
+    if ctx.rank == 0:
+        out = {
+            "metric": "MNIST MLP samples/sec",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic 28x28 (random-init weights)",
+            "config": {
+                "model": f"MLP {spec} SGD",
+                "global_batch": a.batch * n,
+                "seq_len": None,
+                "parallelism": f"dp{n}",
+                "sync": a.sync if n > 1 else "none",
+                "graph_steps": a.graph_steps,
+                "lr": a.lr,
+            },
+            "train_loss": round(st.avg_loss, 4),
+            "train_acc": round(st.accuracy, 2),
+        }
+        print(json.dumps(out), flush=True)
+    ctx.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,428 @@
+// PyTorch / pybind11 bindings of the hipdsml native library (module `_C`).
+//
+// Tensor-facing entry points validate device, dtype, contiguity and sizes
+// before any kernel is launched (a shape mismatch must never reach a kernel
+// that assumes it).
+#include <ATen/hip/HIPContext.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+#include "runtime/runtime.h"
+
+namespace py = pybind11;
+using namespace dsml;
+
+namespace {
+
+void check_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_f32(const torch::Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+}
+
+int32_t dtype_of(const torch::Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kFloat32: return kF32;
+    case torch::kBFloat16: return kBF16;
+    case torch::kFloat16: return kF16;
+    case torch::kUInt8: return kU8;
+    case torch::kInt32: return kI32;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void hip_ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+// Flat descriptor list, order fixed by models/mlp.py::MlpLayout.desc_list().
+MlpDesc desc_from_list(const std::vector<int64_t>& v) {
+  constexpr size_t kA = kMaxLayers + 1;
+  const size_t want = 4 + 6 * kA + 1 + 2 * kMaxLayers + 2 * kA;
+  TORCH_CHECK(v.size() == want, "MlpDesc list has ", v.size(), " entries, expected ", want);
+  MlpDesc d{};
+  size_t p = 0;
+  d.nlayers = (int32_t)v[p++];
+  d.batch = (int32_t)v[p++];
+  d.nbatches = (int32_t)v[p++];
+  d.w_in_lds = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.dims[i] = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.lds_act[i] = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.lds_dz[i] = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.lds_stride[i] = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.lds_w[i] = (int32_t)v[p++];
+  for (size_t i = 0; i < kA; ++i) d.lds_b[i] = (int32_t)v[p++];
+  d.lds_floats = (int32_t)v[p++];
+  for (int i = 0; i < kMaxLayers; ++i) d.w_off[i] = v[p++];
+  for (int i = 0; i < kMaxLayers; ++i) d.b_off[i] = v[p++];
+  for (size_t i = 0; i < kA; ++i) d.act_off[i] = v[p++];
+  for (size_t i = 0; i < kA; ++i) d.dz_off[i] = v[p++];
+  TORCH_CHECK(d.nlayers >= 1 && d.nlayers <= kMaxLayers, "nlayers out of range");
+  TORCH_CHECK(d.batch >= 1 && d.nbatches >= 1, "batch / nbatches must be >= 1");
+  for (int l = 0; l < d.nlayers; ++l) {
+    TORCH_CHECK(d.dims[l] >= 4 && d.dims[l] % 4 == 0,
+                "layer input dims must be multiples of 4 (dim ", l, " = ", d.dims[l], ")");
+    TORCH_CHECK(d.w_off[l] % 4 == 0 && d.b_off[l] % 4 == 0, "param segments must be 16 B aligned");
+  }
+  TORCH_CHECK(d.dims[d.nlayers] >= 1, "output dim must be >= 1");
+  return d;
+}
+
+int64_t layout_param_end(const MlpDesc& d) {
+  int64_t end = 0;
+  for (int l = 0; l < d.nlayers; ++l) {
+    end = std::max<int64_t>(end, d.w_off[l] + (int64_t)d.dims[l + 1] * d.dims[l]);
+    end = std::max<int64_t>(end, d.b_off[l] + d.dims[l + 1]);
+  }
+  return end;
+}
+
+int64_t layout_ws_end(const MlpDesc& d) {
+  int64_t end = 0;
+  for (int l = 1; l <= d.nlayers; ++l) {
+    end = std::max<int64_t>(end, d.dz_off[l] + (int64_t)d.batch * d.dims[l]);
+    if (l < d.nlayers) end = std::max<int64_t>(end, d.act_off[l] + (int64_t)d.batch * d.dims[l]);
+  }
+  return end;
+}
+
+struct PyMlpRunner {
+  MlpDesc d;
+  std::vector<torch::Tensor> keep;  // keep tensors alive while the runner exists
+  std::unique_ptr<MlpRunner> r;
+  hipStream_t stream = nullptr;
+  int device = 0;
+
+  PyMlpRunner(const std::vector<int64_t>& desc, torch::Tensor X, torch::Tensor labels,
+              torch::Tensor P, torch::Tensor G, torch::Tensor V, torch::Tensor ws,
+              torch::Tensor slab, torch::Tensor ctr, torch::Tensor stats, float lr, float momentum,
+              float weight_decay) {
+    d = desc_from_list(desc);
+    check_f32(X, "X");
+    check_f32(P, "params");
+    check_f32(G, "grads");
+    check_f32(ws, "workspace");
+    check_f32(slab, "slab");
+    check_f32(stats, "stats");
+    check_cuda(labels, "labels");
+    check_cuda(ctr, "ctr");
+    TORCH_CHECK(labels.scalar_type() == torch::kInt32, "labels must be int32");
+    TORCH_CHECK(ctr.scalar_type() == torch::kInt64 && ctr.numel() >= 2, "ctr must be int64[2]");
+    TORCH_CHECK(stats.numel() >= 3, "stats must hold 3 floats");
+    TORCH_CHECK(X.dim() == 2 && X.size(1) >= d.dims[0] && X.size(1) % 4 == 0,
+                "X must be [nsamples, >=d0] with a row stride multiple of 4");
+    TORCH_CHECK(X.size(0) >= (int64_t)d.batch * d.nbatches, "X has fewer rows than batch*nbatches");
+    TORCH_CHECK(labels.numel() >= (int64_t)d.batch * d.nbatches, "labels too short");
+    TORCH_CHECK(P.numel() >= layout_param_end(d) && G.numel() == P.numel(),
+                "params/grads too small for the layout");
+    TORCH_CHECK(ws.numel() >= layout_ws_end(d), "workspace too small for the layout");
+    const MlpLaunchCfg c = mlp_plan_first_layer(d);
+    TORCH_CHECK(slab.numel() >= (int64_t)c.nsplit * d.batch * d.dims[1], "slab too small (need ",
+                (int64_t)c.nsplit * d.batch * d.dims[1], ")");
+    const bool need_v = momentum != 0.f || weight_decay != 0.f;
+    if (need_v) {
+      check_f32(V, "velocity");
+      TORCH_CHECK(V.numel() == P.numel(), "velocity must match params");
+    }
+    device = X.get_device();
+    keep = {X, labels, P, G, V, ws, slab, ctr, stats};
+    MlpBuffers b;
+    b.X = X.data_ptr<float>();
+    b.ldx = X.size(1);
+    b.labels = labels.data_ptr<int32_t>();
+    b.P = P.data_ptr<float>();
+    b.G = G.data_ptr<float>();
+    b.V = need_v ? V.data_ptr<float>() : nullptr;
+    b.ws = ws.data_ptr<float>();
+    b.slab = slab.data_ptr<float>();
+    b.ctr = ctr.data_ptr<int64_t>();
+    b.stats = stats.data_ptr<float>();
+    b.nparams = P.numel();
+    hip_ok(hipSetDevice(device), "hipSetDevice");
+    hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    r = std::make_unique<MlpRunner>(d, b, lr, momentum, weight_decay);
+  }
+  ~PyMlpRunner() {
+    r.reset();
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+  // All runner work goes on the runner's own stream; join with torch's stream
+  // first so tensors initialised by torch are visible.
+  void join_torch() {
+    hipEvent_t e;
+    hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipEventRecord(e, cur_stream()), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(stream, e, 0), "hipStreamWaitEvent");
+    hip_ok(hipEventDestroy(e), "hipEventDestroy");
+  }
+  void step(int n) {
+    join_torch();
+    for (int i = 0; i < n; ++i) r->enqueue_step(stream);
+  }
+  void fwd_bwd() { join_torch(); r->enqueue_fwd_bwd(stream); }
+  void update() { join_torch(); r->enqueue_update(stream); }
+  void capture(int steps, bool capture_comm) {
+    join_torch();
+    hip_ok(hipStreamSynchronize(stream), "sync");
+    r->capture(steps, capture_comm, stream);
+  }
+  void replay(int times) {
+    for (int i = 0; i < times; ++i) r->replay(stream);
+  }
+  void synchronize() {
+    py::gil_scoped_release nogil;
+    hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+  }
+  uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(stream); }
+};
+
+struct PyComm {
+  std::unique_ptr<RcclComm> c;
+  PyComm(py::bytes uid, int rank, int nranks, int device, bool blocking) {
+    std::string s = uid;
+    std::vector<uint8_t> v(s.begin(), s.end());
+    py::gil_scoped_release nogil;  // init is collective: do not hold the GIL
+    c = std::make_unique<RcclComm>(v, rank, nranks, device, blocking);
+  }
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "hipdsml native MI355X (gfx950) kernels and device runtime";
+
+  // ---- elementwise --------------------------------------------------------
+  m.def("sgd_update_", [](torch::Tensor P, torch::Tensor G, double scale) {
+    check_f32(P, "P"); check_f32(G, "G");
+    TORCH_CHECK(P.numel() == G.numel(), "P/G size mismatch");
+    hip_ok(sgd_update_f32(P.data_ptr<float>(), G.data_ptr<float>(), P.numel(), (float)scale,
+                          cur_stream()), "sgd_update_f32");
+  });
+  m.def("sgd_momentum_", [](torch::Tensor P, torch::Tensor G, torch::Tensor V, double lr,
+                            double mom, double wd, double gscale) {
+    check_f32(P, "P"); check_f32(G, "G"); check_f32(V, "V");
+    TORCH_CHECK(P.numel() == G.numel() && P.numel() == V.numel(), "P/G/V size mismatch");
+    hip_ok(sgd_momentum_f32(P.data_ptr<float>(), G.data_ptr<float>(), V.data_ptr<float>(),
+                            P.numel(), (float)lr, (float)mom, (float)wd, (float)gscale,
+                            cur_stream()), "sgd_momentum_f32");
+  });
+  m.def("reduce_into", [](torch::Tensor dst, torch::Tensor a, torch::Tensor b, int op) {
+    check_cuda(dst, "dst"); check_cuda(a, "a"); check_cuda(b, "b");
+    TORCH_CHECK(dst.scalar_type() == a.scalar_type() && a.scalar_type() == b.scalar_type(),
+                "dtype mismatch");
+    TORCH_CHECK(dst.numel() == a.numel() && a.numel() == b.numel(), "size mismatch");
+    hip_ok(reduce_into(dst.data_ptr(), a.data_ptr(), b.data_ptr(), dst.numel(), dtype_of(dst), op,
+                       cur_stream()), "reduce_into");
+  });
+  m.def("scale_", [](torch::Tensor x, double alpha) {
+    check_cuda(x, "x");
+    hip_ok(scale_inplace(x.data_ptr(), x.numel(), dtype_of(x), (float)alpha, cur_stream()),
+           "scale_inplace");
+  });
+  m.def("u8_to_f32", [](torch::Tensor dst, torch::Tensor src, double scale) {
+    check_f32(dst, "dst"); check_cuda(src, "src");
+    TORCH_CHECK(src.scalar_type() == torch::kUInt8 && src.numel() == dst.numel(), "bad src");
+    hip_ok(u8_to_f32_scaled(dst.data_ptr<float>(), src.data_ptr<uint8_t>(), dst.numel(),
+                            (float)scale, cur_stream()), "u8_to_f32");
+  });
+  m.def("f32_to_bf16", [](torch::Tensor dst, torch::Tensor src) {
+    check_f32(src, "src"); check_cuda(dst, "dst");
+    TORCH_CHECK(dst.scalar_type() == torch::kBFloat16 && dst.numel() == src.numel(), "bad dst");
+    hip_ok(f32_to_bf16(reinterpret_cast<uint16_t*>(dst.data_ptr()), src.data_ptr<float>(),
+                       src.numel(), cur_stream()), "f32_to_bf16");
+  });
+  m.def("bf16_to_f32", [](torch::Tensor dst, torch::Tensor src) {
+    check_f32(dst, "dst"); check_cuda(src, "src");
+    TORCH_CHECK(src.scalar_type() == torch::kBFloat16 && dst.numel() == src.numel(), "bad src");
+    hip_ok(bf16_to_f32(dst.data_ptr<float>(), reinterpret_cast<const uint16_t*>(src.data_ptr()),
+                       src.numel(), cur_stream()), "bf16_to_f32");
+  });
+
+  // ---- fused MLP -----------------------------------------------------------
+  m.def("mlp_stamps", []() {
+    std::vector<uint64_t> v(kMaxStamps);
+    hip_ok(mlp_read_stamps(v.data()), "mlp_read_stamps");
+    return v;
+  });
+  m.def("mlp_set_stamping", [](bool on) { mlp_set_stamping(on); });
+  m.def("mlp_plan", [](const std::vector<int64_t>& desc) {
+    const MlpDesc d = desc_from_list(desc);
+    const MlpLaunchCfg c = mlp_plan_first_layer(d);
+    return py::make_tuple(c.kchunk, c.nsplit, mlp_wgrad_tiles(d), mlp_rowchain_fits(d));
+  });
+  m.def("mlp_eval", [](const std::vector<int64_t>& desc, torch::Tensor X, torch::Tensor labels,
+                       int64_t row0, torch::Tensor P, torch::Tensor ws, torch::Tensor slab,
+                       torch::Tensor stats) {
+    const MlpDesc d = desc_from_list(desc);
+    check_f32(X, "X"); check_f32(P, "P"); check_f32(slab, "slab"); check_f32(stats, "stats");
+    check_f32(ws, "ws"); check_cuda(labels, "labels");
+    TORCH_CHECK(labels.scalar_type() == torch::kInt32, "labels must be int32");
+    TORCH_CHECK(X.dim() == 2 && X.size(1) % 4 == 0 && X.size(1) >= d.dims[0], "bad X");
+    TORCH_CHECK(row0 >= 0 && row0 + d.batch <= X.size(0) && row0 + d.batch <= labels.numel(),
+                "eval rows out of range");
+    TORCH_CHECK(P.numel() >= layout_param_end(d), "params too small");
+    const MlpLaunchCfg c = mlp_plan_first_layer(d);
+    TORCH_CHECK(slab.numel() >= (int64_t)c.nsplit * d.batch * d.dims[1], "slab too small");
+    TORCH_CHECK(d.lds_floats * 4 <= 160 * 1024, "model too wide for the fused row chain");
+    mlp_eval(d, X.data_ptr<float>(), X.size(1), labels.data_ptr<int32_t>(), row0,
+             P.data_ptr<float>(), ws.data_ptr<float>(), slab.data_ptr<float>(),
+             stats.data_ptr<float>(), cur_stream());
+  });
+
+  py::class_<PyMlpRunner>(m, "MlpRunner")
+      .def(py::init<const std::vector<int64_t>&, torch::Tensor, torch::Tensor, torch::Tensor,
+                    torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+                    torch::Tensor, float, float, float>())
+      .def("step", &PyMlpRunner::step, py::arg("n") = 1)
+      .def("fwd_bwd", &PyMlpRunner::fwd_bwd)
+      .def("update", &PyMlpRunner::update)
+      .def("capture", &PyMlpRunner::capture, py::arg("steps"), py::arg("capture_comm") = true)
+      .def("replay", &PyMlpRunner::replay, py::arg("times") = 1)
+      .def("synchronize", &PyMlpRunner::synchronize)
+      .def("stream_handle", &PyMlpRunner::stream_handle)
+      .def("graph_steps", [](PyMlpRunner& s) { return s.r->graph_steps(); })
+      .def("set_lr", [](PyMlpRunner& s, float lr) { s.r->set_lr(lr); })
+      .def("set_comm", [](PyMlpRunner& s, PyComm* c, int algo, int64_t chunk) {
+        s.r->set_comm(c ? c->c.get() : nullptr, algo, chunk);
+      }, py::arg("comm"), py::arg("algo") = 0, py::arg("chunk_bytes") = 1 << 20)
+      .def("plan", [](PyMlpRunner& s) {
+        const MlpLaunchCfg c = s.r->cfg();
+        return py::make_tuple(c.kchunk, c.nsplit);
+      });
+
+  // ---- RCCL ----------------------------------------------------------------
+  m.def("rccl_unique_id", []() {
+    const auto v = rccl_unique_id();
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  py::class_<PyComm>(m, "RcclComm")
+      .def(py::init<py::bytes, int, int, int, bool>(), py::arg("uid"), py::arg("rank"),
+           py::arg("nranks"), py::arg("device"), py::arg("blocking") = true)
+      .def_property_readonly("rank", [](PyComm& s) { return s.c->rank(); })
+      .def_property_readonly("nranks", [](PyComm& s) { return s.c->nranks(); })
+      .def("allreduce_", [](PyComm& s, torch::Tensor t, int op) {
+        check_cuda(t, "t");
+        s.c->allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, cur_stream());
+      }, py::arg("t"), py::arg("op") = 0)
+      .def("ring_allreduce_", [](PyComm& s, torch::Tensor t, int op, int64_t chunk_bytes) {
+        check_cuda(t, "t");
+        TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "tensor must be 16 B aligned");
+        s.c->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream());
+      }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20)
+      .def("broadcast_", [](PyComm& s, torch::Tensor t, int root) {
+        check_cuda(t, "t");
+        s.c->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());
+      })
+      .def("send", [](PyComm& s, torch::Tensor t, int peer) {
+        check_cuda(t, "t");
+        s.c->send(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
+      })
+      .def("recv_", [](PyComm& s, torch::Tensor t, int peer) {
+        check_cuda(t, "t");
+        s.c->recv(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
+      })
+      .def("barrier", [](PyComm& s) {
+        hipStream_t st = cur_stream();
+        py::gil_scoped_release nogil;
+        s.c->barrier(st);
+      })
+      .def("abort", [](PyComm& s) { s.c->abort(); })
+      .def("async_error", [](PyComm& s) { return s.c->async_error(); })
+      .def_property_readonly("aborted", [](PyComm& s) { return s.c->aborted(); });
+
+  // ---- device runtime (arena / copy engine / stream table) ------------------
+  py::class_<DeviceArena>(m, "DeviceArena")
+      .def(py::init<int, uint64_t, uint64_t>(), py::arg("device"), py::arg("size"),
+           py::arg("base_addr") = DeviceArena::kBaseAddr)
+      .def_property_readonly("min_addr", &DeviceArena::min_addr)
+      .def_property_readonly("max_addr", &DeviceArena::max_addr)
+      .def_property_readonly("size", &DeviceArena::size)
+      .def("contains", &DeviceArena::contains)
+      .def("ptr", [](DeviceArena& a, uint64_t addr, uint64_t n) {
+        try { return reinterpret_cast<uintptr_t>(a.translate(addr, n)); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+      })
+      .def("record_extent", &DeviceArena::record_extent)
+      .def("extent", &DeviceArena::extent)
+      .def("reduce", [](DeviceArena& a, uint64_t dst, uint64_t src, uint64_t nbytes, int dtype,
+                        int op) {
+        const uint64_t es = dtype == kF32 || dtype == kI32 ? 4 : (dtype == kU8 ? 1 : 2);
+        void* d = nullptr; void* sp = nullptr;
+        try { d = a.translate(dst, nbytes); sp = a.translate(src, nbytes); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+        TORCH_CHECK(nbytes % es == 0, "nbytes not a multiple of the element size");
+        hipStream_t s = nullptr;
+        hip_ok(reduce_inplace(d, sp, (int64_t)(nbytes / es), dtype, op, s), "reduce_inplace");
+        hip_ok(hipStreamSynchronize(s), "sync");
+      });
+  py::class_<CopyEngine>(m, "CopyEngine")
+      .def(py::init<int, size_t>(), py::arg("device"), py::arg("staging_bytes") = 16u << 20)
+      .def("h2d", [](CopyEngine& c, DeviceArena& a, uint64_t addr, py::bytes data) {
+        std::string s = data;
+        void* dst;
+        try { dst = a.translate(addr, s.size()); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+        py::gil_scoped_release nogil;
+        c.h2d(dst, s.data(), s.size());
+        a.record_extent(addr, s.size());
+      })
+      .def("d2h", [](CopyEngine& c, DeviceArena& a, uint64_t addr, uint64_t n) {
+        const void* src;
+        try { src = a.translate(addr, n); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+        std::string out(n, '\0');
+        {
+          py::gil_scoped_release nogil;
+          c.d2h(out.data(), src, n);
+        }
+        return py::bytes(out);
+      })
+      .def("d2d", [](CopyEngine& c, DeviceArena& a, uint64_t dst, uint64_t src, uint64_t n) {
+        void* d; const void* s;
+        try { d = a.translate(dst, n); s = a.translate(src, n); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+        py::gil_scoped_release nogil;
+        c.d2d(d, s, n);
+      })
+      .def_property_readonly("bytes_h2d", &CopyEngine::bytes_h2d)
+      .def_property_readonly("bytes_d2h", &CopyEngine::bytes_d2h);
+  py::class_<StreamTable>(m, "StreamTable")
+      .def(py::init<DeviceArena*, CopyEngine*>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("begin_send", &StreamTable::begin_send)
+      .def("begin_receive", [](StreamTable& t, uint64_t id, uint64_t addr, uint64_t n, uint32_t src) {
+        try { t.begin_receive(id, addr, n, src); }
+        catch (const std::out_of_range& e) { throw py::index_error(e.what()); }
+        catch (const std::invalid_argument& e) { throw py::key_error(e.what()); }
+      })
+      .def("push_chunk", [](StreamTable& t, uint64_t id, py::bytes data) {
+        std::string s = data;
+        py::gil_scoped_release nogil;
+        return t.push_chunk(id, s.data(), s.size());
+      })
+      .def("finish", &StreamTable::finish)
+      .def("status", [](StreamTable& t, uint64_t id) { return (int)t.status(id); })
+      .def("read_send_buffer", [](StreamTable& t, uint64_t id) {
+        std::vector<uint8_t> v;
+        try { v = t.read_send_buffer(id); }
+        catch (const std::invalid_argument& e) { throw py::key_error(e.what()); }
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("erase", &StreamTable::erase)
+      .def("__len__", &StreamTable::size);
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    return n;
+  });
+}

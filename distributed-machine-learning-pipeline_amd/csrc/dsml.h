@@ -1,0 +1,108 @@
+// Host-side interface of the hipdsml native library (kernels + runtime).
+//
+// The kernels are plain HIP launchers over raw device pointers and a
+// hipStream_t, so the device runtime (arena / copy engine / stream table /
+// RCCL comm) and the PyTorch binding layer can both drive them.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dsml {
+
+constexpr int kMaxLayers = 8;
+
+// Descriptor of one data-parallel replica's MLP training state.
+// Parameter layout (flat fp32 buffer, PyTorch Linear convention):
+//   layer l (0-based): W_l [dims[l+1] x dims[l]] row-major at w_off[l],
+//                      b_l [dims[l+1]]               at b_off[l].
+// Every segment starts on a 16-float (64 B) boundary so float4 loads are legal.
+// Workspace layout (flat fp32):
+//   act_off[l]  l=1..L-1 : H_l  = relu(Z_l)   [batch x dims[l]]
+//   dz_off[l]   l=1..L   : dZ_l = dLoss/dZ_l  [batch x dims[l]]
+// The reference keeps W1 as [in x out] (client.go:118); conversion helpers in
+// models/mlp.py map between the two layouts.
+struct MlpDesc {
+  int32_t nlayers;
+  int32_t batch;     // rows handled per step by this replica
+  int32_t nbatches;  // batches in the resident dataset (step counter wraps)
+  int32_t w_in_lds;  // row chain stages W_l (l >= 2) in LDS (else reads them from HBM/L2)
+  int32_t dims[kMaxLayers + 1];
+  int32_t lds_act[kMaxLayers + 1];  // float offsets of the LDS activation tiles
+  int32_t lds_dz[kMaxLayers + 1];   // float offsets of the LDS gradient tiles
+  int32_t lds_stride[kMaxLayers + 1];
+  int32_t lds_w[kMaxLayers + 1];    // LDS-staged W_l (l >= 2), row stride dims[l-1] + 4
+  int32_t lds_b[kMaxLayers + 1];    // LDS-staged b_l (l >= 2)
+  int32_t lds_floats;               // total LDS floats of the row-chain kernel
+  int32_t pad1;
+  int64_t w_off[kMaxLayers];
+  int64_t b_off[kMaxLayers];
+  int64_t act_off[kMaxLayers + 1];
+  int64_t dz_off[kMaxLayers + 1];
+};
+
+// ---- fused fp32 MLP step (kernels/mlp_f32.hip) -------------------------------
+// Row tile of the row-chain kernel.
+constexpr int kRowTile = 16;
+
+struct MlpLaunchCfg {
+  int kchunk;   // K elements per split of the first-layer GEMM (multiple of 16, <= 128)
+  int nsplit;   // number of K splits (slabs)
+};
+MlpLaunchCfg mlp_plan_first_layer(const MlpDesc& d);
+int mlp_wgrad_tiles(const MlpDesc& d);
+bool mlp_rowchain_fits(const MlpDesc& d);
+
+// Forward of layer 1 as a split-K MFMA GEMM into per-split slabs.
+hipError_t mlp_f32_first_layer(const float* X, int64_t ldx, const float* P, float* slab,
+                               const int64_t* ctr, int64_t row0, const MlpDesc& d,
+                               const MlpLaunchCfg& c, hipStream_t s);
+// Row-local chain: layer-1 epilogue, layers 2..L forward, softmax-xent,
+// activation gradients down to dZ_1.  train=0 => forward + stats only.
+hipError_t mlp_f32_rowchain(const float* P, const float* slab, int nsplit, float* ws,
+                            const int32_t* labels, int64_t* ctr, int64_t row0,
+                            const MlpDesc& d, float* stats, int train, float inv_batch,
+                            hipStream_t s);
+// Weight/bias gradients of every layer; fused SGD (P -= lr*g) when fused_sgd,
+// else gradients are written to G.
+//
+// Step counters (no atomics): ctr[0] = A, ctr[1] = B.  Step s starts with
+// A = B = s.  K_A and K_B read B; K_B's block 0 writes A = s + 1; K_C reads
+// A - 1 and its block 0 writes B = A.  No kernel writes a slot it also reads,
+// so there is no intra-launch race and kernel boundaries order the rest.
+hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const float* ws,
+                         int64_t* ctr, int64_t row0, const MlpDesc& d, float lr, int fused_sgd,
+                         hipStream_t s);
+
+// ---- elementwise / reduction (kernels/elementwise.hip) -----------------------
+enum DType : int32_t { kF32 = 0, kBF16 = 1, kF16 = 2, kU8 = 3, kI32 = 4 };
+enum ReduceOp : int32_t { kSum = 0, kProd = 1, kMin = 2, kMax = 3 };
+
+// In-kernel phase stamps (s_memrealtime, 100 MHz) of block 0, for profiling.
+constexpr int kMaxStamps = 32;
+hipError_t mlp_read_stamps(uint64_t* host_out);  // kMaxStamps entries
+void mlp_set_stamping(bool on);
+
+hipError_t sgd_update_f32(float* P, const float* G, int64_t n, float scale, hipStream_t s);
+hipError_t sgd_momentum_f32(float* P, const float* G, float* V, int64_t n, float lr,
+                            float momentum, float weight_decay, float gscale, hipStream_t s);
+// dst = op(dst, src) elementwise; n in elements.
+hipError_t reduce_inplace(void* dst, const void* src, int64_t n, int32_t dtype, int32_t op,
+                          hipStream_t s);
+// dst = op(a, b)
+hipError_t reduce_into(void* dst, const void* a, const void* b, int64_t n, int32_t dtype,
+                       int32_t op, hipStream_t s);
+hipError_t scale_inplace(void* x, int64_t n, int32_t dtype, float alpha, hipStream_t s);
+hipError_t u8_to_f32_scaled(float* dst, const uint8_t* src, int64_t n, float scale,
+                            hipStream_t s);
+hipError_t f32_to_bf16(uint16_t* dst, const float* src, int64_t n, hipStream_t s);
+hipError_t bf16_to_f32(float* dst, const uint16_t* src, int64_t n, hipStream_t s);
+
+// ---- bf16 MFMA GEMM with fused epilogues (kernels/gemm_bf16.hip) -------------
+enum Epilogue : int32_t {
+  kEpiNone = 0,       // C = A.B
+  kEpiBias = 1,       // C = A.B + bias
+  kEpiBiasRelu = 2,   // C = relu(A.B + bias)
+  kEpiReluMask = 3,   // C = (A.B) * (mask > 0)   (ReLU backward, mask = post-relu act)
+};
+
+}  // namespace dsml

@@ -1,0 +1,307 @@
+// RCCL communicator (ring all-reduce over ncclSend/ncclRecv, RCCL all-reduce
+// reference path, abort / async error) and the hipGraph-captured MLP replica
+// step.
+//
+// Reference behaviour being replaced: the coordinator-driven "ring"
+// (gpu_coordinator_server.go:272-566) that moved bytes over gRPC to each rank's
+// OWN device and reduced them as uint8.  Here each device
+// process owns one GPU and a real ring moves segments GPU->GPU over xGMI.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "runtime.h"
+
+namespace dsml {
+
+static ncclDataType_t to_nccl(int32_t dt) {
+  switch (dt) {
+    case kF32: return ncclFloat32;
+    case kBF16: return ncclBfloat16;
+    case kF16: return ncclFloat16;
+    case kU8: return ncclUint8;
+    case kI32: return ncclInt32;
+    default: throw std::invalid_argument("unsupported dtype " + std::to_string(dt));
+  }
+}
+static size_t dtype_size(int32_t dt) {
+  switch (dt) {
+    case kF32: case kI32: return 4;
+    case kBF16: case kF16: return 2;
+    case kU8: return 1;
+    default: throw std::invalid_argument("unsupported dtype " + std::to_string(dt));
+  }
+}
+static ncclRedOp_t to_nccl_op(int32_t op) {
+  switch (op) {
+    case kSum: return ncclSum;
+    case kProd: return ncclProd;
+    case kMin: return ncclMin;
+    case kMax: return ncclMax;
+    default: throw std::invalid_argument("unsupported reduce op " + std::to_string(op));
+  }
+}
+
+std::vector<uint8_t> rccl_unique_id() {
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  return std::vector<uint8_t>(reinterpret_cast<uint8_t*>(&id),
+                              reinterpret_cast<uint8_t*>(&id) + sizeof(id));
+}
+
+RcclComm::RcclComm(const std::vector<uint8_t>& uid, int rank, int nranks, int device,
+                   bool blocking)
+    : rank_(rank), nranks_(nranks), device_(device), blocking_(blocking) {
+  if (uid.size() != sizeof(ncclUniqueId))
+    throw std::invalid_argument("unique id must be " + std::to_string(sizeof(ncclUniqueId)) +
+                                " bytes");
+  if (rank < 0 || rank >= nranks) throw std::invalid_argument("rank out of range");
+  DSML_HIP_CHECK(hipSetDevice(device_));
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = blocking ? 1 : 0;
+  check(ncclCommInitRankConfig(&comm_, nranks_, id, rank_, &cfg), "ncclCommInitRankConfig");
+  DSML_HIP_CHECK(hipMalloc(&one_, 64));
+  DSML_HIP_CHECK(hipMemset(one_, 0, 64));
+}
+
+RcclComm::~RcclComm() {
+  (void)hipSetDevice(device_);
+  if (comm_) {
+    if (aborted_) {
+      // already torn down by abort()
+    } else {
+      (void)ncclCommDestroy(comm_);
+    }
+  }
+  if (tmp_) (void)hipFree(tmp_);
+  if (one_) (void)hipFree(one_);
+}
+
+void RcclComm::check(ncclResult_t r, const char* what) {
+  if (r == ncclInProgress) {
+    // Non-blocking communicator: wait for the call to be enqueued, bounded so a
+    // dead peer cannot wedge the caller forever (the health monitor aborts).
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t st = ncclInProgress;
+    while (st == ncclInProgress) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
+      if (st != ncclInProgress) break;
+      if (aborted_) throw std::runtime_error(std::string(what) + ": communicator aborted");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(300))
+        throw std::runtime_error(std::string(what) + ": timed out waiting for RCCL");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    r = st;
+  }
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+void RcclComm::ensure_tmp(size_t bytes) {
+  if (bytes <= tmp_bytes_) return;
+  if (tmp_) DSML_HIP_CHECK(hipFree(tmp_));
+  tmp_bytes_ = (bytes + 255) & ~size_t(255);
+  DSML_HIP_CHECK(hipMalloc(&tmp_, tmp_bytes_));
+}
+
+void RcclComm::allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("allreduce on aborted communicator");
+  check(ncclAllReduce(buf, buf, (size_t)count, to_nccl(dtype), to_nccl_op(op), comm_, s),
+        "ncclAllReduce");
+}
+
+void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op,
+                              int64_t chunk_bytes, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("ring_allreduce on aborted communicator");
+  const int n = nranks_;
+  if (n < 2 || count == 0) return;
+  const size_t es = dtype_size(dtype);
+  // Segment boundaries: equal segments rounded to 16 B so every segment start
+  // stays vector-aligned for the reduce kernel (the reference padded the whole
+  // buffer to a multiple of n instead, gpu_coordinator_server.go:299-334).
+  const int64_t align = 16 / (int64_t)es;
+  int64_t seg = (count + n - 1) / n;
+  seg = (seg + align - 1) / align * align;
+  std::vector<int64_t> off(n + 1);
+  for (int i = 0; i <= n; ++i) off[i] = std::min<int64_t>((int64_t)i * seg, count);
+  int64_t chunk = chunk_bytes > 0 ? chunk_bytes / (int64_t)es : seg;
+  chunk = std::max<int64_t>(align, chunk / align * align);
+  if (chunk > seg) chunk = seg;
+  ensure_tmp((size_t)chunk * es);
+  uint8_t* b = static_cast<uint8_t*>(buf);
+  const int next = (rank_ + 1) % n, prev = (rank_ + n - 1) % n;
+  const ncclDataType_t t = to_nccl(dtype);
+  // Reduce-scatter: step s sends segment (r - s), receives (r - s - 1) and
+  // reduces it; afterwards rank r owns the fully reduced segment (r + 1).
+  for (int st = 0; st < n - 1; ++st) {
+    const int si = ((rank_ - st) % n + n) % n;
+    const int ri = ((rank_ - st - 1) % n + n) % n;
+    const int64_t slen = off[si + 1] - off[si], rlen = off[ri + 1] - off[ri];
+    const int64_t steps = std::max<int64_t>((std::max(slen, rlen) + chunk - 1) / chunk, 1);
+    for (int64_t c = 0; c < steps; ++c) {
+      const int64_t so = c * chunk, ro = c * chunk;
+      const int64_t sn = std::max<int64_t>(0, std::min(chunk, slen - so));
+      const int64_t rn = std::max<int64_t>(0, std::min(chunk, rlen - ro));
+      check(ncclGroupStart(), "ncclGroupStart");
+      if (sn > 0) check(ncclSend(b + (off[si] + so) * es, sn, t, next, comm_, s), "ncclSend");
+      if (rn > 0) check(ncclRecv(tmp_, rn, t, prev, comm_, s), "ncclRecv");
+      check(ncclGroupEnd(), "ncclGroupEnd");
+      if (rn > 0) DSML_HIP_CHECK(reduce_inplace(b + (off[ri] + ro) * es, tmp_, rn, dtype, op, s));
+    }
+  }
+  // All-gather: step s sends segment (r + 1 - s), receives (r - s) in place.
+  for (int st = 0; st < n - 1; ++st) {
+    const int si = ((rank_ + 1 - st) % n + n) % n;
+    const int ri = ((rank_ - st) % n + n) % n;
+    const int64_t slen = off[si + 1] - off[si], rlen = off[ri + 1] - off[ri];
+    check(ncclGroupStart(), "ncclGroupStart");
+    if (slen > 0) check(ncclSend(b + off[si] * es, slen, t, next, comm_, s), "ncclSend");
+    if (rlen > 0) check(ncclRecv(b + off[ri] * es, rlen, t, prev, comm_, s), "ncclRecv");
+    check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+}
+
+void RcclComm::broadcast(void* buf, int64_t count, int32_t dtype, int root, hipStream_t s) {
+  check(ncclBroadcast(buf, buf, (size_t)count, to_nccl(dtype), root, comm_, s), "ncclBroadcast");
+}
+
+void RcclComm::send(const void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s) {
+  check(ncclSend(buf, (size_t)count, to_nccl(dtype), peer, comm_, s), "ncclSend");
+}
+
+void RcclComm::recv(void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s) {
+  check(ncclRecv(buf, (size_t)count, to_nccl(dtype), peer, comm_, s), "ncclRecv");
+}
+
+void RcclComm::barrier(hipStream_t s) {
+  check(ncclAllReduce(one_, one_, 1, ncclInt32, ncclSum, comm_, s), "barrier");
+  DSML_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void RcclComm::abort() {
+  if (aborted_ || !comm_) return;
+  aborted_ = true;
+  (void)ncclCommAbort(comm_);
+}
+
+std::string RcclComm::async_error() {
+  if (aborted_) return "aborted";
+  ncclResult_t st = ncclSuccess;
+  const ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
+  if (r != ncclSuccess) return ncclGetErrorString(r);
+  if (st == ncclSuccess) return "";
+  if (st == ncclInProgress) return "in-progress";
+  return ncclGetErrorString(st);
+}
+
+// ---------------------------------------------------------------------------
+// MlpRunner
+// ---------------------------------------------------------------------------
+MlpRunner::MlpRunner(const MlpDesc& d, const MlpBuffers& b, float lr, float momentum,
+                     float weight_decay)
+    : d_(d), b_(b), lr_(lr), mom_(momentum), wd_(weight_decay) {
+  if (d_.nlayers < 1 || d_.nlayers > kMaxLayers) throw std::invalid_argument("bad nlayers");
+  if (!mlp_rowchain_fits(d_)) throw std::invalid_argument("MLP too wide for the fused row chain");
+  if (b_.ctr == nullptr) throw std::invalid_argument("MlpRunner needs the step counters");
+  cfg_ = mlp_plan_first_layer(d_);
+  if (cfg_.nsplit > 8) throw std::invalid_argument("first layer needs > 8 K splits");
+  if ((mom_ != 0.f || wd_ != 0.f) && b_.V == nullptr)
+    throw std::invalid_argument("momentum/weight decay need a velocity buffer");
+}
+
+MlpRunner::~MlpRunner() { reset_graph(); }
+
+void MlpRunner::reset_graph() {
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+  exec_ = nullptr;
+  graph_ = nullptr;
+  graph_steps_ = 0;
+}
+
+void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
+  comm_ = c;
+  algo_ = algo;
+  chunk_bytes_ = chunk_bytes;
+  reset_graph();
+}
+
+void MlpRunner::set_lr(float lr) {
+  lr_ = lr;
+  reset_graph();  // lr is a baked kernel argument
+}
+
+void MlpRunner::enqueue_fwd_bwd(hipStream_t s) {
+  DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, s));
+  DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
+                                  b_.stats, 1, 1.0f / (float)d_.batch, s));
+  DSML_HIP_CHECK(mlp_f32_wgrad(b_.X, b_.ldx, b_.P, b_.G, b_.ws, b_.ctr, 0, d_, lr_, 0, s));
+}
+
+void MlpRunner::enqueue_update(hipStream_t s) {
+  const int n = comm_ ? comm_->nranks() : 1;
+  const float gscale = 1.0f / (float)n;
+  if (mom_ != 0.f || wd_ != 0.f)
+    DSML_HIP_CHECK(sgd_momentum_f32(b_.P, b_.G, b_.V, b_.nparams, lr_, mom_, wd_, gscale, s));
+  else
+    DSML_HIP_CHECK(sgd_update_f32(b_.P, b_.G, b_.nparams, lr_ * gscale, s));
+}
+
+void MlpRunner::enqueue_step(hipStream_t s) {
+  const bool multi = comm_ != nullptr && comm_->nranks() > 1;
+  const bool plain = mom_ == 0.f && wd_ == 0.f;
+  if (!multi && plain) {
+    // Single replica, plain SGD: the update is fused into the weight-grad kernel.
+    DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, s));
+    DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
+                                    b_.stats, 1, 1.0f / (float)d_.batch, s));
+    DSML_HIP_CHECK(mlp_f32_wgrad(b_.X, b_.ldx, b_.P, b_.G, b_.ws, b_.ctr, 0, d_, lr_, 1, s));
+    return;
+  }
+  enqueue_fwd_bwd(s);
+  if (multi) {
+    if (algo_ == 1)
+      comm_->ring_allreduce(b_.G, b_.nparams, kF32, kSum, chunk_bytes_, s);
+    else
+      comm_->allreduce(b_.G, b_.nparams, kF32, kSum, s);
+  }
+  enqueue_update(s);
+}
+
+void MlpRunner::capture(int steps, bool capture_comm, hipStream_t s) {
+  if (steps < 1) throw std::invalid_argument("capture: steps must be >= 1");
+  reset_graph();
+  capture_comm_ = capture_comm;
+  DSML_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+  try {
+    for (int i = 0; i < steps; ++i) enqueue_step(s);
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(s, &g);
+    if (g) (void)hipGraphDestroy(g);
+    throw;
+  }
+  DSML_HIP_CHECK(hipStreamEndCapture(s, &graph_));
+  DSML_HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  graph_steps_ = steps;
+}
+
+void MlpRunner::replay(hipStream_t s) {
+  if (!exec_) throw std::runtime_error("replay: no captured graph");
+  DSML_HIP_CHECK(hipGraphLaunch(exec_, s));
+}
+
+void mlp_eval(const MlpDesc& d, const float* X, int64_t ldx, const int32_t* labels, int64_t row0,
+              const float* P, float* ws, float* slab, float* stats, hipStream_t s) {
+  const MlpLaunchCfg c = mlp_plan_first_layer(d);
+  DSML_HIP_CHECK(mlp_f32_first_layer(X, ldx, P, slab, nullptr, row0, d, c, s));
+  DSML_HIP_CHECK(
+      mlp_f32_rowchain(P, slab, c.nsplit, ws, labels, nullptr, row0, d, stats, 0, 1.0f, s));
+}
+
+}  // namespace dsml

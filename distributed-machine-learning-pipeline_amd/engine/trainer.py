@@ -1,0 +1,258 @@
+"""Data-parallel MLP training engine.
+
+One replica per process / GPU.  On a GPU the whole step runs in the native
+runner (three fused HIP kernels + gradient all-reduce + SGD, optionally
+captured into one hipGraph); on a CPU-only host the fp32 torch reference math
+runs instead (used by the CPU test-suite and gloo multi-process tests).
+
+Reference training loop being replaced: ``DSML/client/client.go:579-653``
+(10 epochs x 937 batches, forward/backward on the client CPU, gradient pushed
+to every device, "AllReduceRing", gradient pulled back, SGD on the client,
+weights pushed to every device).  Here weights, data and gradients never leave
+HBM; each replica trains on its own shard and gradients are averaged.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from ..data.mnist import Dataset
+from ..models.mlp import MlpLayout, MlpSpec, forward_ref, grads_ref, init_params
+from ..parallel.dist import DistContext, make_native_comm
+
+log = logging.getLogger("hipdsml.trainer")
+
+SYNC_MODES = ("rccl", "ring", "torch")
+
+
+@dataclass
+class StepStats:
+    loss_sum: float = 0.0
+    correct: float = 0.0
+    count: float = 0.0
+
+    @property
+    def avg_loss(self) -> float:
+        return self.loss_sum / max(self.count, 1.0)
+
+    @property
+    def accuracy(self) -> float:
+        return 100.0 * self.correct / max(self.count, 1.0)
+
+
+def _pad_cols(X: torch.Tensor, mult: int = 4) -> torch.Tensor:
+    d = X.shape[1]
+    if d % mult == 0:
+        return X.contiguous()
+    out = torch.zeros(X.shape[0], d + (mult - d % mult), dtype=X.dtype, device=X.device)
+    out[:, :d] = X
+    return out
+
+
+class MlpTrainer:
+    def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
+                 ctx: Optional[DistContext] = None, seed: int = 0, init: str = "reference",
+                 momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
+                 ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
+                 params: Optional[torch.Tensor] = None):
+        if sync not in SYNC_MODES:
+            raise ValueError(f"sync must be one of {SYNC_MODES}")
+        self.ctx = ctx or DistContext()
+        self.spec = spec
+        self.device = self.ctx.device
+        self.batch = int(batch)
+        self.lr = float(lr)
+        self.momentum = float(momentum)
+        self.weight_decay = float(weight_decay)
+        self.sync = sync
+        self.graph_steps = int(graph_steps)
+        if len(data) < self.batch:
+            raise ValueError(f"dataset has {len(data)} rows < batch {self.batch}")
+        if data.X.shape[1] != spec.dims[0]:
+            raise ValueError(f"data dim {data.X.shape[1]} != model input {spec.dims[0]}")
+        self.X = _pad_cols(data.X.to(self.device, torch.float32))
+        self.y = data.y.to(self.device, torch.int32).contiguous()
+        self.nbatches = len(data) // self.batch
+        self.layout = MlpLayout(spec, self.batch, self.nbatches)
+        P = params if params is not None else init_params(self.layout, seed, init)
+        if P.numel() != self.layout.nparams:
+            raise ValueError("params do not match the layout")
+        self.P = P.to(self.device, torch.float32).contiguous().clone()
+        self.G = torch.zeros_like(self.P)
+        self.V = torch.zeros_like(self.P) if (momentum or weight_decay) else torch.empty(0, device=self.device)
+        self.steps_done = 0
+        self._stats_cpu = StepStats()
+        self.comm = None
+        self.runner = None
+        if self.device.type == "cuda":
+            self._init_hip(ring_chunk_bytes)
+            self.backend = "hip"
+        else:
+            self.backend = "torch"
+
+    # ------------------------------------------------------------------ hip --
+    def _init_hip(self, ring_chunk_bytes: int) -> None:
+        from ..ops.native import require_native
+
+        C = require_native()
+        if not self.layout.fused_ok:
+            raise ValueError(f"model {self.spec} does not fit the fused fp32 step "
+                             f"(LDS {self.layout.lds_floats * 4} B); use the wide bf16 engine")
+        d = self.device
+        self.ws = torch.zeros(self.layout.ws_floats, dtype=torch.float32, device=d)
+        self.slab = torch.zeros(self.layout.slab_floats(), dtype=torch.float32, device=d)
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=d)
+        self.stats = torch.zeros(4, dtype=torch.float32, device=d)
+        self.runner = C.MlpRunner(self.layout.desc_list(), self.X, self.y, self.P, self.G, self.V,
+                                  self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
+                                  self.weight_decay)
+        if self.ctx.is_distributed and self.sync in ("rccl", "ring"):
+            self.comm = make_native_comm(self.ctx)
+            self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
+        self._captured = False
+
+    def _hip_step_torch_sync(self, n: int) -> None:
+        import torch.distributed as dist
+
+        stream = torch.cuda.ExternalStream(self.runner.stream_handle(), device=self.device)
+        for _ in range(n):
+            self.runner.fwd_bwd()
+            with torch.cuda.stream(stream):
+                dist.all_reduce(self.G)
+            self.runner.update()
+
+    # -------------------------------------------------------------- public --
+    def train_steps(self, n: int) -> None:
+        """Enqueue `n` optimizer steps (asynchronous on GPU)."""
+        if n <= 0:
+            return
+        if self.backend == "torch":
+            for _ in range(n):
+                self._torch_step()
+                self.steps_done += 1
+            return
+        if self.ctx.is_distributed and self.sync == "torch":
+            self._hip_step_torch_sync(n)
+        elif self.graph_steps > 0:
+            if not self._captured:
+                self.runner.capture(self.graph_steps, True)
+                self._captured = True
+            reps, rem = divmod(n, self.graph_steps)
+            if reps:
+                self.runner.replay(reps)
+            if rem:
+                self.runner.step(rem)
+        else:
+            self.runner.step(n)
+        self.steps_done += n
+
+    def synchronize(self) -> None:
+        if self.runner is not None:
+            self.runner.synchronize()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
+        if self.backend == "torch":
+            s = StepStats(self._stats_cpu.loss_sum, self._stats_cpu.correct, self._stats_cpu.count)
+            if reset:
+                self._stats_cpu = StepStats()
+        else:
+            self.synchronize()
+            v = self.stats.detach().cpu().tolist()
+            s = StepStats(v[0], v[1], v[2])
+            if reset:
+                self.stats.zero_()
+                torch.cuda.synchronize(self.device)
+        if global_ and self.ctx.is_distributed:
+            s = StepStats(*self.ctx.all_reduce_scalars(s.loss_sum, s.correct, s.count))
+        return s
+
+    @torch.no_grad()
+    def evaluate(self, ds: Dataset) -> Dict[str, float]:
+        X = _pad_cols(ds.X.to(self.device, torch.float32))
+        y = ds.y.to(self.device, torch.int32).contiguous()
+        if self.backend == "torch":
+            logits, _ = forward_ref(self.layout, self.P, X[:, : self.spec.dims[0]])
+            p = torch.softmax(logits, 1)
+            loss = (-torch.log(p.gather(1, y.long().view(-1, 1)).squeeze(1) + 1e-10)).sum().item()
+            correct = (logits.argmax(1) == y.long()).sum().item()
+            n = X.shape[0]
+        else:
+            from ..ops.native import require_native
+
+            C = require_native()
+            n = X.shape[0]
+            ev = MlpLayout(self.spec, n, 1)
+            slab = torch.empty(ev.slab_floats(), dtype=torch.float32, device=self.device)
+            ws = torch.empty(16, dtype=torch.float32, device=self.device)
+            stats = torch.zeros(4, dtype=torch.float32, device=self.device)
+            self.synchronize()
+            C.mlp_eval(ev.desc_list(), X, y, 0, self.P, ws, slab, stats)
+            torch.cuda.synchronize(self.device)
+            loss, correct, _ = stats[:3].tolist()
+        return {"loss": loss / max(n, 1), "accuracy": 100.0 * correct / max(n, 1), "n": n}
+
+    # --------------------------------------------------------------- torch --
+    def _torch_step(self) -> None:
+        b = self.steps_done % self.nbatches
+        r0 = b * self.batch
+        Xb = self.X[r0:r0 + self.batch, : self.spec.dims[0]]
+        yb = self.y[r0:r0 + self.batch]
+        g, loss_sum, correct = grads_ref(self.layout, self.P, Xb, yb)
+        self._stats_cpu.loss_sum += float(loss_sum)
+        self._stats_cpu.correct += float(correct)
+        self._stats_cpu.count += self.batch
+        world = self.ctx.world_size
+        if self.ctx.is_distributed:
+            import torch.distributed as dist
+
+            dist.all_reduce(g)
+        if self.momentum or self.weight_decay:
+            gg = g / world + self.weight_decay * self.P
+            self.V.mul_(self.momentum).add_(gg)
+            self.P.sub_(self.V, alpha=self.lr)
+        else:
+            self.P.sub_(g, alpha=self.lr / world)
+
+    # --------------------------------------------------------- state / ckpt --
+    def state_dict(self) -> Dict[str, object]:
+        self.synchronize()
+        return {"spec": list(self.spec.dims), "params": self.P.detach().cpu().clone(),
+                "velocity": self.V.detach().cpu().clone(), "steps_done": self.steps_done,
+                "lr": self.lr, "batch": self.batch}
+
+    def load_state_dict(self, sd: Dict[str, object]) -> None:
+        if list(sd["spec"]) != list(self.spec.dims):
+            raise ValueError("checkpoint is for a different model")
+        self.synchronize()
+        self.P.copy_(sd["params"].to(self.device))
+        if self.V.numel() and sd["velocity"].numel():
+            self.V.copy_(sd["velocity"].to(self.device))
+        self.steps_done = int(sd["steps_done"])
+        if self.backend == "hip":
+            self.ctr[0] = self.steps_done
+            self.ctr[1] = 0
+            torch.cuda.synchronize(self.device)
+
+    def fit(self, epochs: int, log_fn=None, test: Optional[Dataset] = None) -> Dict[str, float]:
+        """Reference-compatible epoch loop (client.go:579-653 log lines)."""
+        log_fn = log_fn or (lambda s: log.info(s))
+        t0 = time.perf_counter()
+        for ep in range(1, epochs + 1):
+            self.train_steps(self.nbatches)
+            st = self.read_stats(global_=True)
+            log_fn(f"Epoch {ep} complete: Avg Loss: {st.avg_loss:.4f}, Accuracy: {st.accuracy:.2f}%")
+        self.synchronize()
+        wall = time.perf_counter() - t0
+        out = {"wall_s": wall,
+               "samples_per_s": epochs * self.nbatches * self.batch * self.ctx.world_size / wall}
+        if test is not None:
+            ev = self.evaluate(test)
+            out["test_accuracy"] = ev["accuracy"]
+            log_fn(f"Final Test Accuracy: {ev['accuracy']:.2f}%")
+        return out

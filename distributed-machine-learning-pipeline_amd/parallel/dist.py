@@ -1,0 +1,115 @@
+"""Process-group context: one process per GPU, ``torch.distributed`` over RCCL
+(backend ``"nccl"`` is RCCL on ROCm) or gloo on CPU.
+
+The reference has no process group at all: its "ranks" are positions in the
+CommInit address list (``gpu_coordinator_server.go:159``).  Here ranks come from
+the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), and the
+native RCCL communicator (``hipdsml._C.RcclComm``) is bootstrapped by sharing an
+``ncclUniqueId`` through the process group's TCP store.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+    initialized_here: bool = False
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @classmethod
+    def from_env(cls, device: str = "auto", backend: Optional[str] = None,
+                 timeout_s: float = 600.0) -> "DistContext":
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if device == "auto":
+            use_gpu = torch.cuda.is_available()
+        else:
+            use_gpu = device.startswith("cuda")
+        if use_gpu:
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cpu")
+        ctx = cls(rank=rank, world_size=world, local_rank=local, device=dev)
+        if world > 1:
+            be = backend or ("nccl" if use_gpu else "gloo")
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                kw = dict(backend=be, rank=rank, world_size=world,
+                          timeout=datetime.timedelta(seconds=timeout_s))
+                if use_gpu and be == "nccl":
+                    kw["device_id"] = dev
+                dist.init_process_group(**kw)
+                ctx.initialized_here = True
+            ctx.backend = dist.get_backend()
+        return ctx
+
+    # -- collectives on small host/device tensors (outside timed regions) ----
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if not self.is_distributed:
+            return t
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+               "min": dist.ReduceOp.MIN, "prod": dist.ReduceOp.PRODUCT}[op]
+        dist.all_reduce(t, op=rop)
+        return t
+
+    def all_reduce_scalars(self, *vals: float, op: str = "sum") -> list:
+        t = torch.tensor(vals, dtype=torch.float64 if self.device.type == "cpu" else torch.float32,
+                         device=self.device)
+        self.all_reduce_(t, op)
+        return [float(v) for v in t.tolist()]
+
+    def barrier(self) -> None:
+        if self.is_distributed:
+            if self.device.type == "cuda":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def share_bytes(self, key: str, value: Optional[bytes]) -> bytes:
+        """Rank 0 publishes `value` under `key` in the TCP store; every rank reads it."""
+        if not self.is_distributed:
+            assert value is not None
+            return value
+        store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            assert value is not None
+            store.set(key, value)
+        return bytes(store.get(key))
+
+    def destroy(self) -> None:
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+            self.initialized_here = False
+
+
+_uid_counter = 0
+
+
+def make_native_comm(ctx: DistContext, blocking: bool = True):
+    """Bootstrap a native RCCL communicator over the process group's store."""
+    from ..ops.native import require_native
+
+    global _uid_counter
+    C = require_native()
+    _uid_counter += 1
+    key = f"hipdsml/rccl_uid/{_uid_counter}"
+    uid = C.rccl_unique_id() if ctx.rank == 0 else None
+    uid = ctx.share_bytes(key, uid)
+    return C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.local_rank, blocking)
