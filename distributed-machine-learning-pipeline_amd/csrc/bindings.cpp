@@ -45,7 +45,7 @@ void hip_ok(hipError_t e, const char* what) {
 // Flat descriptor list, order fixed by models/mlp.py::MlpLayout.desc_list().
 MlpDesc desc_from_list(const std::vector<int64_t>& v) {
   constexpr size_t kA = kMaxLayers + 1;
-  const size_t want = 4 + 6 * kA + 1 + 2 * kMaxLayers + 2 * kA;
+  const size_t want = 4 + 6 * kA + 1 + 2 * kMaxLayers + 2 * kA + 1;
   TORCH_CHECK(v.size() == want, "MlpDesc list has ", v.size(), " entries, expected ", want);
   MlpDesc d{};
   size_t p = 0;
@@ -64,6 +64,7 @@ MlpDesc desc_from_list(const std::vector<int64_t>& v) {
   for (int i = 0; i < kMaxLayers; ++i) d.b_off[i] = v[p++];
   for (size_t i = 0; i < kA; ++i) d.act_off[i] = v[p++];
   for (size_t i = 0; i < kA; ++i) d.dz_off[i] = v[p++];
+  d.lab_off = v[p++];
   TORCH_CHECK(d.nlayers >= 1 && d.nlayers <= kMaxLayers, "nlayers out of range");
   TORCH_CHECK(d.batch >= 1 && d.nbatches >= 1, "batch / nbatches must be >= 1");
   for (int l = 0; l < d.nlayers; ++l) {
@@ -90,7 +91,7 @@ int64_t layout_ws_end(const MlpDesc& d) {
     end = std::max<int64_t>(end, d.dz_off[l] + (int64_t)d.batch * d.dims[l]);
     if (l < d.nlayers) end = std::max<int64_t>(end, d.act_off[l] + (int64_t)d.batch * d.dims[l]);
   }
-  return end;
+  return std::max<int64_t>(end, d.lab_off + d.batch);
 }
 
 struct PyMlpRunner {
@@ -254,7 +255,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     hip_ok(mlp_read_stamps(v.data()), "mlp_read_stamps");
     return v;
   });
-  m.def("mlp_set_stamping", [](bool on) { mlp_set_stamping(on); });
+  m.def("mlp_set_stamping", [](bool on) { mlp_set_stamping(on); mlp_set_stamping_fast(on); });
+  m.def("mlp_stamps_fast", []() {
+    std::vector<uint64_t> v(kMaxStamps);
+    hip_ok(mlp_read_stamps_fast(v.data()), "mlp_read_stamps_fast");
+    return v;
+  });
   m.def("mlp_plan", [](const std::vector<int64_t>& desc) {
     const MlpDesc d = desc_from_list(desc);
     const MlpLaunchCfg c = mlp_plan_first_layer(d);

@@ -38,6 +38,7 @@ struct MlpDesc {
   int64_t b_off[kMaxLayers];
   int64_t act_off[kMaxLayers + 1];
   int64_t dz_off[kMaxLayers + 1];
+  int64_t lab_off;  // ws offset (in 4-byte words) of the staged labels of the current batch
 };
 
 // ---- fused fp32 MLP step (kernels/mlp_f32.hip) -------------------------------
@@ -54,21 +55,29 @@ bool mlp_rowchain_fits(const MlpDesc& d);
 
 // Forward of layer 1 as a split-K MFMA GEMM into per-split slabs.
 hipError_t mlp_f32_first_layer(const float* X, int64_t ldx, const float* P, float* slab,
-                               const int64_t* ctr, int64_t row0, const MlpDesc& d,
-                               const MlpLaunchCfg& c, hipStream_t s);
+                               int64_t* ctr, int64_t row0, const MlpDesc& d,
+                               const MlpLaunchCfg& c, const int32_t* labels, float* ws,
+                               hipStream_t s);
 // Row-local chain: layer-1 epilogue, layers 2..L forward, softmax-xent,
 // activation gradients down to dZ_1.  train=0 => forward + stats only.
 hipError_t mlp_f32_rowchain(const float* P, const float* slab, int nsplit, float* ws,
                             const int32_t* labels, int64_t* ctr, int64_t row0,
                             const MlpDesc& d, float* stats, int train, float inv_batch,
                             hipStream_t s);
+// Shape-specialised row chain for 3-layer MLPs (mlp_f32_fast.hip); returns
+// hipErrorNotSupported when no instantiation matches.
+hipError_t mlp_f32_rowchain_fast(const float* P, const float* slab, int nsplit, float* ws,
+                                 const int32_t* labels, int64_t* ctr, int64_t row0,
+                                 const MlpDesc& d, float* stats, int train, float inv_batch,
+                                 hipStream_t s);
 // Weight/bias gradients of every layer; fused SGD (P -= lr*g) when fused_sgd,
 // else gradients are written to G.
 //
 // Step counters (no atomics): ctr[0] = A, ctr[1] = B.  Step s starts with
-// A = B = s.  K_A and K_B read B; K_B's block 0 writes A = s + 1; K_C reads
-// A - 1 and its block 0 writes B = A.  No kernel writes a slot it also reads,
-// so there is no intra-launch race and kernel boundaries order the rest.
+// A = B = s.  K_A reads B, and its block 0 writes A = s + 1 and stages the
+// batch's labels at ws + lab_off; K_B needs no counter; K_C reads A - 1 and its
+// block 0 writes B = A.  No kernel writes a slot it also reads, so there is no
+// intra-launch race and kernel boundaries order the rest.
 hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const float* ws,
                          int64_t* ctr, int64_t row0, const MlpDesc& d, float lr, int fused_sgd,
                          hipStream_t s);
@@ -81,6 +90,8 @@ enum ReduceOp : int32_t { kSum = 0, kProd = 1, kMin = 2, kMax = 3 };
 constexpr int kMaxStamps = 32;
 hipError_t mlp_read_stamps(uint64_t* host_out);  // kMaxStamps entries
 void mlp_set_stamping(bool on);
+hipError_t mlp_read_stamps_fast(uint64_t* host_out);
+void mlp_set_stamping_fast(bool on);
 
 hipError_t sgd_update_f32(float* P, const float* G, int64_t n, float scale, hipStream_t s);
 hipError_t sgd_momentum_f32(float* P, const float* G, float* V, int64_t n, float lr,

@@ -38,11 +38,81 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// Full-wave (64-lane) reductions.
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Workgroup barrier that orders LDS traffic only.  __syncthreads() is a
+// workgroup release fence + s_barrier, and on gfx950 hipcc lowers that fence to
+// s_waitcnt vmcnt(0): every barrier would also wait for the global STORES the
+// waves issued before it (a full memory round trip each).  Nothing in the
+// row-chain kernels reads its own global stores back, so LDS ordering is all
+// that is needed.  The asm "memory" clobber keeps the compiler from moving
+// memory operations across it.  Must NOT be used while LDS-DMA
+// (global_load_lds) writes are in flight: those count on vmcnt.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// Barrier that also retires every outstanding vector-memory op (LDS-DMA included).
+__device__ __forceinline__ void full_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// DPP lane permutations (no LDS round trip, unlike __shfl_* = ds_bpermute).
+constexpr int kDppQuadXor1 = 0xB1;      // quad_perm:[1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;      // quad_perm:[2,3,0,1]
+constexpr int kDppRowMirror = 0x140;    // lane i <-> 15-i within a row of 16
+constexpr int kDppRowHalfMirror = 0x141;  // lane i <-> 7-i within a half row
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+// Sum over the 4 lanes of each quad (every lane gets its quad's sum).
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_f<kDppQuadXor1>(v);
+  v += dpp_f<kDppQuadXor2>(v);
   return v;
+}
+// Full-wave (64-lane) sum, wave-uniform result: quad DPP, half-row and row
+// mirrors (row sums), then 4 v_readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v = quad_sum(v);
+  v += dpp_f<kDppRowHalfMirror>(v);
+  v += dpp_f<kDppRowMirror>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+}
+// Sum over each row of 16 lanes (every lane gets its row's sum).
+__device__ __forceinline__ float row16_sum(float v) {
+  v = quad_sum(v);
+  v += dpp_f<kDppRowHalfMirror>(v);
+  v += dpp_f<kDppRowMirror>(v);
+  return v;
+}
+__device__ __forceinline__ void argmax_combine(float& mx, int& amax, float om, int oa) {
+  if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+}
+// (max, first argmax) over each row of 16 lanes.
+__device__ __forceinline__ void row16_argmax(float& mx, int& amax) {
+  argmax_combine(mx, amax, dpp_f<kDppQuadXor1>(mx), dpp_i<kDppQuadXor1>(amax));
+  argmax_combine(mx, amax, dpp_f<kDppQuadXor2>(mx), dpp_i<kDppQuadXor2>(amax));
+  argmax_combine(mx, amax, dpp_f<kDppRowHalfMirror>(mx), dpp_i<kDppRowHalfMirror>(amax));
+  argmax_combine(mx, amax, dpp_f<kDppRowMirror>(mx), dpp_i<kDppRowMirror>(amax));
+}
+// (max, argmax-first) over the 4 lanes of each quad.
+__device__ __forceinline__ void quad_argmax(float& mx, int& amax) {
+  {
+    const float om = dpp_f<kDppQuadXor1>(mx);
+    const int oa = dpp_i<kDppQuadXor1>(amax);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  {
+    const float om = dpp_f<kDppQuadXor2>(mx);
+    const int oa = dpp_i<kDppQuadXor2>(amax);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
 }
 
 }  // namespace dsml

@@ -23,6 +23,8 @@
 // issues ALL of its global loads for a phase before the first dependent use
 // (explicit load batches + sched_barrier), giving one memory round trip per
 // phase instead of one per K-step.
+#include <cstdlib>
+
 #include "common.h"
 #include "../dsml.h"
 
@@ -58,8 +60,8 @@ __device__ int g_dsml_stamp_on;
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mlp_f32_first_layer_k(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ P,
-    float* __restrict__ slab, const int64_t* __restrict__ ctr, int64_t row0, MlpDesc d,
-    int kchunk) {
+    float* __restrict__ slab, int64_t* __restrict__ ctr, int64_t row0, MlpDesc d,
+    int kchunk, const int32_t* __restrict__ labels, float* __restrict__ ws) {
   const int B = d.batch, K = d.dims[0], N = d.dims[1];
   const float* __restrict__ W = P + d.w_off[0];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -82,6 +84,12 @@ __global__ __launch_bounds__(256) void mlp_f32_first_layer_k(
     b[it] = *reinterpret_cast<const float4*>(wb + (kk < ke ? kk : ke - 4));
   }
   const int64_t r0 = ctr ? row_of_step(step, d.nbatches, B) : row0;
+  if (ctr != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+    // Stage this batch's labels for K_B and hand the counter on: A = s + 1.
+    int32_t* lab = reinterpret_cast<int32_t*>(ws + d.lab_off);
+    for (int t = threadIdx.x; t < B; t += 256) lab[t] = labels[r0 + t];
+    if (threadIdx.x == 0) st_ctr(ctr, step + 1);
+  }
   const float* xa = X + (r0 + (mv ? m : B - 1)) * ldx;
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
@@ -157,12 +165,8 @@ __global__ __launch_bounds__(256) void mlp_f32_rowchain_k(
   const int stamp_on = g_dsml_stamp_on;
   DSML_STAMP(0);
 
-  int64_t r0 = row0;
-  if (ctr != nullptr) {
-    const uint64_t s = ld_ctr(ctr + 1);
-    r0 = row_of_step(s, d.nbatches, B);
-    if (blockIdx.x == 0 && tid == 0) st_ctr(ctr, s + 1);  // A = s + 1 (nobody reads A here)
-  }
+  // Labels: staged by K_A for training steps (ctr != nullptr), direct for eval.
+  const int32_t* lab = ctr ? reinterpret_cast<const int32_t*>(ws + d.lab_off) : labels + row0;
   // ---- phase 1a: stage weights of layers 2..L into LDS ----------------------
   if constexpr (WLDS) {
     for (int l = 2; l <= L; ++l) {
@@ -279,23 +283,17 @@ __global__ __launch_bounds__(256) void mlp_f32_rowchain_k(
       const int r = lane >> 2, sub = lane & 3;
       const int m = m0 + r;
       const bool valid = m < B;
-      const int y = valid ? labels[r0 + m] : -1;
+      const int y = valid ? lab[m] : -1;
       float mx = -3.402823466e38f;
       int amax = 0x7fffffff;
       for (int c = sub; c < C; c += 4) {
         const float z = Z[r * sL + c];
         if (z > mx) { mx = z; amax = c; }
       }
-#pragma unroll
-      for (int o = 1; o < 4; o <<= 1) {
-        const float om = __shfl_xor(mx, o, 64);
-        const int oa = __shfl_xor(amax, o, 64);
-        if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
-      }
+      quad_argmax(mx, amax);
       float se = 0.f;
       for (int c = sub; c < C; c += 4) se += expf(Z[r * sL + c] - mx);
-#pragma unroll
-      for (int o = 1; o < 4; o <<= 1) se += __shfl_xor(se, o, 64);
+      se = quad_sum(se);
       const float inv = 1.f / se;
       float loss = 0.f;
       for (int c = sub; c < Cp; c += 4) {
@@ -410,6 +408,20 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     lda = K;
   }
 
+  // Fused SGD reads the old weights: issue those loads with the operand batch.
+  float wold[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  float bold = 0.f;
+  const int64_t woff = d.w_off[l];
+  if (fused_sgd) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = tn * 16 + 4 * q + r;
+      const float* wr = P + woff + (int64_t)(row < N ? row : N - 1) * K;
+      wold[r][0] = wr[k0c];
+      wold[r][1] = wr[k1c];
+    }
+    bold = P[d.b_off[l] + nc];
+  }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   for (int mb = 0; mb < B; mb += 64) {
@@ -438,15 +450,14 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
   dbacc += __shfl_xor(dbacc, 32, 64);
 
   float* Wt = fused_sgd ? P : Gout;
-  const int64_t woff = d.w_off[l];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = tn * 16 + 4 * q + r;
     if (row < N) {
       float* wr = Wt + woff + (int64_t)row * K;
       if (fused_sgd) {
-        if (k0v) wr[k0] -= lr * acc0[r];
-        if (k1v) wr[k1] -= lr * acc1[r];
+        if (k0v) wr[k0] = wold[r][0] - lr * acc0[r];
+        if (k1v) wr[k1] = wold[r][1] - lr * acc1[r];
       } else {
         if (k0v) wr[k0] = acc0[r];
         if (k1v) wr[k1] = acc1[r];
@@ -455,7 +466,7 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
   }
   if (tk == 0 && q == 0 && nv) {
     float* bp = Wt + d.b_off[l] + n;
-    if (fused_sgd) *bp -= lr * dbacc;
+    if (fused_sgd) *bp = bold - lr * dbacc;
     else *bp = dbacc;
   }
   // Step-counter hand-off: B = A (K_C never reads B; A is not written here).
@@ -473,6 +484,7 @@ MlpLaunchCfg mlp_plan_first_layer(const MlpDesc& d) {
   const int want = (64 + tiles - 1) / tiles;
   const int minsplit = (kblocks + 7) / 8;
   int nsplit = want > minsplit ? want : minsplit;
+  if (nsplit > 8 && minsplit <= 8) nsplit = 8;  // the row chain sums <= 8 slabs
   if (nsplit > kblocks) nsplit = kblocks;
   const int per = (kblocks + nsplit - 1) / nsplit;
   MlpLaunchCfg c;
@@ -490,11 +502,12 @@ int mlp_wgrad_tiles(const MlpDesc& d) {
 bool mlp_rowchain_fits(const MlpDesc& d) { return d.lds_floats * 4 <= 160 * 1024; }
 
 hipError_t mlp_f32_first_layer(const float* X, int64_t ldx, const float* P, float* slab,
-                               const int64_t* ctr, int64_t row0, const MlpDesc& d,
-                               const MlpLaunchCfg& c, hipStream_t s) {
+                               int64_t* ctr, int64_t row0, const MlpDesc& d,
+                               const MlpLaunchCfg& c, const int32_t* labels, float* ws,
+                               hipStream_t s) {
   dim3 grid((d.dims[1] + 31) / 32, (d.batch + 31) / 32, c.nsplit);
   hipLaunchKernelGGL(mlp_f32_first_layer_k, grid, dim3(256), 0, s, X, ldx, P, slab, ctr, row0,
-                     d, c.kchunk);
+                     d, c.kchunk, labels, ws);
   return hipGetLastError();
 }
 
@@ -503,6 +516,12 @@ hipError_t mlp_f32_rowchain(const float* P, const float* slab, int nsplit, float
                             const MlpDesc& d, float* stats, int train, float inv_batch,
                             hipStream_t s) {
   if (nsplit < 1 || nsplit > 8) return hipErrorInvalidValue;
+  static const bool no_fast = getenv("HIPDSML_NO_FAST") != nullptr;
+  if (!no_fast) {
+    const hipError_t e = mlp_f32_rowchain_fast(P, slab, nsplit, ws, labels, ctr, row0, d, stats,
+                                               train, inv_batch, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   dim3 grid((d.batch + kRowTile - 1) / kRowTile);
   const size_t lds = (size_t)d.lds_floats * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

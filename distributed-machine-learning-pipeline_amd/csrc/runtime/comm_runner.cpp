@@ -237,7 +237,7 @@ void MlpRunner::set_lr(float lr) {
 }
 
 void MlpRunner::enqueue_fwd_bwd(hipStream_t s) {
-  DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, s));
+  DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, b_.labels, b_.ws, s));
   DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
                                   b_.stats, 1, 1.0f / (float)d_.batch, s));
   DSML_HIP_CHECK(mlp_f32_wgrad(b_.X, b_.ldx, b_.P, b_.G, b_.ws, b_.ctr, 0, d_, lr_, 0, s));
@@ -257,7 +257,7 @@ void MlpRunner::enqueue_step(hipStream_t s) {
   const bool plain = mom_ == 0.f && wd_ == 0.f;
   if (!multi && plain) {
     // Single replica, plain SGD: the update is fused into the weight-grad kernel.
-    DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, s));
+    DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, b_.labels, b_.ws, s));
     DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
                                     b_.stats, 1, 1.0f / (float)d_.batch, s));
     DSML_HIP_CHECK(mlp_f32_wgrad(b_.X, b_.ldx, b_.P, b_.G, b_.ws, b_.ctr, 0, d_, lr_, 1, s));
@@ -299,7 +299,7 @@ void MlpRunner::replay(hipStream_t s) {
 void mlp_eval(const MlpDesc& d, const float* X, int64_t ldx, const int32_t* labels, int64_t row0,
               const float* P, float* ws, float* slab, float* stats, hipStream_t s) {
   const MlpLaunchCfg c = mlp_plan_first_layer(d);
-  DSML_HIP_CHECK(mlp_f32_first_layer(X, ldx, P, slab, nullptr, row0, d, c, s));
+  DSML_HIP_CHECK(mlp_f32_first_layer(X, ldx, P, slab, nullptr, row0, d, c, labels, ws, s));
   DSML_HIP_CHECK(
       mlp_f32_rowchain(P, slab, c.nsplit, ws, labels, nullptr, row0, d, stats, 0, 1.0f, s));
 }

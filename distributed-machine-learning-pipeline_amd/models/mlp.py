@@ -84,6 +84,7 @@ class MlpLayout:
     lds_b: List[int] = field(default_factory=list)
     lds_floats: int = 0
     w_in_lds: int = 1
+    lab_off: int = 0
 
     def __post_init__(self):
         d = self.spec.dims
@@ -106,6 +107,8 @@ class MlpLayout:
                 off = _rup(off + self.batch * d[l], 16)
             self.dz_off[l] = off
             off = _rup(off + self.batch * d[l], 16)
+        self.lab_off = off  # staged int32 labels of the current batch
+        off = _rup(off + self.batch, 16)
         self.ws_floats = max(off, 16)
         # LDS of the row-chain kernel (floats, 16 B aligned)
         self.lds_act = [0] * (MAX_LAYERS + 1)
@@ -146,6 +149,7 @@ class MlpLayout:
         out += [self.lds_floats]
         out += pad(self.w_off, MAX_LAYERS) + pad(self.b_off, MAX_LAYERS)
         out += pad(self.act_off, A) + pad(self.dz_off, A)
+        out += [self.lab_off]
         return [int(x) for x in out]
 
     @property
@@ -163,7 +167,10 @@ class MlpLayout:
         kblocks = (self.spec.dims[0] + 15) // 16
         tiles = ((self.spec.dims[1] + 31) // 32) * ((self.batch + 31) // 32)
         want = (64 + tiles - 1) // tiles
-        nsplit = max(want, (kblocks + 7) // 8)
+        minsplit = (kblocks + 7) // 8
+        nsplit = max(want, minsplit)
+        if nsplit > 8 and minsplit <= 8:
+            nsplit = 8
         nsplit = min(nsplit, kblocks)
         per = (kblocks + nsplit - 1) // nsplit
         nsplit = (kblocks + per - 1) // per

@@ -49,6 +49,9 @@ def test_native_loaded():
     ((784, 128, 64, 10), 50),     # partial row tiles
     ((784, 128, 64, 10), 128),
     ((64, 32, 10), 32),
+    ((784, 256, 128, 10), 64),   # specialised row chain <256,128,10>
+    ((784, 128, 128, 10), 48),   # specialised row chain <128,128,10>, partial tile
+    ((784, 96, 48, 10), 64),     # generic row chain, 3 layers
 ])
 def test_fused_step_matches_reference(dims, batch):
     spec = MlpSpec(dims)
