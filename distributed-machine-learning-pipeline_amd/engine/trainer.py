@@ -58,7 +58,7 @@ class MlpTrainer:
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "reference",
                  momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
                  ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
-                 params: Optional[torch.Tensor] = None):
+                 params: Optional[torch.Tensor] = None, external_comm=None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -86,7 +86,7 @@ class MlpTrainer:
         self.V = torch.zeros_like(self.P) if (momentum or weight_decay) else torch.empty(0, device=self.device)
         self.steps_done = 0
         self._stats_cpu = StepStats()
-        self.comm = None
+        self.comm = external_comm
         self.runner = None
         if self.device.type == "cuda":
             self._init_hip(ring_chunk_bytes)
@@ -111,7 +111,8 @@ class MlpTrainer:
                                   self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
                                   self.weight_decay)
         if self.ctx.is_distributed and self.sync in ("rccl", "ring"):
-            self.comm = make_native_comm(self.ctx)
+            if self.comm is None:
+                self.comm = make_native_comm(self.ctx)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
         self._captured = False
 
@@ -196,6 +197,41 @@ class MlpTrainer:
             torch.cuda.synchronize(self.device)
             loss, correct, _ = stats[:3].tolist()
         return {"loss": loss / max(n, 1), "accuracy": 100.0 * correct / max(n, 1), "n": n}
+
+    # ------------------------------------------------- per-batch RPC helpers --
+    def batch_gradients(self, X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Flat gradient (param layout) of one batch at the current params —
+        the RunBackward RPC.  GPU: the fused HIP kernels on a one-batch plan."""
+        rows = X.shape[0]
+        if self.backend == "torch":
+            g, _, _ = grads_ref(self.layout, self.P, X.to(self.P.device), y.to(self.P.device))
+            return g
+        from ..ops.native import require_native
+
+        C = require_native()
+        lay = MlpLayout(self.spec, rows, 1)
+        Xd = _pad_cols(X.to(self.device, torch.float32))
+        yd = y.to(self.device, torch.int32).contiguous()
+        G = torch.zeros_like(self.P)
+        ws = torch.zeros(lay.ws_floats, dtype=torch.float32, device=self.device)
+        slab = torch.zeros(lay.slab_floats(), dtype=torch.float32, device=self.device)
+        ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        stats = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.synchronize()
+        r = C.MlpRunner(lay.desc_list(), Xd, yd, self.P, G, torch.empty(0, device=self.device),
+                        ws, slab, ctr, stats, self.lr, 0.0, 0.0)
+        r.fwd_bwd()
+        r.synchronize()
+        return G
+
+    def apply_gradients(self, g: torch.Tensor, scale: float = 1.0) -> None:
+        """P -= lr * scale * g (the ApplyGradients RPC; HIP kernel on GPU)."""
+        from ..ops.functional import sgd_update_
+
+        self.synchronize()
+        sgd_update_(self.P, g.to(self.P.device).contiguous(), self.lr * scale)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     # --------------------------------------------------------------- torch --
     def _torch_step(self) -> None:

@@ -1,0 +1,381 @@
+"""GPUDevice servicer: one process (or in-process server) per GPU.
+
+MI355X-native replacement of ``DSML/gpu_device_service/gpu_device_server.go``:
+the memory is a real HBM arena (HipDevice) or a host buffer (HostDevice, for
+the CPU plumbing config), transfers between devices are pushed by the sending
+device itself (BeginSend with ``dstAddress``), reductions run on the device
+(HIP kernels), and the extension RPCs let the coordinator bootstrap an RCCL
+communicator and run collectives / whole training steps on the GPU.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from typing import Dict, Optional
+
+import grpc
+import torch
+
+from ..runtime.device import (DT_SIZE, STATUS_FAILED, STATUS_SUCCESS, TORCH_DTYPES, OutOfRange,
+                              _Device, make_device)
+from .proto import pb
+from .stubs import GPUDeviceStub, connect, serve
+
+log = logging.getLogger("hipdsml.device")
+
+CHUNK = 1 << 20  # StreamSend chunk size
+
+
+class GPUDeviceServicer:
+    def __init__(self, device: _Device, name: str = ""):
+        self.dev = device
+        self.name = name or f"device-{device.device_id}"
+        self.comms: Dict[int, object] = {}      # commId -> native RcclComm
+        self.comm_meta: Dict[int, dict] = {}    # commId -> {"rank", "nranks", "peers"}
+        self._peer_stubs: Dict[str, GPUDeviceStub] = {}
+        self._lock = threading.Lock()
+        self.trainer = None
+        self._fwd_cache = None
+        self.counters = {"h2d_bytes": 0, "d2h_bytes": 0, "stream_bytes_in": 0,
+                         "stream_bytes_out": 0, "reduces": 0, "allreduces": 0, "train_steps": 0}
+
+    # ------------------------------------------------------------ helpers --
+    def _peer(self, address: str) -> GPUDeviceStub:
+        with self._lock:
+            s = self._peer_stubs.get(address)
+            if s is None:
+                s = GPUDeviceStub(connect(address))
+                self._peer_stubs[address] = s
+            return s
+
+    def _push(self, sid: int, send_addr: int, n: int, address: str) -> None:
+        """Background device->device transfer of a BeginSend'd buffer."""
+        try:
+            data = self.dev.read(send_addr, n, internal=True)
+
+            def chunks():
+                if n == 0:
+                    yield pb.DataChunk(data=b"", streamId=sid)
+                for off in range(0, n, CHUNK):
+                    yield pb.DataChunk(data=data[off:off + CHUNK], streamId=sid)
+
+            resp = self._peer(address).StreamSend(chunks(), timeout=120)
+            self.counters["stream_bytes_out"] += n
+            self.dev.set_status(sid, STATUS_SUCCESS if resp.success else STATUS_FAILED)
+        except Exception as e:  # peer died / transport error
+            log.warning("stream %d push to %s failed: %s", sid, address, e)
+            self.dev.set_status(sid, STATUS_FAILED)
+
+    # ---------------------------------------------------------- reference API --
+    def GetDeviceMetadata(self, request, context):
+        md = pb.DeviceMetadata(deviceId=pb.DeviceId(value=self.dev.device_id),
+                               minMemAddr=pb.MemAddr(value=self.dev.min_addr),
+                               maxMemAddr=pb.MemAddr(value=self.dev.max_addr),
+                               name=self.name, backend=self.dev.backend)
+        return pb.GetDeviceMetadataResponse(metadata=md)
+
+    def BeginSend(self, request, context):
+        addr, n = request.sendBuffAddr.value, request.numBytes
+        sid = self.dev.begin_send(addr, n, request.dstRank.value)
+        if request.dstAddress:
+            try:
+                self.dev.check(addr, n, internal=True)
+            except OutOfRange as e:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            threading.Thread(target=self._push, args=(sid, addr, n, request.dstAddress),
+                             daemon=True).start()
+        return pb.BeginSendResponse(initiated=True, streamId=pb.StreamId(value=sid))
+
+    def BeginReceive(self, request, context):
+        sid = request.streamId.value
+        own = (sid >> 32) == self.dev.device_id
+        if own and self.dev.stream(sid) is None:
+            context.abort(grpc.StatusCode.NOT_FOUND, f"stream ID {sid} not found")
+        try:
+            self.dev.begin_receive(sid, request.recvBuffAddr.value, request.numBytes,
+                                   request.srcRank.value, create=True)
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        return pb.BeginReceiveResponse(initiated=True)
+
+    def StreamSend(self, request_iterator, context):
+        first = next(request_iterator, None)
+        if first is None or first.streamId == 0:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, "stream ID not provided")
+        sid = first.streamId
+        nbytes = [0]
+
+        def gen():
+            nbytes[0] += len(first.data)
+            yield first.data
+            for c in request_iterator:
+                nbytes[0] += len(c.data)
+                yield c.data
+
+        ok = self.dev.receive_chunks(sid, gen())
+        self.counters["stream_bytes_in"] += nbytes[0]
+        return pb.StreamSendResponse(success=ok)
+
+    def GetStreamStatus(self, request, context):
+        return pb.GetStreamStatusResponse(status=self.dev.stream_status(request.streamId.value))
+
+    def Memcpy(self, request, context):
+        which = request.WhichOneof("either")
+        if which == "hostToDevice":
+            r = request.hostToDevice
+            try:
+                self.dev.write(r.dstMemAddr.value, r.hostSrcData)
+            except OutOfRange as e:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            self.counters["h2d_bytes"] += len(r.hostSrcData)
+            return pb.MemcpyResponse(hostToDevice=pb.MemcpyHostToDeviceResponse(success=True))
+        if which == "deviceToHost":
+            r = request.deviceToHost
+            addr = r.srcMemAddr.value
+            n = r.numBytes or self.dev.extent(addr)
+            if n == 0:
+                if not self.dev.in_range(addr):
+                    context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"memory address {addr:#x} out of range")
+                context.abort(grpc.StatusCode.INTERNAL, f"no data found at memory address {addr:#x}")
+            try:
+                data = self.dev.read(addr, n)
+            except OutOfRange as e:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            self.counters["d2h_bytes"] += n
+            return pb.MemcpyResponse(deviceToHost=pb.MemcpyDeviceToHostResponse(dstData=data))
+        context.abort(grpc.StatusCode.INVALID_ARGUMENT, "invalid Memcpy request")
+
+    # ---------------------------------------------------------- collectives --
+    def Reduce(self, request, context):
+        try:
+            self.dev.reduce(request.dstAddr, request.srcAddr, request.numBytes, request.dtype, request.op)
+            if request.scale not in (0.0, 1.0):
+                self.dev.scale(request.dstAddr, request.numBytes, request.dtype, request.scale)
+            self.dev.synchronize()
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        except ValueError as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        self.counters["reduces"] += 1
+        return pb.ReduceResponse(success=True)
+
+    def GetCommUniqueId(self, request, context):
+        if self.dev.backend != "hip":
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, "RCCL needs a GPU device")
+        from ..ops.native import require_native
+
+        return pb.GetCommUniqueIdResponse(uniqueId=require_native().rccl_unique_id())
+
+    def CommSetup(self, request, context):
+        cid = request.commId
+        meta = {"rank": request.rank, "nranks": request.nranks, "peers": list(request.peerAddresses)}
+        backend = "rpc"
+        if request.uniqueId:
+            if self.dev.backend != "hip":
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION, "RCCL needs a GPU device")
+            from ..ops.native import require_native
+
+            C = require_native()
+            try:
+                comm = C.RcclComm(request.uniqueId, request.rank, request.nranks, self.dev.gpu, True)
+            except Exception as e:  # init failure (peer died during bootstrap)
+                context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
+            self.comms[cid] = comm
+            backend = "rccl"
+        self.comm_meta[cid] = meta
+        return pb.CommSetupResponse(success=True, backend=backend)
+
+    def DeviceAllReduce(self, request, context):
+        comm = self.comms.get(request.commId)
+        if comm is None:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"no RCCL communicator for comm {request.commId}")
+        if comm.aborted:
+            context.abort(grpc.StatusCode.ABORTED, "communicator aborted")
+        es = DT_SIZE[request.dtype]
+        if request.count % es:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, "count is not a multiple of the element size")
+        try:
+            t = self.dev.tensor(request.addr, request.count, TORCH_DTYPES[request.dtype], internal=False)
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        algo = request.algo or "ring"
+        reps = max(1, request.repeat)
+        chunk = request.chunkBytes or (1 << 20)
+        torch.cuda.synchronize(self.dev.gpu)
+        t0 = time.perf_counter()
+        try:
+            with torch.cuda.device(self.dev.gpu):
+                for _ in range(reps):
+                    if algo == "rccl":
+                        comm.allreduce_(t, request.op)
+                    else:
+                        comm.ring_allreduce_(t, request.op, chunk)
+                torch.cuda.synchronize(self.dev.gpu)
+        except Exception as e:
+            context.abort(grpc.StatusCode.INTERNAL, f"all-reduce failed: {e}")
+        us = (time.perf_counter() - t0) * 1e6 / reps
+        self.counters["allreduces"] += reps
+        return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
+
+    def Abort(self, request, context):
+        ids = [request.commId] if request.commId in self.comms else list(self.comms)
+        for cid in ids:
+            try:
+                self.comms[cid].abort()
+            except Exception:  # pragma: no cover
+                pass
+        log.warning("%s: abort comm(s) %s: %s", self.name, ids, request.reason)
+        return pb.AbortResponse(success=True)
+
+    def CommTeardown(self, request, context):
+        self.comms.pop(request.commId, None)
+        self.comm_meta.pop(request.commId, None)
+        return pb.CommTeardownResponse(success=True)
+
+    # -------------------------------------------------------------- training --
+    def _torch_device(self) -> torch.device:
+        return torch.device("cuda", self.dev.gpu) if self.dev.backend == "hip" else torch.device("cpu")
+
+    def ConfigureModel(self, request, context):
+        from ..data.mnist import load_mnist, mnist_available, synthetic_mnist
+        from ..engine.trainer import MlpTrainer
+        from ..models.mlp import MlpLayout, MlpSpec
+        from ..parallel.dist import DistContext
+
+        try:
+            spec = MlpSpec(tuple(request.dims) or (784, 128, 64, 10))
+        except ValueError as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        batch = request.batch or 64
+        world = max(1, request.worldSize)
+        rank = request.rank
+        n = request.numSamples or 60032
+        if request.dataset in ("", "synthetic"):
+            ds = synthetic_mnist(n, seed=request.dataSeed + rank, dim=spec.dims[0])
+        elif request.dataset.startswith("mnist") and mnist_available():
+            ds = load_mnist(split="t10k").shard(rank, world)
+        else:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"dataset {request.dataset!r} unavailable")
+        layout = MlpLayout(spec, batch, max(1, len(ds) // batch))
+        params = None
+        if request.weightsAddr:
+            nb = spec.num_params * 4
+            raw = self.dev.read(request.weightsAddr, nb)
+            import numpy as np
+
+            params = layout.from_reference(np.frombuffer(raw, dtype=np.float32))
+        ctx = DistContext(rank=rank, world_size=world, device=self._torch_device())
+        comm = self.comms.get(request.commId) if world > 1 else None
+        if world > 1 and comm is None and self.dev.backend == "hip":
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                          "data-parallel TrainSteps needs an RCCL comm (CommInit backend=rccl)")
+        try:
+            self.trainer = MlpTrainer(spec, ds, batch=batch, lr=request.lr or 0.01, ctx=ctx,
+                                      seed=request.seed, momentum=request.momentum,
+                                      graph_steps=request.graphSteps, params=params,
+                                      external_comm=comm, sync=request.sync or "rccl")
+        except (ValueError, RuntimeError) as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        return pb.ConfigureModelResponse(success=True, numParams=spec.num_params,
+                                         batchesPerEpoch=self.trainer.nbatches,
+                                         paramBytes=layout.nparams * 4)
+
+    def _need_trainer(self, context):
+        if self.trainer is None:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, "ConfigureModel first")
+        return self.trainer
+
+    def TrainSteps(self, request, context):
+        tr = self._need_trainer(context)
+        if tr.backend == "torch" and tr.ctx.world_size > 1:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                          "host devices train data-parallel through the RPC ring (client rpc mode)")
+        t0 = time.perf_counter()
+        try:
+            tr.train_steps(int(request.steps))
+            tr.synchronize()
+        except Exception as e:
+            context.abort(grpc.StatusCode.INTERNAL, f"train step failed: {e}")
+        us = (time.perf_counter() - t0) * 1e6
+        st = tr.read_stats()
+        self.counters["train_steps"] += int(request.steps)
+        return pb.TrainStepsResponse(success=True, lossSum=st.loss_sum, correct=st.correct,
+                                     count=st.count, elapsedUs=us, stepsDone=tr.steps_done)
+
+    def Evaluate(self, request, context):
+        from ..data.mnist import load_mnist, mnist_available, synthetic_mnist
+
+        tr = self._need_trainer(context)
+        if request.dataset.startswith("mnist") and mnist_available():
+            ds = load_mnist(split="t10k", limit=request.numSamples or None)
+        else:
+            ds = synthetic_mnist(request.numSamples or 10000, seed=request.seed or 777,
+                                 dim=tr.spec.dims[0])
+        ev = tr.evaluate(ds)
+        return pb.EvaluateResponse(success=True, accuracy=ev["accuracy"], loss=ev["loss"], count=ev["n"])
+
+    def RunForward(self, request, context):
+        from ..models.mlp import forward_ref, loss_and_dlogits_ref
+
+        tr = self._need_trainer(context)
+        rows = request.numRows or tr.batch
+        d0 = tr.spec.dims[0]
+        try:
+            X = self.dev.tensor(request.inputAddr, rows * d0 * 4, torch.float32).view(rows, d0)
+            y = (self.dev.tensor(request.labelsAddr, rows * 4, torch.int32)
+                 if request.labelsAddr else None)
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        X = X.clone()
+        y = y.clone() if y is not None else None
+        logits, _ = forward_ref(tr.layout, tr.P, X)
+        loss = correct = 0.0
+        if y is not None:
+            loss_sum, _, corr = loss_and_dlogits_ref(logits, y)
+            loss, correct = float(loss_sum) / rows, int(corr)
+        if request.outputAddr:
+            self.dev.write(request.outputAddr, logits.detach().float().cpu().numpy().tobytes(),
+                           internal=True)
+        self._fwd_cache = (X, y)
+        return pb.RunForwardResponse(success=True, loss=loss, correct=int(correct))
+
+    def RunBackward(self, request, context):
+        tr = self._need_trainer(context)
+        if self._fwd_cache is None or self._fwd_cache[1] is None:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, "RunForward with labels first")
+        X, y = self._fwd_cache
+        g = tr.batch_gradients(X, y)
+        data = g.detach().float().cpu().numpy().tobytes()
+        try:
+            self.dev.write(request.gradientAddr, data, internal=True)
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        return pb.RunBackwardResponse(success=True, numBytes=len(data))
+
+    def ApplyGradients(self, request, context):
+        tr = self._need_trainer(context)
+        nb = tr.layout.nparams * 4
+        try:
+            g = self.dev.tensor(request.gradientAddr, nb, torch.float32).to(tr.device)
+        except OutOfRange as e:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        tr.apply_gradients(g, request.scale or 1.0)
+        return pb.ApplyGradientsResponse(success=True)
+
+    def GetStats(self, request, context):
+        d = dict(self.counters)
+        d.update({"device_id": self.dev.device_id, "backend": self.dev.backend,
+                  "comms": sorted(self.comms), "steps_done": getattr(self.trainer, "steps_done", 0)})
+        return pb.GetStatsResponse(json=json.dumps(d))
+
+
+def start_device_server(device_id: int, mem_size: int, address: str = "127.0.0.1:0",
+                        backend: str = "auto", gpu: int = 0, max_workers: int = 32):
+    """Start one device server; returns (grpc_server, address, servicer)."""
+    dev = make_device(device_id, mem_size, backend, gpu=gpu)
+    svc = GPUDeviceServicer(dev)
+    server, addr = serve("GPUDevice", svc, address, max_workers=max_workers)
+    log.info("GPU Device server listening on %s with device ID %d (%s)", addr, device_id, dev.backend)
+    return server, addr, svc
