@@ -1,0 +1,165 @@
+"""All-reduce benchmarks (second half of the BASELINE headline metric:
+"ring-AllReduce latency (ms) at 1 MiB").
+
+``rpc``    — the reference experiment's shape (allreduce_comparison_test.go:32-133):
+             n device servers + coordinator, NaiveAllReduce(1 MiB, latencyMs=10)
+             vs AllReduceRing(1 MiB), through the gpu_sim API.  Reported both
+             "as published" (ring on count = dataSize/4 bytes, uint8, like the
+             reference) and apples-to-apples (ring on the full 1 MiB, fp32).
+``device`` — one process per GPU (torchrun): the native ring (ncclSend/ncclRecv
+             reduce-scatter + all-gather with HIP reduce kernels) and RCCL's own
+             all-reduce on device buffers, latency (us) and bus bandwidth
+             (2(n-1)/n * bytes / t) over a size sweep.
+
+Prints one JSON line per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+
+def _spawn_cluster(a):
+    """Device servers + coordinator as separate OS processes (the reference's
+    deployment shape: cmd/gpu_device_server + cmd/gpu_coordinator_server)."""
+    import subprocess
+
+    from ..cli import _wait_port, child_env
+
+    procs, addrs = [], []
+    for i in range(a.n):
+        port = a.base_port + i
+        addrs.append(f"127.0.0.1:{port}")
+        procs.append(subprocess.Popen([sys.executable, "-m", "hipdsml", "device-server", "--ports", str(port),
+                                       "--device-ids", str(i + 1), "--backend", a.backend,
+                                       "--mem-size", str(a.mem_size)], env=child_env(),
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+    caddr = f"127.0.0.1:{a.base_port + 100}"
+    procs.append(subprocess.Popen([sys.executable, "-m", "hipdsml", "coordinator", "--port",
+                                   str(a.base_port + 100), "--health-interval", "0"], env=child_env(),
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+    for ad in addrs + [caddr]:
+        _wait_port(ad)
+    return procs, addrs, caddr
+
+
+def bench_rpc(a) -> None:
+    import numpy as np
+
+    from ..rpc.coordinator import start_coordinator
+    from ..rpc.device_server import start_device_server
+    from ..rpc.proto import DT_FLOAT32, DT_UINT8, pb
+    from ..rpc.stubs import GPUCoordinatorStub, connect
+
+    procs, servers = [], []
+    if a.inproc:
+        servers = [start_device_server(i + 1, a.mem_size, backend=a.backend) for i in range(a.n)]
+        cserver, caddr, csvc = start_coordinator(health_interval=0)
+        addrs = [s[1] for s in servers]
+    else:
+        procs, addrs, caddr = _spawn_cluster(a)
+    coord = GPUCoordinatorStub(connect(caddr, timeout=30))
+    try:
+        init = coord.CommInit(pb.CommInitRequest(numDevices=a.n, device_addresses=addrs))
+        cid = init.commId
+        backend = init.devices[0].backend
+        size = a.size
+        naive = []
+        for _ in range(a.reps):
+            r = coord.NaiveAllReduce(pb.NaiveAllReduceRequest(commId=cid, dataSize=size, latencyMs=a.latency_ms))
+            naive.append(r.totalTimeUs / 1e3)
+        rng = np.random.default_rng(0)
+        for d in init.devices:
+            coord.Memcpy(pb.MemcpyRequest(hostToDevice=pb.MemcpyHostToDeviceRequest(
+                hostSrcData=rng.standard_normal(size // 4).astype(np.float32).tobytes(),
+                dstDeviceId=d.deviceId, dstMemAddr=pb.MemAddr(value=0x1000))))
+        res = {}
+        for label, count, dt in (("ring_as_published", size // 4, DT_UINT8), ("ring_full_fp32", size, DT_FLOAT32)):
+            ts = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                coord.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=count, dtype=dt))
+                ts.append((time.perf_counter() - t0) * 1e3)
+            res[label] = ts
+        out = {"bench": "allreduce_rpc", "n_devices": a.n, "backend": backend,
+               "processes": "in-process" if a.inproc else "one per server",
+               "data_bytes": size, "latency_ms_injected": a.latency_ms,
+               "naive_ms_median": round(statistics.median(naive), 3),
+               "ring_as_published_ms_median": round(statistics.median(res["ring_as_published"]), 3),
+               "ring_full_fp32_ms_median": round(statistics.median(res["ring_full_fp32"]), 3),
+               "reference": {"naive_ms": 83, "ring_ms": 8}}
+        print(json.dumps(out), flush=True)
+    finally:
+        if a.inproc:
+            csvc.stop()
+            cserver.stop(0)
+            for s in servers:
+                s[0].stop(0)
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.wait(timeout=30)
+
+
+def bench_device(a) -> None:
+    import torch
+
+    from ..parallel.dist import DistContext, make_native_comm
+
+    ctx = DistContext.from_env(device="cuda")
+    comm = make_native_comm(ctx)
+    n = ctx.world_size
+    sizes = [int(s) for s in a.sizes.split(",")]
+    for nbytes in sizes:
+        t = torch.ones(nbytes // 4, dtype=torch.float32, device=ctx.device)
+        for algo in a.algos.split(","):
+            fn = (lambda: comm.allreduce_(t, 0)) if algo == "rccl" else (
+                lambda: comm.ring_allreduce_(t, 0, a.chunk_bytes))
+            for _ in range(a.warmup):
+                fn()
+            torch.cuda.synchronize()
+            ctx.barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                fn()
+            torch.cuda.synchronize()
+            us = (time.perf_counter() - t0) * 1e6 / a.iters
+            us = ctx.all_reduce_scalars(us, op="max")[0] if ctx.is_distributed else us
+            if ctx.rank == 0:
+                busbw = (2 * (n - 1) / n * nbytes / (us * 1e-6) / 1e9) if n > 1 else 0.0
+                print(json.dumps({"bench": "allreduce_device", "algo": algo, "n_gpus": n, "bytes": nbytes,
+                                  "us": round(us, 2), "ms": round(us / 1e3, 4),
+                                  "busbw_GBps": round(busbw, 2)}), flush=True)
+    ctx.destroy()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="hipdsml bench-allreduce")
+    sub = ap.add_subparsers(dest="mode", required=True)
+    r = sub.add_parser("rpc")
+    r.add_argument("--n", type=int, default=3)
+    r.add_argument("--size", type=int, default=1 << 20)
+    r.add_argument("--latency-ms", type=int, default=10)
+    r.add_argument("--reps", type=int, default=5)
+    r.add_argument("--backend", default="host", choices=["host", "hip", "auto"])
+    r.add_argument("--mem-size", type=int, default=8 << 20)
+    r.add_argument("--base-port", type=int, default=6103)
+    r.add_argument("--inproc", action="store_true", help="all servers in this process (GIL-bound)")
+    d = sub.add_parser("device")
+    d.add_argument("--sizes", default="4096,65536,1048576,16777216,67108864")
+    d.add_argument("--algos", default="ring,rccl")
+    d.add_argument("--chunk-bytes", type=int, default=4 << 20)
+    d.add_argument("--iters", type=int, default=50)
+    d.add_argument("--warmup", type=int, default=10)
+    a = ap.parse_args(argv)
+    (bench_rpc if a.mode == "rpc" else bench_device)(a)
+    return 0
+
+
+if __name__ == "__main__":
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(main())

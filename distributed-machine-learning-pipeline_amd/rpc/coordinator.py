@@ -282,8 +282,10 @@ class GPUCoordinatorServicer:
         try:
             if c.backend == "rccl":
                 self._allreduce_rccl(c, op)
-            else:
+            elif op.algo == "coordinator-ring":
                 self._allreduce_rpc_ring(c, op)
+            else:  # "device-ring" (default): devices drive the ring themselves
+                self._allreduce_device_ring(c, op)
         except Exception as e:
             self._fail(c, f"{type(e).__name__}: {e}")
             return False
@@ -303,6 +305,13 @@ class GPUCoordinatorServicer:
                 algo=algo, chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
             for d in c.devices])
 
+    def _allreduce_device_ring(self, c: Communicator, op) -> None:
+        self._parallel([
+            (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
+                commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
+                algo="rpc-ring", chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
+            for d in c.devices])
+
     def _wait_stream(self, d: DeviceInfo, sid: int) -> None:
         delay, t_end = 2e-4, time.time() + self.rpc_timeout
         while True:
@@ -317,16 +326,33 @@ class GPUCoordinatorServicer:
             time.sleep(delay)
             delay = min(delay * 2, 0.01)
 
-    def _transfer(self, src: DeviceInfo, dst: DeviceInfo, src_addr: int, dst_addr: int,
-                  nbytes: int) -> None:
-        """Device `src` pushes nbytes to device `dst` (device-driven stream)."""
-        sid = src.stub.BeginSend(pb.BeginSendRequest(
+    def _begin_send(self, src: DeviceInfo, dst: DeviceInfo, src_addr: int, nbytes: int) -> int:
+        return src.stub.BeginSend(pb.BeginSendRequest(
             sendBuffAddr=pb.MemAddr(value=src_addr), numBytes=nbytes, dstRank=pb.Rank(value=dst.rank),
             dstAddress=dst.address), timeout=self.rpc_timeout).streamId.value
+
+    def _begin_receive(self, src: DeviceInfo, dst: DeviceInfo, sid: int, dst_addr: int, nbytes: int):
         dst.stub.BeginReceive(pb.BeginReceiveRequest(
             streamId=pb.StreamId(value=sid), recvBuffAddr=pb.MemAddr(value=dst_addr),
             numBytes=nbytes, srcRank=pb.Rank(value=src.rank)), timeout=self.rpc_timeout)
-        self._wait_stream(src, sid)
+
+    def _transfer(self, src: DeviceInfo, dst: DeviceInfo, src_addr: int, dst_addr: int,
+                  nbytes: int, reduce_op=None) -> None:
+        """Device `src` pushes nbytes to device `dst` (device-driven stream).
+        The receiver's WaitStream / Reduce(waitStreamId) block server-side on
+        the stream's completion event — no status polling."""
+        sid = self._begin_send(src, dst, src_addr, nbytes)
+        self._begin_receive(src, dst, sid, dst_addr, nbytes)
+        if reduce_op is None:
+            st = dst.stub.WaitStream(pb.WaitStreamRequest(streamId=pb.StreamId(value=sid)),
+                                     timeout=self.rpc_timeout).status
+            if st != SUCCESS:
+                raise CollectiveError(f"stream {sid} to device {dst.device_id} failed")
+        else:
+            red_dst, dtype, op = reduce_op
+            dst.stub.Reduce(pb.ReduceRequest(dstAddr=red_dst, srcAddr=dst_addr, numBytes=nbytes,
+                                             dtype=dtype, op=op, waitStreamId=sid),
+                            timeout=self.rpc_timeout)
 
     def _allreduce_rpc_ring(self, c: Communicator, op) -> None:
         devs = c.devices
@@ -354,10 +380,8 @@ class GPUCoordinatorServicer:
                     scr = dst.metadata.maxMemAddr.value
 
                     def job(src=src, dst=dst, lo=lo, ln=ln, scr=scr, r_dst=(r + 1) % n):
-                        self._transfer(src, dst, base[src.rank] + lo, scr, ln)
-                        dst.stub.Reduce(pb.ReduceRequest(dstAddr=base[r_dst] + lo, srcAddr=scr,
-                                                         numBytes=ln, dtype=op.dtype, op=op.op),
-                                        timeout=self.rpc_timeout)
+                        self._transfer(src, dst, base[src.rank] + lo, scr, ln,
+                                       reduce_op=(base[r_dst] + lo, op.dtype, op.op))
                     jobs.append(job)
                 self._parallel(jobs)
         # All-gather: step s, rank r sends segment (r + 1 - s) straight into place.

@@ -148,7 +148,16 @@ class GPUDeviceServicer:
         context.abort(grpc.StatusCode.INVALID_ARGUMENT, "invalid Memcpy request")
 
     # ---------------------------------------------------------- collectives --
+    def WaitStream(self, request, context):
+        tmo = (request.timeoutMs or 120000) / 1000.0
+        return pb.WaitStreamResponse(status=self.dev.wait_stream(request.streamId.value, tmo))
+
     def Reduce(self, request, context):
+        if request.waitStreamId:
+            st = self.dev.wait_stream(request.waitStreamId, 120.0)
+            if st != STATUS_SUCCESS:
+                context.abort(grpc.StatusCode.ABORTED, f"stream {request.waitStreamId} did not complete")
+            self.dev.drop_stream(request.waitStreamId)
         try:
             self.dev.reduce(request.dstAddr, request.srcAddr, request.numBytes, request.dtype, request.op)
             if request.scale not in (0.0, 1.0):
@@ -187,10 +196,106 @@ class GPUDeviceServicer:
         self.comm_meta[cid] = meta
         return pb.CommSetupResponse(success=True, backend=backend)
 
+    def _rpc_ring(self, cid: int, addr: int, count: int, dtype: int, op: int, chunk: int) -> None:
+        """Device-driven ring all-reduce over gRPC streams (CPU / no-RCCL path).
+
+        Every device runs the same 2(n-1) steps; in each it binds the receive of
+        its predecessor's segment locally, pushes its own segment to its
+        successor (StreamSend), waits for the incoming one and reduces it in
+        place.  Stream ids are deterministic (comm, call sequence, step, sender)
+        so no coordinator round trip is needed per step."""
+        meta = self.comm_meta[cid]
+        r, n, peers = meta["rank"], meta["nranks"], meta["peers"]
+        seq = meta.setdefault("seq", 0)
+        meta["seq"] = seq + 1
+        es = DT_SIZE[dtype]
+        elems = count // es
+        seg = -(-elems // n)
+        off = [min(i * seg, elems) * es for i in range(n + 1)]
+        nxt, prv = peers[(r + 1) % n], (r - 1) % n
+        scratch = self.dev.scratch_addr
+
+        def sid_of(step, src):
+            return (1 << 62) | ((cid & 0xFFFF) << 44) | ((seq & 0xFFFFF) << 24) | ((step & 0xFFF) << 12) | (src & 0xFFF)
+
+        def push(sid, lo, ln):
+            data = self.dev.read(addr + lo, ln, internal=True)
+
+            def chunks():
+                for o in range(0, max(ln, 1), CHUNK):
+                    yield pb.DataChunk(data=data[o:o + CHUNK], streamId=sid, srcRank=r)
+            ok = self._peer(nxt).StreamSend(chunks(), timeout=120).success
+            self.counters["stream_bytes_out"] += ln
+            if not ok:
+                raise RuntimeError(f"push of stream {sid} to {nxt} failed")
+
+        step = 0
+        for s_ in range(n - 1):  # reduce-scatter
+            si, ri = (r - s_) % n, (r - s_ - 1) % n
+            sl, rl = off[si + 1] - off[si], off[ri + 1] - off[ri]
+            sid_in = sid_of(step, prv)
+            if rl:
+                self.dev.begin_receive(sid_in, scratch, rl, prv)
+            err = []
+            t = None
+            if sl:
+                t = threading.Thread(target=_capture, args=(err, push, sid_of(step, r), off[si], sl))
+                t.start()
+            if rl:
+                if self.dev.wait_stream(sid_in, 120.0) != STATUS_SUCCESS:
+                    raise RuntimeError(f"ring step {step}: receive from rank {prv} failed")
+                self.dev.drop_stream(sid_in)
+                self.dev.reduce(addr + off[ri], scratch, rl, dtype, op)
+                self.dev.synchronize()
+            if t:
+                t.join()
+            if err:
+                raise err[0]
+            step += 1
+        for s_ in range(n - 1):  # all-gather, straight into place
+            si, ri = (r + 1 - s_) % n, (r - s_) % n
+            sl, rl = off[si + 1] - off[si], off[ri + 1] - off[ri]
+            sid_in = sid_of(step, prv)
+            if rl:
+                self.dev.begin_receive(sid_in, addr + off[ri], rl, prv)
+            err = []
+            t = None
+            if sl:
+                t = threading.Thread(target=_capture, args=(err, push, sid_of(step, r), off[si], sl))
+                t.start()
+            if rl:
+                if self.dev.wait_stream(sid_in, 120.0) != STATUS_SUCCESS:
+                    raise RuntimeError(f"ring step {step}: receive from rank {prv} failed")
+                self.dev.drop_stream(sid_in)
+            if t:
+                t.join()
+            if err:
+                raise err[0]
+            step += 1
+        del chunk
+
     def DeviceAllReduce(self, request, context):
         comm = self.comms.get(request.commId)
+        if comm is None and request.commId in self.comm_meta:
+            es = DT_SIZE.get(request.dtype, 0)
+            if es == 0 or request.count % es:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, "bad dtype / count")
+            try:
+                self.dev.check(request.addr, request.count)
+            except OutOfRange as e:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            t0 = time.perf_counter()
+            try:
+                for _ in range(max(1, request.repeat)):
+                    self._rpc_ring(request.commId, request.addr, request.count, request.dtype,
+                                   request.op, request.chunkBytes)
+            except Exception as e:
+                context.abort(grpc.StatusCode.INTERNAL, f"device ring failed: {e}")
+            self.counters["allreduces"] += max(1, request.repeat)
+            return pb.DeviceAllReduceResponse(success=True,
+                                              elapsedUs=(time.perf_counter() - t0) * 1e6)
         if comm is None:
-            context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"no RCCL communicator for comm {request.commId}")
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"no communicator {request.commId} on this device")
         if comm.aborted:
             context.abort(grpc.StatusCode.ABORTED, "communicator aborted")
         es = DT_SIZE[request.dtype]
@@ -369,6 +474,13 @@ class GPUDeviceServicer:
         d.update({"device_id": self.dev.device_id, "backend": self.dev.backend,
                   "comms": sorted(self.comms), "steps_done": getattr(self.trainer, "steps_done", 0)})
         return pb.GetStatsResponse(json=json.dumps(d))
+
+
+def _capture(err, fn, *args):
+    try:
+        fn(*args)
+    except Exception as e:  # surfaced by the caller after join()
+        err.append(e)
 
 
 def start_device_server(device_id: int, mem_size: int, address: str = "127.0.0.1:0",

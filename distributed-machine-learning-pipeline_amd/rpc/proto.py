@@ -112,7 +112,10 @@ MESSAGES: M = {
     "RunBackwardResponse": [("success", 1, "bool"), ("numBytes", 2, "uint64")],
     # -- extensions (device) -------------------------------------------------
     "ReduceRequest": [("dstAddr", 1, "uint64"), ("srcAddr", 2, "uint64"), ("numBytes", 3, "uint64"),
-                      ("dtype", 4, ".DataType"), ("op", 5, ".ReduceOp"), ("scale", 6, "double")],
+                      ("dtype", 4, ".DataType"), ("op", 5, ".ReduceOp"), ("scale", 6, "double"),
+                      ("waitStreamId", 7, "uint64")],
+    "WaitStreamRequest": [("streamId", 1, ".StreamId"), ("timeoutMs", 2, "uint32")],
+    "WaitStreamResponse": [("status", 1, ".Status")],
     "ReduceResponse": [("success", 1, "bool")],
     "GetCommUniqueIdRequest": [("commId", 1, "uint64")],
     "GetCommUniqueIdResponse": [("uniqueId", 1, "bytes")],
@@ -162,6 +165,7 @@ SERVICES = {
         ("RunForward", "RunForwardRequest", "RunForwardResponse", False),
         ("RunBackward", "RunBackwardRequest", "RunBackwardResponse", False),
         ("Reduce", "ReduceRequest", "ReduceResponse", False),
+        ("WaitStream", "WaitStreamRequest", "WaitStreamResponse", False),
         ("GetCommUniqueId", "GetCommUniqueIdRequest", "GetCommUniqueIdResponse", False),
         ("CommSetup", "CommSetupRequest", "CommSetupResponse", False),
         ("DeviceAllReduce", "DeviceAllReduceRequest", "DeviceAllReduceResponse", False),

@@ -50,6 +50,7 @@ class _Stream:
     received: int = 0
     status: int = STATUS_IN_PROGRESS
     bound: threading.Event = field(default_factory=threading.Event)
+    done: threading.Event = field(default_factory=threading.Event)
 
 
 class _Device:
@@ -116,6 +117,15 @@ class _Device:
             st = self._streams.get(sid)
             if st is not None:
                 st.status = status
+                if status != STATUS_IN_PROGRESS:
+                    st.done.set()
+
+    def wait_stream(self, sid: int, timeout: float) -> int:
+        """Block until stream `sid` completes (event-driven, no polling)."""
+        with self._lock:
+            st = self._streams.setdefault(sid, _Stream())
+        st.done.wait(timeout)
+        return st.status
 
     def stream_status(self, sid: int) -> int:
         st = self.stream(sid)
@@ -130,6 +140,7 @@ class _Device:
                 st = self._streams.setdefault(sid, _Stream())
         if not st.bound.wait(wait_s):
             st.status = STATUS_FAILED
+            st.done.set()
             return False
         off = 0
         ok = True
@@ -142,6 +153,7 @@ class _Device:
         ok = ok and off == st.num_bytes and st.initiated_recv
         st.received = off
         st.status = STATUS_SUCCESS if ok else STATUS_FAILED
+        st.done.set()
         if ok:
             self.record_extent(st.recv_addr, off)
         return ok
