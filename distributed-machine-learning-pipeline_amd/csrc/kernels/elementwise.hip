@@ -86,9 +86,10 @@ __device__ __forceinline__ int32_t ropi(int32_t a, int32_t b) {
 template <int OP>
 __global__ __launch_bounds__(256) void reduce_f32_k(float* __restrict__ dst,
                                                     const float* __restrict__ a,
-                                                    const float* __restrict__ b, int64_t n) {
+                                                    const float* __restrict__ b, int64_t n,
+                                                    int vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t nv = n >> 2;
+  const int64_t nv = vec ? n >> 2 : 0;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const float4 x = reinterpret_cast<const float4*>(a)[v];
     const float4 y = reinterpret_cast<const float4*>(b)[v];
@@ -115,9 +116,10 @@ __device__ __forceinline__ uint16_t f2h(float f) {
 template <int OP, bool BF>
 __global__ __launch_bounds__(256) void reduce_h16_k(uint16_t* __restrict__ dst,
                                                     const uint16_t* __restrict__ a,
-                                                    const uint16_t* __restrict__ b, int64_t n) {
+                                                    const uint16_t* __restrict__ b, int64_t n,
+                                                    int vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t nv = n >> 3;
+  const int64_t nv = vec ? n >> 3 : 0;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const uint4 x = reinterpret_cast<const uint4*>(a)[v];
     const uint4 y = reinterpret_cast<const uint4*>(b)[v];
@@ -145,9 +147,10 @@ __device__ __forceinline__ uint8_t ropu8(uint8_t a, uint8_t b) {
 template <int OP>
 __global__ __launch_bounds__(256) void reduce_u8_k(uint8_t* __restrict__ dst,
                                                    const uint8_t* __restrict__ a,
-                                                   const uint8_t* __restrict__ b, int64_t n) {
+                                                   const uint8_t* __restrict__ b, int64_t n,
+                                                   int vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t nv = n >> 4;
+  const int64_t nv = vec ? n >> 4 : 0;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const uint4 x = reinterpret_cast<const uint4*>(a)[v];
     const uint4 y = reinterpret_cast<const uint4*>(b)[v];
@@ -175,24 +178,27 @@ __global__ __launch_bounds__(256) void reduce_i32_k(int32_t* __restrict__ dst,
 template <int OP>
 static hipError_t launch_reduce(void* dst, const void* a, const void* b, int64_t n,
                                 int32_t dtype, hipStream_t s) {
+  // 16 B vector body when all three pointers are 16 B aligned, else the
+  // element-wise path (ring segments of odd sizes land on any byte offset).
   const uintptr_t al = (uintptr_t)dst | (uintptr_t)a | (uintptr_t)b;
-  if (al & 15) return hipErrorInvalidValue;  // vector paths need 16 B alignment
+  const int vec = (al & 15) == 0;
   switch (dtype) {
     case kF32:
-      hipLaunchKernelGGL(reduce_f32_k<OP>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s,
-                         (float*)dst, (const float*)a, (const float*)b, n);
+      hipLaunchKernelGGL(reduce_f32_k<OP>, dim3(grid_for(vec ? (n + 3) / 4 : n)), dim3(256), 0, s,
+                         (float*)dst, (const float*)a, (const float*)b, n, vec);
       break;
     case kBF16:
-      hipLaunchKernelGGL((reduce_h16_k<OP, true>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, s,
-                         (uint16_t*)dst, (const uint16_t*)a, (const uint16_t*)b, n);
+      hipLaunchKernelGGL((reduce_h16_k<OP, true>), dim3(grid_for(vec ? (n + 7) / 8 : n)), dim3(256),
+                         0, s, (uint16_t*)dst, (const uint16_t*)a, (const uint16_t*)b, n, vec);
       break;
     case kF16:
-      hipLaunchKernelGGL((reduce_h16_k<OP, false>), dim3(grid_for((n + 7) / 8)), dim3(256), 0,
-                         s, (uint16_t*)dst, (const uint16_t*)a, (const uint16_t*)b, n);
+      hipLaunchKernelGGL((reduce_h16_k<OP, false>), dim3(grid_for(vec ? (n + 7) / 8 : n)),
+                         dim3(256), 0, s, (uint16_t*)dst, (const uint16_t*)a, (const uint16_t*)b, n,
+                         vec);
       break;
     case kU8:
-      hipLaunchKernelGGL(reduce_u8_k<OP>, dim3(grid_for((n + 15) / 16)), dim3(256), 0, s,
-                         (uint8_t*)dst, (const uint8_t*)a, (const uint8_t*)b, n);
+      hipLaunchKernelGGL(reduce_u8_k<OP>, dim3(grid_for(vec ? (n + 15) / 16 : n)), dim3(256), 0, s,
+                         (uint8_t*)dst, (const uint8_t*)a, (const uint8_t*)b, n, vec);
       break;
     case kI32:
       hipLaunchKernelGGL(reduce_i32_k<OP>, dim3(grid_for(n)), dim3(256), 0, s, (int32_t*)dst,

@@ -29,7 +29,7 @@ from __future__ import annotations
 import logging
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import FIRST_EXCEPTION, ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
@@ -102,8 +102,12 @@ class GPUCoordinatorServicer:
             context.abort(grpc.StatusCode.NOT_FOUND, f"communicator {comm_id} not found")
         return c
 
-    def _parallel(self, fns):
+    def _parallel(self, fns, on_error=None):
         futs = [self._pool.submit(f) for f in fns]
+        if on_error is not None:
+            done, _ = wait(futs, return_when=FIRST_EXCEPTION)
+            if any(f.exception() is not None for f in done):
+                on_error()  # e.g. abort peers still blocked on the failed rank
         errs, out = [], []
         for f in futs:
             try:
@@ -298,19 +302,23 @@ class GPUCoordinatorServicer:
         return op.memAddrs[rank].value if rank in op.memAddrs else DEFAULT_ADDR
 
     def _allreduce_rccl(self, c: Communicator, op) -> None:
-        algo = op.algo or "ring"
+        algo = op.algo if op.algo in ("ring", "rccl") else "ring"
         self._parallel([
             (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                 commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
                 algo=algo, chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
-            for d in c.devices])
+            for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
+
+    def _abort_all(self, c: Communicator, reason: str) -> None:
+        for d in list(c.devices):
+            self._pool.submit(self._safe_abort, d, c.id, reason)
 
     def _allreduce_device_ring(self, c: Communicator, op) -> None:
         self._parallel([
             (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                 commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
                 algo="rpc-ring", chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
-            for d in c.devices])
+            for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
 
     def _wait_stream(self, d: DeviceInfo, sid: int) -> None:
         delay, t_end = 2e-4, time.time() + self.rpc_timeout
@@ -359,7 +367,8 @@ class GPUCoordinatorServicer:
         n = len(devs)
         es = DT_SIZE[op.dtype]
         elems = op.count // es
-        seg = -(-elems // n)
+        al = 16 // es
+        seg = (-(-elems // n) + al - 1) // al * al
         off = [min(i * seg, elems) * es for i in range(n + 1)]
         scratch = min(d.metadata.maxMemAddr.value for d in devs)  # private window above max
         chunk = (op.chunkBytes or (1 << 20)) // es * es

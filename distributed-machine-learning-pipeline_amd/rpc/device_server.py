@@ -210,7 +210,8 @@ class GPUDeviceServicer:
         meta["seq"] = seq + 1
         es = DT_SIZE[dtype]
         elems = count // es
-        seg = -(-elems // n)
+        al = 16 // es  # 16 B aligned segments keep the HIP reduce on its vector path
+        seg = (-(-elems // n) + al - 1) // al * al
         off = [min(i * seg, elems) * es for i in range(n + 1)]
         nxt, prv = peers[(r + 1) % n], (r - 1) % n
         scratch = self.dev.scratch_addr
@@ -325,6 +326,8 @@ class GPUDeviceServicer:
         return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
 
     def Abort(self, request, context):
+        # unblock any device-driven ring step waiting on a peer that died
+        self.dev.fail_pending_streams()
         ids = [request.commId] if request.commId in self.comms else list(self.comms)
         for cid in ids:
             try:

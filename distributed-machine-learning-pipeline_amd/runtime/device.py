@@ -164,6 +164,14 @@ class _Device:
             for k in done[:-keep_last] if len(done) > keep_last else []:
                 del self._streams[k]
 
+    def fail_pending_streams(self) -> None:
+        with self._lock:
+            for st in self._streams.values():
+                if st.status == STATUS_IN_PROGRESS:
+                    st.status = STATUS_FAILED
+                    st.bound.set()
+                    st.done.set()
+
     def drop_stream(self, sid: int) -> None:
         with self._lock:
             self._streams.pop(sid, None)
