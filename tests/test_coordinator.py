@@ -209,3 +209,25 @@ def test_allreduce_comparison():  # TestAllReduceComparison (allreduce_compariso
         assert ring.success
         assert c.devices[2][2].dev.read(0x1000, 16) == bytes([3]) * 16  # values checked (the reference never did)
         print(f"naive={naive.totalTimeMs} ms ring={ring_ms:.1f} ms")
+
+
+@pytest.mark.parametrize("algo", ["device-ring", "coordinator-ring"])
+def test_device_failure_during_allreduce_fails_fast(algo):
+    """BASELINE config 5 (fault injection), CPU plumbing: a device dies, the next
+    AllReduceRing must fail promptly (peers aborted, no hang) and the
+    communicator must end FAILED."""
+    n = 3
+    with cluster(n_devices=n, mem_size=1 << 20, rpc_timeout=60.0) as c:
+        cid = c.comm_init().commId
+        for i in range(n):
+            c.devices[i][2].dev.write(0x1000, np.ones(4096, np.float32).tobytes())
+        c.devices[2][0].stop(0)  # kill rank 2 without waiting for the health probe
+        t0 = time.time()
+        with pytest.raises(grpc.RpcError) as e:
+            c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=4096 * 4, algo=algo))
+        assert time.time() - t0 < 20.0
+        assert e.value.code() == grpc.StatusCode.INTERNAL
+        assert _status(c, cid) == FAILED
+        with pytest.raises(grpc.RpcError) as e:
+            c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=16))
+        assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION
