@@ -34,8 +34,9 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--sync", default="rccl", choices=["rccl", "ring", "torch"])
-    ap.add_argument("--graph-steps", type=int, default=50,
-                    help="steps captured per hipGraph (0 = eager launches)")
+    ap.add_argument("--graph-steps", type=int, default=-1,
+                    help="steps captured per hipGraph (0 = eager C++ launch loop; default: 50 "
+                         "on one GPU, 0 with N>1 so the RCCL all-reduce is never captured)")
     ap.add_argument("--samples-per-rank", type=int, default=60032)
     a = ap.parse_args()
 
@@ -51,6 +52,8 @@ def main() -> int:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE",
               file=sys.stderr)
     ctx = DistContext.from_env(device="cuda")
+    if a.graph_steps < 0:
+        a.graph_steps = 50 if ctx.world_size == 1 else 0
     spec = MlpSpec.parse(a.model)
     ds = synthetic_mnist(a.samples_per_rank, seed=1000 + ctx.rank, dim=spec.dims[0])
     tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,

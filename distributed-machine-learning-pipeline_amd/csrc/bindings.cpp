@@ -19,6 +19,10 @@ void check_cuda(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+void check_cuda_strided(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+
 void check_f32(const torch::Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
@@ -249,6 +253,131 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                        src.numel(), cur_stream()), "bf16_to_f32");
   });
 
+  // ---- bf16 GEMM toolkit (wide MLP) -------------------------------------------
+  auto bf16p = [](const torch::Tensor& t, const char* name) -> uint16_t* {
+    check_cuda_strided(t, name);
+    TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bfloat16");
+    return reinterpret_cast<uint16_t*>(t.data_ptr());
+  };
+  m.def("gemm_bf16_nt", [bf16p](torch::Tensor A, torch::Tensor B, torch::Tensor Cp, int64_t M,
+                               int64_t N, int64_t K, int64_t splits) {
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "A, B must be 2-D");
+    TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "A, B rows must be contiguous");
+    TORCH_CHECK(A.size(0) >= M && B.size(0) >= N && A.size(1) >= K && B.size(1) >= K, "A/B too small");
+    check_f32(Cp, "Cp");
+    const int S = gemm_bf16_num_splits((int)K, (int)splits);
+    TORCH_CHECK(Cp.numel() >= (int64_t)S * M * N, "Cp too small: need ", (int64_t)S * M * N);
+    hip_ok(gemm_bf16_nt(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), Cp.data_ptr<float>(),
+                        (int)M, (int)N, (int)K, (int)splits, cur_stream()), "gemm_bf16_nt");
+    return S;
+  });
+  m.def("gemm_num_splits", [](int64_t K, int64_t splits) { return gemm_bf16_num_splits((int)K, (int)splits); });
+  m.def("gemm_epilogue", [bf16p](torch::Tensor Cp, int64_t S, int64_t M, int64_t N, double alpha,
+                                c10::optional<torch::Tensor> bias, bool relu,
+                                c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
+                                c10::optional<torch::Tensor> obf, c10::optional<torch::Tensor> obfT) {
+    check_f32(Cp, "Cp");
+    TORCH_CHECK(Cp.numel() >= S * M * N, "Cp too small");
+    const float* b = nullptr;
+    if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= N, "bias too small"); b = bias->data_ptr<float>(); }
+    auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
+    };
+    const uint16_t* mk = nullptr; int64_t ldm = 0;
+    if (mask) { chk2(*mask, M, N, "mask"); mk = bf16p(*mask, "mask"); ldm = mask->stride(0); }
+    float* o32 = nullptr; int64_t ldo = 0;
+    if (of32) { check_cuda_strided(*of32, "of32"); TORCH_CHECK(of32->scalar_type() == torch::kFloat32, "of32 f32");
+                chk2(*of32, M, N, "of32"); o32 = of32->data_ptr<float>(); ldo = of32->stride(0); }
+    uint16_t* ob = nullptr; int64_t ldb = 0;
+    if (obf) { chk2(*obf, M, N, "obf"); ob = bf16p(*obf, "obf"); ldb = obf->stride(0); }
+    uint16_t* obt = nullptr; int64_t ldt = 0;
+    if (obfT) { chk2(*obfT, N, M, "obfT"); obt = bf16p(*obfT, "obfT"); ldt = obfT->stride(0); }
+    hip_ok(gemm_epilogue(Cp.data_ptr<float>(), (int)S, (int)M, (int)N, (float)alpha, b, relu ? 1 : 0,
+                         mk, ldm, o32, ldo, ob, ldb, obt, ldt, cur_stream()), "gemm_epilogue");
+  }, py::arg("Cp"), py::arg("S"), py::arg("M"), py::arg("N"), py::arg("alpha") = 1.0,
+     py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("mask") = py::none(),
+     py::arg("of32") = py::none(), py::arg("obf") = py::none(), py::arg("obfT") = py::none());
+  m.def("cast_transpose", [bf16p](torch::Tensor X, int64_t M, int64_t K, torch::Tensor Y,
+                                 c10::optional<torch::Tensor> YT) {
+    check_f32(X, "X");
+    TORCH_CHECK(X.dim() == 2 && X.size(0) >= M && X.size(1) >= K, "X shape");
+    TORCH_CHECK(Y.dim() == 2 && Y.size(0) >= M && Y.stride(1) == 1, "Y shape");
+    const int64_t Kp = Y.size(1);
+    TORCH_CHECK(Kp >= K, "Y narrower than K");
+    uint16_t* yt = nullptr; int64_t ldt = 0;
+    if (YT) { TORCH_CHECK(YT->dim() == 2 && YT->size(0) >= Kp && YT->size(1) >= M && YT->stride(1) == 1, "YT shape");
+              yt = bf16p(*YT, "YT"); ldt = YT->stride(0); }
+    hip_ok(cast_transpose(X.data_ptr<float>(), X.stride(0), (int)M, (int)K, (int)Kp, bf16p(Y, "Y"),
+                          Y.stride(0), yt, ldt, cur_stream()), "cast_transpose");
+  });
+  m.def("softmax_xent", [bf16p](torch::Tensor logits, torch::Tensor labels, int64_t B, int64_t C,
+                               double inv_batch, torch::Tensor dz, c10::optional<torch::Tensor> dzT,
+                               torch::Tensor stats) {
+    check_f32(logits, "logits"); check_cuda(labels, "labels"); check_f32(stats, "stats");
+    TORCH_CHECK(labels.scalar_type() == torch::kInt32 && labels.numel() >= B, "labels");
+    TORCH_CHECK(logits.dim() == 2 && logits.size(0) >= B && logits.size(1) >= C, "logits shape");
+    TORCH_CHECK(dz.dim() == 2 && dz.size(0) >= B && dz.stride(1) == 1, "dz shape");
+    const int64_t Cp = dz.size(1);
+    uint16_t* t = nullptr; int64_t ldt = 0;
+    if (dzT) { TORCH_CHECK(dzT->dim() == 2 && dzT->size(0) >= Cp && dzT->size(1) >= B, "dzT shape");
+               t = bf16p(*dzT, "dzT"); ldt = dzT->stride(0); }
+    hip_ok(softmax_xent(logits.data_ptr<float>(), logits.stride(0), labels.data_ptr<int32_t>(), (int)B,
+                        (int)C, (int)Cp, (float)inv_batch, bf16p(dz, "dz"), dz.stride(0), t, ldt,
+                        stats.data_ptr<float>(), cur_stream()), "softmax_xent");
+  });
+  m.def("rowsum_bf16", [bf16p](torch::Tensor X, int64_t N, int64_t cols, c10::optional<torch::Tensor> out,
+                              c10::optional<torch::Tensor> bias, double lr) {
+    TORCH_CHECK(X.dim() == 2 && X.size(0) >= N && X.size(1) >= cols, "X shape");
+    TORCH_CHECK(out.has_value() != bias.has_value(), "exactly one of out / bias");
+    torch::Tensor t = out ? *out : *bias;
+    check_f32(t, "out/bias");
+    TORCH_CHECK(t.numel() >= N, "out/bias too small");
+    hip_ok(rowsum_bf16(bf16p(X, "X"), X.stride(0), (int)N, (int)cols, out ? t.data_ptr<float>() : nullptr,
+                       bias ? t.data_ptr<float>() : nullptr, (float)lr, cur_stream()), "rowsum_bf16");
+  }, py::arg("X"), py::arg("N"), py::arg("cols"), py::arg("out") = py::none(), py::arg("bias") = py::none(),
+     py::arg("lr") = 0.0);
+  m.def("gemm_bf16_nt_fused", [bf16p](torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, int64_t K,
+                                     double alpha, c10::optional<torch::Tensor> bias, bool relu,
+                                     c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
+                                     c10::optional<torch::Tensor> obf, c10::optional<torch::Tensor> obfT,
+                                     c10::optional<torch::Tensor> sgdW, double lr) {
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A, B 2-D rows");
+    TORCH_CHECK(A.size(0) >= M && B.size(0) >= N && A.size(1) >= K && B.size(1) >= K, "A/B too small");
+    auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
+    };
+    GemmEpi e{};
+    e.alpha = (float)alpha;
+    e.relu = relu ? 1 : 0;
+    e.lr = (float)lr;
+    if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= N, "bias"); e.bias = bias->data_ptr<float>(); }
+    if (mask) { chk2(*mask, M, N, "mask"); e.mask = bf16p(*mask, "mask"); e.ldm = mask->stride(0); }
+    if (of32) { chk2(*of32, M, N, "of32"); TORCH_CHECK(of32->scalar_type() == torch::kFloat32, "of32 f32");
+                e.of32 = of32->data_ptr<float>(); e.ldo = of32->stride(0); }
+    if (obf) { chk2(*obf, M, N, "obf"); e.obf = bf16p(*obf, "obf"); e.ldb = obf->stride(0); }
+    if (obfT) { chk2(*obfT, N, M, "obfT"); e.obfT = bf16p(*obfT, "obfT"); e.ldt = obfT->stride(0); }
+    if (sgdW) { chk2(*sgdW, M, N, "sgdW"); TORCH_CHECK(sgdW->scalar_type() == torch::kFloat32, "sgdW f32");
+                e.sgdW = sgdW->data_ptr<float>(); e.ldw = sgdW->stride(0); }
+    hip_ok(gemm_bf16_nt(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), nullptr, (int)M, (int)N,
+                        (int)K, 1, cur_stream(), &e), "gemm_bf16_nt_fused");
+  }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("alpha") = 1.0,
+     py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("mask") = py::none(),
+     py::arg("of32") = py::none(), py::arg("obf") = py::none(), py::arg("obfT") = py::none(),
+     py::arg("sgdW") = py::none(), py::arg("lr") = 0.0);
+  m.def("sgd_cast", [bf16p](torch::Tensor W, c10::optional<torch::Tensor> G, int64_t N, int64_t K, double lr,
+                           torch::Tensor Wb, c10::optional<torch::Tensor> WbT) {
+    check_f32(W, "W");
+    TORCH_CHECK(W.numel() >= N * K, "W too small");
+    const float* g = nullptr;
+    if (G) { check_f32(*G, "G"); TORCH_CHECK(G->numel() >= N * K, "G too small"); g = G->data_ptr<float>(); }
+    TORCH_CHECK(Wb.dim() == 2 && Wb.size(0) >= N && Wb.size(1) >= K && Wb.stride(1) == 1, "Wb shape");
+    uint16_t* t = nullptr; int64_t ldt = 0;
+    if (WbT) { TORCH_CHECK(WbT->dim() == 2 && WbT->size(0) >= K && WbT->size(1) >= N && WbT->stride(1) == 1, "WbT shape");
+               t = bf16p(*WbT, "WbT"); ldt = WbT->stride(0); }
+    hip_ok(sgd_cast(W.data_ptr<float>(), g, (int)N, (int)K, (float)lr, bf16p(Wb, "Wb"), Wb.stride(0), t, ldt,
+                    cur_stream()), "sgd_cast");
+  });
+
   // ---- fused MLP -----------------------------------------------------------
   m.def("mlp_stamps", []() {
     std::vector<uint64_t> v(kMaxStamps);
@@ -298,6 +427,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stream_handle", &PyMlpRunner::stream_handle)
       .def("graph_steps", [](PyMlpRunner& s) { return s.r->graph_steps(); })
       .def("set_lr", [](PyMlpRunner& s, float lr) { s.r->set_lr(lr); })
+      .def("set_world_size", [](PyMlpRunner& s, int n) { s.r->set_world_size(n); })
       .def("set_comm", [](PyMlpRunner& s, PyComm* c, int algo, int64_t chunk) {
         s.r->set_comm(c ? c->c.get() : nullptr, algo, chunk);
       }, py::arg("comm"), py::arg("algo") = 0, py::arg("chunk_bytes") = 1 << 20)

@@ -109,11 +109,42 @@ hipError_t f32_to_bf16(uint16_t* dst, const float* src, int64_t n, hipStream_t s
 hipError_t bf16_to_f32(float* dst, const uint16_t* src, int64_t n, hipStream_t s);
 
 // ---- bf16 MFMA GEMM with fused epilogues (kernels/gemm_bf16.hip) -------------
-enum Epilogue : int32_t {
-  kEpiNone = 0,       // C = A.B
-  kEpiBias = 1,       // C = A.B + bias
-  kEpiBiasRelu = 2,   // C = relu(A.B + bias)
-  kEpiReluMask = 3,   // C = (A.B) * (mask > 0)   (ReLU backward, mask = post-relu act)
+// Cp[s][M][N] (fp32 split-K slabs) = A[M x K] . B[N x K]^T, bf16 operands with
+// K-contiguous rows (lda, ldb, K multiples of 8; 16 B aligned base pointers).
+struct GemmEpi {
+  float alpha;
+  const float* bias;
+  int relu;
+  const uint16_t* mask;
+  int64_t ldm;
+  float* of32;
+  int64_t ldo;
+  uint16_t* obf;
+  int64_t ldb;
+  uint16_t* obfT;
+  int64_t ldt;
+  float* sgdW;  // fused SGD target (fp32 [M x N], ld ldw): W -= lr * acc
+  int64_t ldw;
+  float lr;
 };
+// epi != nullptr: single K split, epilogue applied in-kernel (Cp unused).
+hipError_t gemm_bf16_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* Cp,
+                        int M, int N, int K, int splits, hipStream_t s,
+                        const GemmEpi* epi = nullptr);
+int gemm_bf16_num_splits(int K, int splits);
+// out = epi(alpha * sum_s Cp[s] + bias): relu, ReLU'-mask (bf16 mask > 0), fp32 / bf16 /
+// transposed-bf16 outputs (each nullable).
+hipError_t gemm_epilogue(const float* Cp, int S, int M, int N, float alpha, const float* bias,
+                         int relu, const uint16_t* mask, int64_t ldm, float* of32, int64_t ldo,
+                         uint16_t* obf, int64_t ldb, uint16_t* obfT, int64_t ldt, hipStream_t s);
+hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uint16_t* Y,
+                          int64_t ldo, uint16_t* YT, int64_t ldt, hipStream_t s);
+hipError_t softmax_xent(const float* logits, int64_t ldl, const int32_t* labels, int B, int C,
+                        int Cp, float inv_batch, uint16_t* dz, int64_t ldz, uint16_t* dzT,
+                        int64_t ldt, float* stats, hipStream_t s);
+hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
+                       float lr, hipStream_t s);
+hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,
+                    uint16_t* WbT, int64_t ldt, hipStream_t s);
 
 }  // namespace dsml

@@ -231,6 +231,12 @@ void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
   reset_graph();
 }
 
+void MlpRunner::set_world_size(int n) {
+  if (n < 1) throw std::invalid_argument("world size must be >= 1");
+  world_ = n;
+  reset_graph();
+}
+
 void MlpRunner::set_lr(float lr) {
   lr_ = lr;
   reset_graph();  // lr is a baked kernel argument
@@ -244,7 +250,7 @@ void MlpRunner::enqueue_fwd_bwd(hipStream_t s) {
 }
 
 void MlpRunner::enqueue_update(hipStream_t s) {
-  const int n = comm_ ? comm_->nranks() : 1;
+  const int n = comm_ ? comm_->nranks() : world_;
   const float gscale = 1.0f / (float)n;
   if (mom_ != 0.f || wd_ != 0.f)
     DSML_HIP_CHECK(sgd_momentum_f32(b_.P, b_.G, b_.V, b_.nparams, lr_, mom_, wd_, gscale, s));

@@ -220,6 +220,9 @@ class MlpRunner {
   const MlpDesc& desc() const { return d_; }
   MlpLaunchCfg cfg() const { return cfg_; }
   void set_lr(float lr);
+  // Replicas averaging gradients outside the runner (torch.distributed path);
+  // the update then applies lr / world.  Defaults to the comm's size.
+  void set_world_size(int n);
 
  private:
   MlpDesc d_;
@@ -228,6 +231,7 @@ class MlpRunner {
   float lr_, mom_, wd_;
   RcclComm* comm_ = nullptr;
   int algo_ = 0;
+  int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;

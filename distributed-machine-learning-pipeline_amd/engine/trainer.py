@@ -110,6 +110,7 @@ class MlpTrainer:
         self.runner = C.MlpRunner(self.layout.desc_list(), self.X, self.y, self.P, self.G, self.V,
                                   self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
                                   self.weight_decay)
+        self.runner.set_world_size(self.ctx.world_size)
         if self.ctx.is_distributed and self.sync in ("rccl", "ring"):
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)

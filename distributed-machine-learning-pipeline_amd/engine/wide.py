@@ -1,0 +1,188 @@
+"""Wide-MLP engine (BASELINE config 4: MLP 784-4096-4096-10, bf16 on MI355X).
+
+Mixed precision: fp32 master weights (flat, same layout as models/mlp.py),
+bf16 copies of W and W^T for the MFMA GEMMs (refreshed by the fused
+update+cast kernel), bf16 activations (+ transposed copies for the weight
+gradients), fp32 accumulation, fp32 gradients all-reduced across replicas.
+
+Every product is a bf16 "NT" GEMM on v_mfma_f32_16x16x32_bf16
+(kernels/gemm_bf16.hip), split-K for the skinny (M = batch) GEMMs so a step
+fills the 256 CUs, then one epilogue kernel (bias / ReLU / ReLU'-mask / casts /
+transposed copy).  Per step, with L layers: 1 input cast, L forward GEMMs,
+softmax-CE, 2L-1 backward GEMMs, L bias reductions, the all-reduce and L
+update kernels.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from ..data.mnist import Dataset
+from ..models.mlp import MlpLayout, MlpSpec, init_params
+from ..parallel.dist import DistContext, make_native_comm
+from .trainer import StepStats
+
+
+def _rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class WideMlpTrainer:
+    def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
+                 ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
+                 sync: str = "rccl", target_wgs: int = 512, graph: bool = True):
+        from ..ops.native import require_native
+
+        self.C = require_native()
+        self.ctx = ctx or DistContext(device=torch.device("cuda", 0))
+        if self.ctx.device.type != "cuda":
+            raise ValueError("WideMlpTrainer runs on a GPU")
+        if batch % 8:
+            raise ValueError("batch must be a multiple of 8 (16 B bf16 rows)")
+        if spec.dims[-1] > 64:
+            raise ValueError("softmax kernel supports <= 64 classes")
+        self.spec, self.batch, self.lr, self.sync = spec, batch, lr, sync
+        self.device = dev = self.ctx.device
+        self.target_wgs = target_wgs
+        d = spec.dims
+        L = spec.nlayers
+        self.L = L
+        self.pd = [_rup(x, 16) for x in d]
+        self.layout = MlpLayout(spec, batch, 1)
+        self.X = data.X.to(dev, torch.float32).contiguous()
+        self.y = data.y.to(dev, torch.int32).contiguous()
+        self.nbatches = len(data) // batch
+        self.P = init_params(self.layout, seed, init).to(dev)
+        self.G = torch.zeros_like(self.P)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.Wb = [torch.zeros(d[l + 1], self.pd[l], **bf) for l in range(L)]
+        self.WbT = [torch.zeros(self.pd[l], self.pd[l + 1], **bf) for l in range(L)]
+        self.H = [torch.zeros(batch, self.pd[l], **bf) for l in range(L)]
+        self.HT = [torch.zeros(self.pd[l], batch, **bf) for l in range(L)]
+        self.dZ = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L + 1)]
+        self.dZT = [None] + [torch.zeros(self.pd[l], batch, **bf) for l in range(1, L + 1)]
+        self.logits = torch.zeros(batch, d[L], dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.views = self.layout.views(self.P)
+        self.gviews = self.layout.views(self.G)
+        # GEMM plans: (A, B, M, N, K, splits)
+        self.plans: Dict[str, tuple] = {}
+        ws = 0
+        for l in range(L):
+            ws = max(ws, self._plan(f"f{l}", batch, d[l + 1], self.pd[l]))
+            ws = max(ws, self._plan(f"w{l}", d[l + 1], d[l], batch))
+            if l > 0:
+                ws = max(ws, self._plan(f"b{l}", batch, d[l], self.pd[l + 1]))
+        self.Cp = torch.zeros(ws, dtype=torch.float32, device=dev)
+        self.steps_done = 0
+        # One hipGraph per epoch (every batch offset baked in): replaying it
+        # removes the ~25 host launches per step.  Single replica only (the
+        # RCCL collective stays outside graphs).
+        self.graph_enabled = graph and not self.ctx.is_distributed
+        self._graph = None
+        self.comm = None
+        if self.ctx.is_distributed and sync in ("rccl", "ring"):
+            self.comm = make_native_comm(self.ctx)
+        for l in range(L):  # bf16 copies of the initial weights
+            W, _ = self.views[l]
+            self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, self.Wb[l], self.WbT[l])
+
+    def _plan(self, name: str, M: int, N: int, K: int) -> int:
+        tiles = math.ceil(M / 64) * math.ceil(N / 64)
+        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128)))
+        S = self.C.gemm_num_splits(K, splits)
+        self.plans[name] = (M, N, K, splits)
+        return S * M * N
+
+    def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor) -> int:
+        M, N, K, splits = self.plans[name]
+        return self.C.gemm_bf16_nt(A, B, self.Cp, M, N, K, splits)
+
+    # ----------------------------------------------------------------- step --
+    def _step(self) -> None:
+        C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
+        r0 = (self.steps_done % self.nbatches) * Bt
+        C.cast_transpose(self.X[r0:r0 + Bt], Bt, d[0], self.H[0], self.HT[0])
+        for l in range(L):
+            S = self._gemm(f"f{l}", self.H[l], self.Wb[l])
+            _, b = self.views[l]
+            if l < L - 1:
+                C.gemm_epilogue(self.Cp, S, Bt, d[l + 1], bias=b, relu=True, obf=self.H[l + 1],
+                                obfT=self.HT[l + 1])
+            else:
+                C.gemm_epilogue(self.Cp, S, Bt, d[l + 1], bias=b, of32=self.logits)
+        C.softmax_xent(self.logits, self.y[r0:r0 + Bt], Bt, d[L], 1.0 / Bt, self.dZ[L], self.dZT[L],
+                       self.stats)
+        world = self.ctx.world_size
+        fused_sgd = world == 1
+        scale = self.lr / world
+        for l in range(L - 1, -1, -1):
+            W, b = self.views[l]
+            gW, gb = self.gviews[l]
+            if l > 0:  # activation gradient first: it needs the pre-update W_l^T
+                S = self._gemm(f"b{l}", self.dZ[l + 1], self.WbT[l])
+                C.gemm_epilogue(self.Cp, S, Bt, d[l], mask=self.H[l], obf=self.dZ[l], obfT=self.dZT[l])
+            if fused_sgd:
+                # dW_l = dZ^T H_l with SGD fused in the GEMM epilogue: W -= lr*dW and
+                # the bf16 W / W^T copies are refreshed from the accumulators.
+                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, sgdW=W,
+                                     lr=scale, obf=self.Wb[l], obfT=self.WbT[l])
+                C.rowsum_bf16(self.dZT[l + 1], d[l + 1], Bt, bias=b, lr=scale)
+            else:
+                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, of32=gW)
+                C.rowsum_bf16(self.dZT[l + 1], d[l + 1], Bt, out=gb)
+        if not fused_sgd:
+            if self.comm is not None:
+                (self.comm.ring_allreduce_(self.G, 0, 4 << 20) if self.sync == "ring"
+                 else self.comm.allreduce_(self.G, 0))
+            else:
+                import torch.distributed as dist
+
+                dist.all_reduce(self.G)
+            for l in range(L):
+                W, b = self.views[l]
+                gW, gb = self.gviews[l]
+                C.sgd_cast(W, gW, d[l + 1], d[l], scale, self.Wb[l], self.WbT[l])
+                C.sgd_update_(b, gb, scale)
+        self.steps_done += 1
+
+    def _capture_epoch(self) -> None:
+        torch.cuda.synchronize(self.device)
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        saved = self.steps_done
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(self.nbatches):
+                self._step()
+        self.steps_done = saved
+        self._graph = g
+
+    def train_steps(self, n: int) -> None:
+        with torch.cuda.device(self.device):
+            while n > 0:
+                if (self.graph_enabled and self.steps_done % self.nbatches == 0
+                        and n >= self.nbatches):
+                    if self._graph is None:
+                        self._capture_epoch()
+                    self._graph.replay()
+                    self.steps_done += self.nbatches
+                    n -= self.nbatches
+                else:
+                    self._step()
+                    n -= 1
+
+    def synchronize(self) -> None:
+        torch.cuda.synchronize(self.device)
+
+    def read_stats(self, reset: bool = True) -> StepStats:
+        self.synchronize()
+        v = self.stats.tolist()
+        if reset:
+            self.stats.zero_()
+        return StepStats(v[0], v[1], v[2])
+
+    def grads_for_test(self) -> torch.Tensor:
+        return self.G

@@ -1,0 +1,68 @@
+"""Multi-replica path on ONE MI355X: two processes share cuda:0 and average
+gradients over gloo (RCCL refuses two ranks on one GPU: "invalid usage").
+This exercises exactly the N>1 step structure of bench.py — fused HIP
+fwd/bwd writing gradients, all-reduce, HIP SGD update — except the RCCL call
+itself (covered on 8 GPUs by the driver's scaling run)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir, kind):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from hipdsml.data.mnist import synthetic_mnist
+    from hipdsml.models.mlp import MlpSpec
+    from hipdsml.parallel.dist import DistContext
+
+    ctx = DistContext.from_env(device="cuda", backend="gloo")
+    if kind == "fused":
+        from hipdsml.engine.trainer import MlpTrainer
+
+        spec = MlpSpec((784, 128, 64, 10))
+        ds = synthetic_mnist(64 * 4, seed=200 + rank)
+        tr = MlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7, sync="torch")
+    else:
+        from hipdsml.engine.wide import WideMlpTrainer
+
+        spec = MlpSpec((784, 256, 128, 10))
+        ds = synthetic_mnist(64 * 4, seed=200 + rank)
+        tr = WideMlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7, sync="torch")
+    tr.train_steps(4)
+    tr.synchronize()
+    torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+@pytest.mark.parametrize("kind", ["fused", "wide"])
+def test_two_replicas_one_gpu(kind):
+    from hipdsml.data.mnist import synthetic_mnist
+    from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d, kind), nprocs=world,
+                           start_method="spawn", join=True)
+        outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
+    assert torch.equal(outs[0], outs[1])
+    dims = (784, 128, 64, 10) if kind == "fused" else (784, 256, 128, 10)
+    lay = MlpLayout(MlpSpec(dims), 64, 4)
+    P = init_params(lay, 7, "reference" if kind == "fused" else "kaiming")
+    shards = [synthetic_mnist(64 * 4, seed=200 + r) for r in range(world)]
+    for s in range(4):
+        g = sum(grads_ref(lay, P, sh.X[s * 64:(s + 1) * 64], sh.y[s * 64:(s + 1) * 64])[0] for sh in shards)
+        P = P - 0.05 * g / world
+    err = (outs[0] - P).abs().max().item()
+    assert err < (2e-5 if kind == "fused" else 5e-3), err
