@@ -108,7 +108,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         for p in lib:
             link += ["-L", p, f"-Wl,-rpath,{p}"]
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-                 "-lamdhip64", "-lrccl"]
+                 "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx"]
         p = subprocess.run(link, capture_output=True, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(link)}\n{p.stdout}\n{p.stderr}")

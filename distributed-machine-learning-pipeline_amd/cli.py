@@ -8,6 +8,7 @@ compile-time constant there is a flag here (SURVEY §5 "Config / flag system").
   device-server  start device servers (one per --ports entry; --gpus maps them to GPUs)
   coordinator    start the coordinator (health-check interval configurable)
   train          run the training client (device / rpc mode)
+  fit            data-parallel training job (torchrun-compatible; config, checkpoints, metrics)
   local          spawn device servers (one process per GPU) + coordinator + client
   bench-allreduce  ring vs naive all-reduce latency through the gpu_sim API
 """
@@ -131,6 +132,10 @@ def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
     if argv and argv[0] == "train":
         return cmd_train(argv[1:])
+    if argv and argv[0] == "fit":
+        from .engine.fit import main as fit_main
+
+        return fit_main(argv[1:])
     if argv and argv[0] == "bench-allreduce":
         return cmd_bench_allreduce(argv[1:])
     ap = argparse.ArgumentParser(prog="hipdsml")

@@ -7,6 +7,8 @@
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "runtime/runtime.h"
 
 namespace py = pybind11;
@@ -556,6 +558,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("erase", &StreamTable::erase)
       .def("__len__", &StreamTable::size);
 
+  // roctx ranges / markers (shown by rocprofv3 --marker-trace; no-ops otherwise).
+  m.def("roctx_push", [](const std::string& name) { return roctxRangePushA(name.c_str()); });
+  m.def("roctx_pop", []() { return roctxRangePop(); });
+  m.def("roctx_mark", [](const std::string& name) { roctxMarkA(name.c_str()); });
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

@@ -272,8 +272,8 @@ class MlpTrainer:
             self.V.copy_(sd["velocity"].to(self.device))
         self.steps_done = int(sd["steps_done"])
         if self.backend == "hip":
-            self.ctr[0] = self.steps_done
-            self.ctr[1] = 0
+            # A = B = s at the start of step s (dsml.h step-counter protocol)
+            self.ctr.fill_(self.steps_done)
             torch.cuda.synchronize(self.device)
 
     def fit(self, epochs: int, log_fn=None, test: Optional[Dataset] = None) -> Dict[str, float]:

@@ -177,12 +177,49 @@ class WideMlpTrainer:
     def synchronize(self) -> None:
         torch.cuda.synchronize(self.device)
 
-    def read_stats(self, reset: bool = True) -> StepStats:
+    def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         self.synchronize()
         v = self.stats.tolist()
         if reset:
             self.stats.zero_()
-        return StepStats(v[0], v[1], v[2])
+        s = StepStats(v[0], v[1], v[2])
+        if global_ and self.ctx.is_distributed:
+            s = StepStats(*self.ctx.all_reduce_scalars(s.loss_sum, s.correct, s.count))
+        return s
 
     def grads_for_test(self) -> torch.Tensor:
         return self.G
+
+    def state_dict(self) -> Dict[str, object]:
+        self.synchronize()
+        return {"spec": list(self.spec.dims), "params": self.P.detach().cpu().clone(),
+                "velocity": torch.empty(0), "steps_done": self.steps_done, "lr": self.lr,
+                "batch": self.batch}
+
+    def load_state_dict(self, sd: Dict[str, object]) -> None:
+        if list(sd["spec"]) != list(self.spec.dims):
+            raise ValueError("checkpoint is for a different model")
+        self.synchronize()
+        self.P.copy_(sd["params"].to(self.device))
+        self.steps_done = int(sd["steps_done"])
+        d = self.spec.dims
+        for l in range(self.L):  # refresh the bf16 GEMM copies from the fp32 masters
+            W, _ = self.views[l]
+            self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, self.Wb[l], self.WbT[l])
+        self.synchronize()
+
+    @torch.no_grad()
+    def evaluate(self, ds: Dataset) -> Dict[str, float]:
+        """fp32 evaluation of the master weights (torch ops on the GPU)."""
+        from ..models.mlp import forward_ref
+
+        X = ds.X.to(self.device, torch.float32)
+        y = ds.y.to(self.device).long()
+        self.synchronize()
+        logits, _ = forward_ref(self.layout, self.P, X)
+        p = torch.softmax(logits, 1)
+        loss = (-torch.log(p.gather(1, y.view(-1, 1)).squeeze(1) + 1e-10)).sum().item()
+        correct = (logits.argmax(1) == y).sum().item()
+        n = X.shape[0]
+        return {"loss": loss / max(n, 1), "accuracy": 100.0 * correct / max(n, 1), "n": n}
+
