@@ -57,7 +57,7 @@ def test_fit_job_gpu(tmp_path, model, engine):
     from hipdsml.engine.fit import run
 
     lines = []
-    r = run(TrainConfig(model=model, samples=64 * 50, epochs=3, lr=0.05, device="cuda",
+    r = run(TrainConfig(model=model, engine=engine, samples=64 * 50, epochs=3, lr=0.05, device="cuda",
                         checkpoint=str(tmp_path), metrics=str(tmp_path / "m.jsonl")),
             out=lines.append)
     assert r["engine"] == engine and r["steps"] == 150
