@@ -9,7 +9,8 @@ random-init weights of the same architecture; fp32 compute like the reference.
 
 Weak scaling: each rank trains batch 64 on its own shard; global batch = 64*N.
 Every timed step is a full optimizer step: fused forward/backward HIP kernels,
-gradient all-reduce over RCCL (N>1), SGD update.
+gradient all-reduce (N>1: fused into the weight-gradient kernel as a one-shot
+exchange over xGMI, or RCCL — chosen at init by a self-test + timing), SGD update.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: launched by torch.distributed.run, one rank per GPU)
@@ -33,11 +34,16 @@ def main() -> int:
     ap.add_argument("--model", default="784-128-64-10")
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--sync", default="rccl", choices=["rccl", "ring", "torch"])
-    ap.add_argument("--graph-steps", type=int, default=-1,
-                    help="steps captured per hipGraph (0 = eager C++ launch loop; default: 50 "
-                         "on one GPU, 0 with N>1 so the RCCL all-reduce is never captured)")
+    ap.add_argument("--sync", default="auto", choices=["auto", "xgmi", "rccl", "ring", "torch"],
+                    help="gradient all-reduce (N>1): auto = the fused xGMI peer exchange if it "
+                         "passes its self-test and beats RCCL at init, else RCCL")
+    ap.add_argument("--graph-steps", type=int, default=50,
+                    help="steps captured per hipGraph (0 = eager C++ launch loop); steps with an "
+                         "RCCL collective always run as the eager C++ loop")
     ap.add_argument("--samples-per-rank", type=int, default=60032)
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
+                         "two ranks on one GPU); use with --sync xgmi or torch")
     a = ap.parse_args()
 
     import torch
@@ -51,9 +57,10 @@ def main() -> int:
     if world_env != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE",
               file=sys.stderr)
-    ctx = DistContext.from_env(device="cuda")
-    if a.graph_steps < 0:
-        a.graph_steps = 50 if ctx.world_size == 1 else 0
+    if a.rehearse_one_gpu:
+        ctx = DistContext.from_env(device="cuda", backend="gloo", device_index=0)
+    else:
+        ctx = DistContext.from_env(device="cuda")
     spec = MlpSpec.parse(a.model)
     ds = synthetic_mnist(a.samples_per_rank, seed=1000 + ctx.rank, dim=spec.dims[0])
     tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,
@@ -93,7 +100,7 @@ def main() -> int:
                 "global_batch": a.batch * n,
                 "seq_len": None,
                 "parallelism": f"dp{n}",
-                "sync": a.sync if n > 1 else "none",
+                "sync": tr.sync_active,
                 "graph_steps": a.graph_steps,
                 "lr": a.lr,
             },

@@ -433,10 +433,46 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_comm", [](PyMlpRunner& s, PyComm* c, int algo, int64_t chunk) {
         s.r->set_comm(c ? c->c.get() : nullptr, algo, chunk);
       }, py::arg("comm"), py::arg("algo") = 0, py::arg("chunk_bytes") = 1 << 20)
+      .def("set_exchange", [](PyMlpRunner& s, PeerExchange* x) { s.r->set_exchange(x); },
+           py::arg("exchange").none(true), py::keep_alive<1, 2>())
+      .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
       .def("plan", [](PyMlpRunner& s) {
         const MlpLaunchCfg c = s.r->cfg();
         return py::make_tuple(c.kchunk, c.nsplit);
       });
+
+  // ---- xGMI peer exchange (gradient all-reduce fused into K_C) -------------
+  m.def("mlp_wgrad_tiles", [](const std::vector<int64_t>& desc) {
+    return mlp_wgrad_tiles(desc_from_list(desc));
+  });
+  py::class_<PeerExchange>(m, "PeerExchange")
+      .def(py::init<int, int64_t, int>(), py::arg("device"), py::arg("half_floats"),
+           py::arg("ntiles"))
+      .def("ipc_handle", [](PeerExchange& x) {
+        const auto v = x.ipc_handle();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("connect_ipc", [](PeerExchange& x, int rank, const std::vector<py::bytes>& hs) {
+        std::vector<std::vector<uint8_t>> v;
+        for (const auto& h : hs) {
+          std::string t = h;
+          v.emplace_back(t.begin(), t.end());
+        }
+        x.connect_ipc(rank, v);
+      })
+      .def("connect_local", &PeerExchange::connect_local)
+      .def("reset", [](PeerExchange& x) { x.reset(cur_stream()); })
+      .def("error", [](PeerExchange& x) {
+        py::gil_scoped_release nogil;
+        return x.error(cur_stream());
+      })
+      .def("set_timeout_ms", &PeerExchange::set_timeout_ms)
+      .def_property_readonly("nranks", &PeerExchange::nranks)
+      .def_property_readonly("rank", &PeerExchange::rank)
+      .def_property_readonly("ntiles", &PeerExchange::ntiles)
+      .def_property_readonly("half", &PeerExchange::half)
+      .def_property_readonly("memory_kind", &PeerExchange::memory_kind)
+      .def_property_readonly("connected", &PeerExchange::connected);
 
   // ---- RCCL ----------------------------------------------------------------
   m.def("rccl_unique_id", []() {

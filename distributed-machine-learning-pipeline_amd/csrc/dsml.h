@@ -82,6 +82,29 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
                          int64_t* ctr, int64_t row0, const MlpDesc& d, float lr, int fused_sgd,
                          hipStream_t s);
 
+// ---- peer exchange: gradient all-reduce fused into K_C over xGMI -------------
+// Every replica's K_C publishes each weight-gradient tile into its own
+// exchange buffer (IPC-shared with the peers, uncached), raises a per-tile
+// flag (= step + 1), waits for the same tile's flag of every peer, reads the
+// peers' tiles over xGMI, sums all N in rank order (bit-identical replicas)
+// and applies SGD with lr / N in place.  Buffers alternate by step parity, so
+// a peer that is one step ahead never overwrites data still being read.
+constexpr int kMaxPeers = 8;
+struct XchgTab {                 // device-resident pointer table (as mapped in this process)
+  float* buf[kMaxPeers];         // rank r's exchange buffer: [2][half] floats
+  uint64_t* flags[kMaxPeers];    // rank r's per-tile flags
+};
+struct XchgArgs {
+  const XchgTab* tab = nullptr;
+  int32_t nranks = 1, rank = 0;
+  int64_t half = 0;              // floats per parity half (>= nparams)
+  uint32_t* err = nullptr;       // set to 1 when a peer did not arrive in time
+  uint64_t timeout_ticks = 0;    // s_memrealtime ticks (100 MHz)
+};
+int mlp_wgrad_tiles(const MlpDesc& d);
+hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
+                              const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
+
 // ---- elementwise / reduction (kernels/elementwise.hip) -----------------------
 enum DType : int32_t { kF32 = 0, kBF16 = 1, kF16 = 2, kU8 = 3, kI32 = 4 };
 enum ReduceOp : int32_t { kSum = 0, kProd = 1, kMin = 2, kMax = 3 };

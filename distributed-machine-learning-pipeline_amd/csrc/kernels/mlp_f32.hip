@@ -376,10 +376,30 @@ __global__ __launch_bounds__(256) void mlp_f32_rowchain_k(
 // (single replica) updates P in place; the kernel never reads W, so the
 // in-place update inside the launch is race-free.
 // ---------------------------------------------------------------------------
+// System-coherent accesses for the peer exchange (bypass the non-coherent
+// caches: sc0 sc1), so no L2 writeback / invalidate fences are needed.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ float ld_sys(const float* p) {
+  return __builtin_bit_cast(float, __hip_atomic_load((const gu32*)(p), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__device__ __forceinline__ void st_sys(float* p, float v) {
+  __hip_atomic_store((gu32*)(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load((const gu64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool XCHG>
 __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ P, float* __restrict__ Gout,
     const float* __restrict__ ws, int64_t* __restrict__ ctr, int64_t row0, MlpDesc d, float lr,
-    int fused_sgd) {
+    int fused_sgd, XchgArgs xa) {
   const int B = d.batch;
   int bid = blockIdx.x;
   int l = 0;
@@ -448,6 +468,79 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
   }
   dbacc += __shfl_xor(dbacc, 16, 64);
   dbacc += __shfl_xor(dbacc, 32, 64);
+
+  if constexpr (XCHG) {
+    // ---- publish this tile, wait for the peers' copies, sum in rank order ----
+    const uint64_t step = ld_ctr(ctr) - 1;
+    const uint64_t want = step + 1;
+    const int64_t poff = (int64_t)(step & 1) * xa.half;
+    const XchgTab* __restrict__ tab = xa.tab;
+    const bool bl = tk == 0 && q == 0;
+    float* mine = tab->buf[xa.rank] + poff;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = tn * 16 + 4 * q + r;
+      if (row < N) {
+        if (k0v) st_sys(mine + woff + (int64_t)row * K + k0, acc0[r]);
+        if (k1v) st_sys(mine + woff + (int64_t)row * K + k1, acc1[r]);
+      }
+    }
+    if (bl && nv) st_sys(mine + d.b_off[l] + n, dbacc);
+    // every lane's payload stores are complete before the flag is raised
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      st_sys64(tab->flags[xa.rank] + blockIdx.x, want);
+    if (lane < xa.nranks && lane != xa.rank) {
+      const uint64_t* f = tab->flags[lane] + blockIdx.x;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (ld_sys64(f) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __asm__ volatile("" ::: "memory");
+    // All peers' tiles in one load batch, then the ordered sum.
+    const int rc[4] = {min(tn * 16 + 4 * q + 0, N - 1), min(tn * 16 + 4 * q + 1, N - 1),
+                       min(tn * 16 + 4 * q + 2, N - 1), min(tn * 16 + 4 * q + 3, N - 1)};
+    float pv[kMaxPeers][9];
+#pragma unroll
+    for (int p = 0; p < kMaxPeers; ++p) {
+      if (p < xa.nranks && p != xa.rank) {
+        const float* pb = tab->buf[p] + poff;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[p][2 * r] = ld_sys(pb + woff + (int64_t)rc[r] * K + k0c);
+          pv[p][2 * r + 1] = ld_sys(pb + woff + (int64_t)rc[r] * K + k1c);
+        }
+        pv[p][8] = bl ? ld_sys(pb + d.b_off[l] + nc) : 0.f;
+      }
+    }
+    float sum[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) sum[j] = 0.f;
+#pragma unroll
+    for (int p = 0; p < kMaxPeers; ++p) {
+      if (p < xa.nranks) {
+        const bool me = p == xa.rank;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sum[2 * r] += me ? acc0[r] : pv[p][2 * r];
+          sum[2 * r + 1] += me ? acc1[r] : pv[p][2 * r + 1];
+        }
+        sum[8] += me ? dbacc : pv[p][8];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc0[r] = sum[2 * r];
+      acc1[r] = sum[2 * r + 1];
+    }
+    dbacc = sum[8];
+  }
 
   float* Wt = fused_sgd ? P : Gout;
 #pragma unroll
@@ -556,8 +649,19 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
                          int64_t* ctr, int64_t row0, const MlpDesc& d, float lr, int fused_sgd,
                          hipStream_t s) {
   dim3 grid(mlp_wgrad_tiles(d));
-  hipLaunchKernelGGL(mlp_f32_wgrad_k, grid, dim3(64), 0, s, X, ldx, P, G, ws, ctr, row0, d, lr,
-                     fused_sgd);
+  hipLaunchKernelGGL(mlp_f32_wgrad_k<false>, grid, dim3(64), 0, s, X, ldx, P, G, ws, ctr, row0, d,
+                     lr, fused_sgd, XchgArgs{});
+  return hipGetLastError();
+}
+
+hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
+                              const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s) {
+  if (ctr == nullptr || x.tab == nullptr || x.err == nullptr || x.nranks < 1 ||
+      x.nranks > kMaxPeers || x.rank < 0 || x.rank >= x.nranks)
+    return hipErrorInvalidValue;
+  dim3 grid(mlp_wgrad_tiles(d));
+  hipLaunchKernelGGL(mlp_f32_wgrad_k<true>, grid, dim3(64), 0, s, X, ldx, P, nullptr, ws, ctr, 0,
+                     d, lr_over_n, 1, x);
   return hipGetLastError();
 }
 

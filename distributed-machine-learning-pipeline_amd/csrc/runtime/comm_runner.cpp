@@ -231,6 +231,18 @@ void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
   reset_graph();
 }
 
+void MlpRunner::set_exchange(PeerExchange* x) {
+  if (x != nullptr) {
+    if (!x->connected()) throw std::invalid_argument("set_exchange: exchange not connected");
+    if (mom_ != 0.f || wd_ != 0.f)
+      throw std::invalid_argument("the fused xGMI exchange implements plain SGD only");
+    if (x->ntiles() != mlp_wgrad_tiles(d_) || x->half() < b_.nparams)
+      throw std::invalid_argument("set_exchange: exchange buffers sized for another model");
+  }
+  xchg_ = x;
+  reset_graph();
+}
+
 void MlpRunner::set_world_size(int n) {
   if (n < 1) throw std::invalid_argument("world size must be >= 1");
   world_ = n;
@@ -259,6 +271,14 @@ void MlpRunner::enqueue_update(hipStream_t s) {
 }
 
 void MlpRunner::enqueue_step(hipStream_t s) {
+  if (xchg_ != nullptr) {
+    DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, b_.labels, b_.ws, s));
+    DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
+                                    b_.stats, 1, 1.0f / (float)d_.batch, s));
+    DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
+                                      lr_ / (float)xchg_->nranks(), xchg_->args(), s));
+    return;
+  }
   const bool multi = comm_ != nullptr && comm_->nranks() > 1;
   const bool plain = mom_ == 0.f && wd_ == 0.f;
   if (!multi && plain) {

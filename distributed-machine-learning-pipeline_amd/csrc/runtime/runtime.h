@@ -182,6 +182,52 @@ class RcclComm {
 };
 
 // ---------------------------------------------------------------------------
+// Peer exchange buffers for the xGMI-fused gradient all-reduce (dsml.h
+// XchgArgs).  One per replica: [2 x half floats][ntiles flags] in uncached HBM,
+// exported by IPC handle; peers' buffers are opened from their handles (or, for
+// replicas living in one process, referenced directly).
+class PeerExchange {
+ public:
+  PeerExchange(int device, int64_t half_floats, int ntiles);
+  ~PeerExchange();
+  PeerExchange(const PeerExchange&) = delete;
+  PeerExchange& operator=(const PeerExchange&) = delete;
+
+  std::vector<uint8_t> ipc_handle() const;
+  // handles[r] = rank r's ipc_handle() (own entry ignored).
+  void connect_ipc(int rank, const std::vector<std::vector<uint8_t>>& handles);
+  // Replicas of one process (same or peer-accessible devices).
+  void connect_local(int rank, const std::vector<PeerExchange*>& peers);
+  // Zero own flags and the error word (stream-ordered).  Collective in effect:
+  // every rank resets, then all ranks barrier before the next exchange.
+  void reset(hipStream_t s);
+  uint32_t error(hipStream_t s);
+  void set_timeout_ms(double ms);
+  bool connected() const { return args_.tab != nullptr; }
+  const XchgArgs& args() const { return args_; }
+  int nranks() const { return args_.nranks; }
+  int rank() const { return args_.rank; }
+  int ntiles() const { return ntiles_; }
+  int64_t half() const { return half_; }
+  const char* memory_kind() const { return kind_; }
+  float* buf() const { return static_cast<float*>(base_); }
+  uint64_t* flags() const { return reinterpret_cast<uint64_t*>(static_cast<char*>(base_) + flag_off_); }
+
+ private:
+  void publish_table(const XchgTab& t, int rank, int n);
+  int device_;
+  int64_t half_;
+  int ntiles_;
+  size_t flag_off_ = 0, bytes_ = 0;
+  void* base_ = nullptr;
+  const char* kind_ = "";
+  std::vector<void*> opened_;
+  XchgTab* dtab_ = nullptr;
+  uint32_t* err_ = nullptr;
+  XchgArgs args_;
+};
+
+// ---------------------------------------------------------------------------
 // One data-parallel replica's training step.  Buffers are owned by the caller
 // (PyTorch tensors); the runner only records pointers and launch plans.
 struct MlpBuffers {
@@ -204,6 +250,10 @@ class MlpRunner {
   ~MlpRunner();
   void set_comm(RcclComm* c, int algo /*0 = rccl allreduce, 1 = in-house ring*/,
                 int64_t chunk_bytes);
+  // Gradient all-reduce fused into the weight-gradient kernel over xGMI
+  // (plain SGD only).  Takes precedence over the RCCL communicator.
+  void set_exchange(PeerExchange* x);
+  bool exchange_active() const { return xchg_ != nullptr; }
   // Enqueue one full step on stream s (no host sync).
   void enqueue_step(hipStream_t s);
   // Enqueue only fwd/bwd (grads -> G, no update) — used by the DP engine when
@@ -230,6 +280,7 @@ class MlpRunner {
   MlpLaunchCfg cfg_;
   float lr_, mom_, wd_;
   RcclComm* comm_ = nullptr;
+  PeerExchange* xchg_ = nullptr;
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;

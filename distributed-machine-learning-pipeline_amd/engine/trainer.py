@@ -26,7 +26,7 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("rccl", "ring", "torch")
+SYNC_MODES = ("auto", "xgmi", "rccl", "ring", "torch")
 
 
 @dataclass
@@ -44,6 +44,15 @@ class StepStats:
         return 100.0 * self.correct / max(self.count, 1.0)
 
 
+def _xgmi_eligible(ctx: DistContext) -> bool:
+    """All ranks on one node, one GPU each, <= 8: the fused exchange applies."""
+    import os
+
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size))
+    return ctx.device.type == "cuda" and ctx.backend == "nccl" and 1 < ctx.world_size <= 8 \
+        and local == ctx.world_size
+
+
 def _pad_cols(X: torch.Tensor, mult: int = 4) -> torch.Tensor:
     d = X.shape[1]
     if d % mult == 0:
@@ -58,7 +67,8 @@ class MlpTrainer:
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "reference",
                  momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
                  ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
-                 params: Optional[torch.Tensor] = None, external_comm=None):
+                 params: Optional[torch.Tensor] = None, external_comm=None,
+                 capture_collectives: bool = False, xchg_timeout_ms: float = 10000.0):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -87,6 +97,10 @@ class MlpTrainer:
         self.steps_done = 0
         self._stats_cpu = StepStats()
         self.comm = external_comm
+        self.xchg = None
+        self.capture_collectives = capture_collectives
+        self.xchg_timeout_ms = xchg_timeout_ms
+        self.sync_active = "none"
         self.runner = None
         if self.device.type == "cuda":
             self._init_hip(ring_chunk_bytes)
@@ -111,11 +125,80 @@ class MlpTrainer:
                                   self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
                                   self.weight_decay)
         self.runner.set_world_size(self.ctx.world_size)
-        if self.ctx.is_distributed and self.sync in ("rccl", "ring"):
+        self._captured = False
+        if not self.ctx.is_distributed:
+            return
+        if self.sync == "torch":
+            self.sync_active = "torch"
+            return
+        plain = not (self.momentum or self.weight_decay)
+        if self.sync == "xgmi" and not plain:
+            raise ValueError("sync='xgmi' implements plain SGD; use rccl for momentum/weight decay")
+        if self.sync != "xgmi":  # xgmi is strict: no RCCL fallback communicator
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
-        self._captured = False
+            self.sync_active = "ring" if self.sync == "ring" else "rccl"
+        if self.sync == "xgmi" or (self.sync == "auto" and plain and _xgmi_eligible(self.ctx)):
+            self._init_xgmi(strict=self.sync == "xgmi")
+
+    def _init_xgmi(self, strict: bool) -> None:
+        """Set up the fused xGMI exchange, check one step against a
+        torch.distributed all-reduce, and (sync='auto') keep it only if it is
+        also faster than the RCCL step.  Every decision is collective."""
+        from ..parallel import xchg as X
+
+        err = ""
+        try:
+            self.xchg = X.make_peer_exchange(self.ctx, self.layout, self.xchg_timeout_ms)
+            self.runner.set_exchange(self.xchg)
+            diff = X.verify_against_allreduce(self)
+            if not diff <= 1e-5:
+                err = f"self-test mismatch {diff}"
+        except Exception as e:  # noqa: BLE001 - any failure falls back to RCCL
+            err = f"{type(e).__name__}: {e}"
+        bad = self.ctx.all_reduce_scalars(1.0 if err else 0.0, op="max")[0]
+        if not bad and self.sync == "auto":
+            t_x = self._time_steps(20)
+            self.runner.set_exchange(None)
+            t_r = self._time_steps(20)
+            if t_x < t_r:
+                self.runner.set_exchange(self.xchg)
+            log.info("sync auto: xgmi %.1f us/step, rccl %.1f us/step", 1e6 * t_x, 1e6 * t_r)
+        elif bad:
+            if strict:
+                raise RuntimeError(f"xGMI exchange unavailable: {err or 'failed on a peer'}")
+            log.warning("xGMI exchange disabled (%s); using RCCL", err or "failed on a peer")
+            self.runner.set_exchange(None)
+        self.sync_active = "xgmi" if (not bad and self._xchg_on()) else self.sync_active
+        if not self._xchg_on():
+            self.xchg = None
+
+    def _xchg_on(self) -> bool:
+        return bool(self.runner.exchange_active())
+
+    def _time_steps(self, n: int) -> float:
+        """Max-over-ranks wall time per step of `n` eager steps; state restored."""
+        from ..parallel import xchg as X
+
+        P0, ctr0, st0 = self.P.clone(), self.ctr.clone(), self.stats.clone()
+        self.runner.step(2)
+        self.runner.synchronize()
+        self.ctx.barrier()
+        t0 = time.perf_counter()
+        self.runner.step(n)
+        self.runner.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        dt = self.ctx.all_reduce_scalars(dt, op="max")[0]
+        self.P.copy_(P0)
+        self.ctr.copy_(ctr0)
+        self.stats.copy_(st0)
+        if self.xchg is not None:
+            X.reset_group(self.ctx, self.xchg)
+        else:
+            torch.cuda.synchronize(self.device)
+            self.ctx.barrier()
+        return dt
 
     def _hip_step_torch_sync(self, n: int) -> None:
         import torch.distributed as dist
@@ -137,9 +220,10 @@ class MlpTrainer:
                 self._torch_step()
                 self.steps_done += 1
             return
-        if self.ctx.is_distributed and self.sync == "torch":
+        collective_in_step = self.ctx.is_distributed and self.sync_active in ("rccl", "ring")
+        if self.ctx.is_distributed and self.sync_active == "torch":
             self._hip_step_torch_sync(n)
-        elif self.graph_steps > 0:
+        elif self.graph_steps > 0 and (self.capture_collectives or not collective_in_step):
             if not self._captured:
                 self.runner.capture(self.graph_steps, True)
                 self._captured = True
@@ -155,6 +239,10 @@ class MlpTrainer:
     def synchronize(self) -> None:
         if self.runner is not None:
             self.runner.synchronize()
+            if self.xchg is not None:
+                from ..parallel.xchg import check
+
+                check(self.xchg)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
@@ -275,6 +363,10 @@ class MlpTrainer:
             # A = B = s at the start of step s (dsml.h step-counter protocol)
             self.ctr.fill_(self.steps_done)
             torch.cuda.synchronize(self.device)
+            if self.xchg is not None:  # flags may be ahead of the restored step
+                from ..parallel.xchg import reset_group
+
+                reset_group(self.ctx, self.xchg)
 
     def fit(self, epochs: int, log_fn=None, test: Optional[Dataset] = None) -> Dict[str, float]:
         """Reference-compatible epoch loop (client.go:579-653 log lines)."""

@@ -33,7 +33,7 @@ class DistContext:
 
     @classmethod
     def from_env(cls, device: str = "auto", backend: Optional[str] = None,
-                 timeout_s: float = 600.0) -> "DistContext":
+                 timeout_s: float = 600.0, device_index: Optional[int] = None) -> "DistContext":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -42,8 +42,9 @@ class DistContext:
         else:
             use_gpu = device.startswith("cuda")
         if use_gpu:
-            torch.cuda.set_device(local)
-            dev = torch.device("cuda", local)
+            idx = local if device_index is None else device_index
+            torch.cuda.set_device(idx)
+            dev = torch.device("cuda", idx)
         else:
             dev = torch.device("cpu")
         ctx = cls(rank=rank, world_size=world, local_rank=local, device=dev)
@@ -77,8 +78,8 @@ class DistContext:
 
     def barrier(self) -> None:
         if self.is_distributed:
-            if self.device.type == "cuda":
-                dist.barrier(device_ids=[self.local_rank])
+            if self.device.type == "cuda" and self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
 
@@ -92,6 +93,14 @@ class DistContext:
             assert value is not None
             store.set(key, value)
         return bytes(store.get(key))
+
+    def all_gather_bytes(self, key: str, value: bytes) -> list:
+        """Every rank publishes `value`; returns all ranks' values in rank order."""
+        if not self.is_distributed:
+            return [value]
+        store = dist.distributed_c10d._get_default_store()
+        store.set(f"{key}/{self.rank}", value)
+        return [bytes(store.get(f"{key}/{r}")) for r in range(self.world_size)]
 
     def destroy(self) -> None:
         if self.initialized_here and dist.is_initialized():
@@ -112,4 +121,4 @@ def make_native_comm(ctx: DistContext, blocking: bool = True):
     key = f"hipdsml/rccl_uid/{_uid_counter}"
     uid = C.rccl_unique_id() if ctx.rank == 0 else None
     uid = ctx.share_bytes(key, uid)
-    return C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.local_rank, blocking)
+    return C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.device.index, blocking)

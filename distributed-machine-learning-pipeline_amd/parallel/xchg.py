@@ -1,0 +1,118 @@
+"""xGMI peer exchange: the gradient all-reduce fused into the weight-gradient
+kernel (``csrc/kernels/mlp_f32.hip`` XCHG path, ``csrc/runtime/peer_exchange.cpp``).
+
+Why: the flagship gradient is 437 KB.  At that size an all-reduce is pure
+latency — a ring (the reference's algorithm, ``gpu_coordinator_server.go:338-356``,
+or RCCL's) pays 2(N-1) hops, plus a kernel boundary before and after.  On an
+MI355X node every GPU has a direct xGMI link to every other, so each replica
+can instead read all peers' gradient tiles directly (one-shot) inside the
+kernel that produced its own, sum them in rank order and apply SGD — no
+collective launch, no extra kernel, and the step stays hipGraph-capturable.
+
+Bootstrap (collective over the process group): every rank allocates an
+uncached exchange buffer, publishes its IPC handle through the TCP store,
+opens the peers' handles, zeroes its flags, then all ranks barrier.
+"""
+from __future__ import annotations
+
+import logging
+from typing import List, Optional
+
+import torch
+
+from ..models.mlp import MlpLayout
+from .dist import DistContext
+
+log = logging.getLogger("hipdsml.xchg")
+
+_key = 0
+
+
+def wgrad_tiles(layout: MlpLayout) -> int:
+    d = layout.spec.dims
+    return sum(((d[l + 1] + 15) // 16) * ((d[l] + 31) // 32) for l in range(len(d) - 1))
+
+
+def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 10000.0):
+    """Collective: returns a connected ``_C.PeerExchange`` for this rank."""
+    from ..ops.native import require_native
+
+    global _key
+    C = require_native()
+    if ctx.world_size > 8:
+        raise ValueError("the xGMI exchange spans one node (<= 8 GPUs)")
+    x = C.PeerExchange(ctx.device.index, layout.nparams, wgrad_tiles(layout))
+    x.set_timeout_ms(timeout_ms)
+    _key += 1
+    handles = ctx.all_gather_bytes(f"hipdsml/xchg/{_key}", x.ipc_handle())
+    x.connect_ipc(ctx.rank, handles)
+    x.reset()
+    torch.cuda.synchronize(ctx.device)
+    ctx.barrier()
+    log.info("peer exchange: rank %d/%d, %s memory, %d tiles", ctx.rank, ctx.world_size,
+             x.memory_kind, x.ntiles)
+    return x
+
+
+def make_local_group(layout: MlpLayout, devices: List[int], timeout_ms: float = 10000.0):
+    """Exchanges for N replicas living in ONE process (tests / single-process
+    multi-GPU): peers are referenced directly instead of through IPC."""
+    from ..ops.native import require_native
+
+    C = require_native()
+    xs = [C.PeerExchange(dev, layout.nparams, wgrad_tiles(layout)) for dev in devices]
+    for r, x in enumerate(xs):
+        x.set_timeout_ms(timeout_ms)
+        x.connect_local(r, xs)
+    return xs
+
+
+def reset_group(ctx: DistContext, x) -> None:
+    """Collective flag reset (after a resume or a self-test rewound the step
+    counter): nobody may still be reading when the flags go back to zero."""
+    torch.cuda.synchronize(ctx.device)
+    ctx.barrier()
+    x.reset()
+    torch.cuda.synchronize(ctx.device)
+    ctx.barrier()
+
+
+def check(x, where: str = "") -> None:
+    if x is not None and x.error():
+        raise RuntimeError(f"xGMI peer exchange timed out waiting for a peer{where}: "
+                           "a replica stopped or fell behind")
+
+
+def verify_against_allreduce(trainer, tol: float = 1e-6) -> Optional[float]:
+    """One step through the exchange vs. the same step with a torch.distributed
+    all-reduce; restores the trainer state afterwards.  Returns the max abs
+    difference (all ranks) — replicas must also agree bit-for-bit."""
+    import torch.distributed as dist
+
+    ctx = trainer.ctx
+    r = trainer.runner
+    P0, ctr0, st0 = trainer.P.clone(), trainer.ctr.clone(), trainer.stats.clone()
+    r.fwd_bwd()
+    r.synchronize()
+    g = trainer.G.clone()
+    dist.all_reduce(g)
+    want = P0 - (trainer.lr / ctx.world_size) * g
+    trainer.ctr.copy_(ctr0)
+    torch.cuda.synchronize(ctx.device)
+    r.step(1)
+    r.synchronize()
+    check(trainer.xchg, " (self-test)")
+    diff = (trainer.P - want).abs().max().reshape(1)
+    ref = trainer.P.clone()
+    dist.broadcast(ref, 0)
+    mismatch = (trainer.P != ref).any().float().reshape(1)
+    stats = torch.cat([diff, mismatch])
+    dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    trainer.P.copy_(P0)
+    trainer.ctr.copy_(ctr0)
+    trainer.stats.copy_(st0)
+    reset_group(ctx, trainer.xchg)
+    d, mm = stats.tolist()
+    if mm:
+        return float("inf")
+    return d

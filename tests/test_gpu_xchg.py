@@ -1,0 +1,105 @@
+"""xGMI peer exchange (gradient all-reduce fused into the weight-gradient
+kernel) on ONE MI355X: N replicas share the GPU, either inside one process
+(pointers exchanged directly) or as separate processes (IPC handles) — the
+same kernel and flag protocol that runs across GPUs of a node."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from hipdsml.data.mnist import synthetic_mnist
+from hipdsml.engine.trainer import MlpTrainer
+from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
+from hipdsml.parallel.dist import DistContext
+from hipdsml.parallel.xchg import make_local_group
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+DIMS = (784, 128, 64, 10)
+
+
+def _reference(world, steps, lr, nb, seed=7):
+    lay = MlpLayout(MlpSpec(DIMS), 64, nb)
+    P = init_params(lay, seed, "reference")
+    shards = [synthetic_mnist(64 * nb, seed=300 + r) for r in range(world)]
+    for s in range(steps):
+        b = s % nb
+        g = None
+        for sh in shards:
+            gi = grads_ref(lay, P, sh.X[b * 64:(b + 1) * 64], sh.y[b * 64:(b + 1) * 64])[0]
+            g = gi if g is None else g + gi
+        P = P - lr * g / world
+    return P
+
+
+def _local_group(world, nb, graph_steps, timeout_ms=5000.0):
+    trs = [MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * nb, seed=300 + r), batch=64, lr=0.05,
+                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps)
+           for r in range(world)]
+    xs = make_local_group(trs[0].layout, [0] * world, timeout_ms)
+    for t, x in zip(trs, xs):
+        t.runner.set_exchange(x)
+        t.xchg = x
+    return trs, xs
+
+
+@pytest.mark.parametrize("world,graph_steps", [(2, 0), (3, 0), (2, 5)])
+def test_local_group_matches_reference(world, graph_steps):
+    nb, steps = 4, 10
+    trs, xs = _local_group(world, nb, graph_steps)
+    for chunk in (5, 5):
+        for t in trs:
+            t.train_steps(chunk)
+        for t in trs:
+            t.synchronize()  # raises if a peer timed out
+    Ps = [t.P.cpu() for t in trs]
+    for P in Ps[1:]:
+        assert torch.equal(P, Ps[0])  # replicas bit-identical (rank-order sums)
+    want = _reference(world, steps, 0.05, nb)
+    err = (Ps[0] - want).abs().max().item()
+    assert err < 2e-5, err
+    assert xs[0].memory_kind in ("uncached", "finegrained", "coarse")
+
+
+def test_missing_peer_times_out_instead_of_hanging():
+    trs, xs = _local_group(2, 2, 0, timeout_ms=200.0)
+    trs[0].train_steps(1)  # rank 1 never runs
+    with pytest.raises(RuntimeError, match="timed out"):
+        trs[0].synchronize()
+    xs[0].reset()
+    torch.cuda.synchronize()
+    assert xs[0].error() == 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ipc_worker(rank, world, port, outdir, graph_steps):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    ctx = DistContext.from_env(device="cuda", backend="gloo")
+    tr = MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * 4, seed=300 + rank), batch=64, lr=0.05,
+                    ctx=ctx, seed=7, sync="xgmi", graph_steps=graph_steps, xchg_timeout_ms=5000.0)
+    assert tr.sync_active == "xgmi"
+    tr.train_steps(6)
+    tr.synchronize()
+    torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+@pytest.mark.parametrize("graph_steps", [0, 3])
+def test_two_processes_ipc(graph_steps):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps), nprocs=world,
+                           start_method="spawn", join=True)
+        Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
+    assert torch.equal(Ps[0], Ps[1])
+    err = (Ps[0] - _reference(world, 6, 0.05, 4)).abs().max().item()
+    assert err < 2e-5, err
