@@ -41,7 +41,9 @@ def cmd_device_server(a) -> int:
     ids = [int(i) for i in a.device_ids.split(",")] if a.device_ids else list(range(1, len(ports) + 1))
     servers = []
     for port, gpu, did in zip(ports, gpus, ids):
-        server, addr, _ = start_device_server(did, a.mem_size, f"{a.host}:{port}", backend=a.backend, gpu=gpu)
+        server, addr, svc = start_device_server(did, a.mem_size, f"{a.host}:{port}", backend=a.backend, gpu=gpu)
+        if a.fail_after and did == (a.fail_device or did):
+            svc.arm_fault(a.fail_after, a.fail_mode)
         print(f"GPU Device server listening on port {addr.rsplit(':', 1)[1]} with device ID {did}", flush=True)
         servers.append(server)
     _serve_forever([lambda s=s: s.stop(1) for s in servers])
@@ -147,6 +149,10 @@ def main(argv=None) -> int:
     d.add_argument("--device-ids", default="")
     d.add_argument("--backend", default="auto", choices=["auto", "host", "hip"])
     d.add_argument("--mem-size", type=int, default=64 << 20)
+    d.add_argument("--fail-after", type=int, default=0,
+                   help="fault injection: die on the N-th data-plane RPC (0 = never)")
+    d.add_argument("--fail-device", type=int, default=0, help="only this device id (0 = all)")
+    d.add_argument("--fail-mode", default="exit", choices=["exit", "stop"])
     c = sub.add_parser("coordinator")
     c.add_argument("--host", default="127.0.0.1")
     c.add_argument("--port", type=int, default=50051)

@@ -151,13 +151,14 @@ class MlpTrainer:
         err = ""
         try:
             self.xchg = X.make_peer_exchange(self.ctx, self.layout, self.xchg_timeout_ms)
+        except X.ExchangeUnavailable as e:  # agreed on every rank
+            err = str(e)
+        if not err:
             self.runner.set_exchange(self.xchg)
-            diff = X.verify_against_allreduce(self)
+            diff = X.verify_against_allreduce(self)  # collective, same result on all ranks
             if not diff <= 1e-5:
                 err = f"self-test mismatch {diff}"
-        except Exception as e:  # noqa: BLE001 - any failure falls back to RCCL
-            err = f"{type(e).__name__}: {e}"
-        bad = self.ctx.all_reduce_scalars(1.0 if err else 0.0, op="max")[0]
+        bad = bool(err)
         if not bad and self.sync == "auto":
             t_x = self._time_steps(20)
             self.runner.set_exchange(None)

@@ -33,22 +33,42 @@ def wgrad_tiles(layout: MlpLayout) -> int:
     return sum(((d[l + 1] + 15) // 16) * ((d[l] + 31) // 32) for l in range(len(d) - 1))
 
 
+class ExchangeUnavailable(RuntimeError):
+    pass
+
+
 def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 10000.0):
-    """Collective: returns a connected ``_C.PeerExchange`` for this rank."""
+    """Collective: returns a connected ``_C.PeerExchange`` for this rank, or
+    raises :class:`ExchangeUnavailable` on EVERY rank if any rank failed (the
+    outcome is agreed before anyone leaves, so no rank is left in a collective)."""
     from ..ops.native import require_native
 
     global _key
     C = require_native()
+    x, err, h = None, "", b""
     if ctx.world_size > 8:
-        raise ValueError("the xGMI exchange spans one node (<= 8 GPUs)")
-    x = C.PeerExchange(ctx.device.index, layout.nparams, wgrad_tiles(layout))
-    x.set_timeout_ms(timeout_ms)
+        err = "the xGMI exchange spans one node (<= 8 GPUs)"
+    else:
+        try:
+            x = C.PeerExchange(ctx.device.index, layout.nparams, wgrad_tiles(layout))
+            x.set_timeout_ms(timeout_ms)
+            h = x.ipc_handle()
+        except Exception as e:  # noqa: BLE001
+            err = f"allocation/export: {e}"
     _key += 1
-    handles = ctx.all_gather_bytes(f"hipdsml/xchg/{_key}", x.ipc_handle())
-    x.connect_ipc(ctx.rank, handles)
-    x.reset()
-    torch.cuda.synchronize(ctx.device)
-    ctx.barrier()
+    handles = ctx.all_gather_bytes(f"hipdsml/xchg/{_key}", h)  # every rank publishes
+    if not err and any(len(hh) == 0 for hh in handles):
+        err = "a peer could not allocate its exchange buffer"
+    if not err:
+        try:
+            x.connect_ipc(ctx.rank, handles)
+            x.reset()
+            torch.cuda.synchronize(ctx.device)
+        except Exception as e:  # noqa: BLE001
+            err = f"connect: {e}"
+    ok = ctx.all_reduce_scalars(0.0 if err else 1.0, op="min")[0]
+    if not ok:
+        raise ExchangeUnavailable(err or "failed on a peer")
     log.info("peer exchange: rank %d/%d, %s memory, %d tiles", ctx.rank, ctx.world_size,
              x.memory_kind, x.ntiles)
     return x
@@ -83,10 +103,11 @@ def check(x, where: str = "") -> None:
                            "a replica stopped or fell behind")
 
 
-def verify_against_allreduce(trainer, tol: float = 1e-6) -> Optional[float]:
+def verify_against_allreduce(trainer, tol: float = 1e-6) -> float:
     """One step through the exchange vs. the same step with a torch.distributed
     all-reduce; restores the trainer state afterwards.  Returns the max abs
-    difference (all ranks) — replicas must also agree bit-for-bit."""
+    difference over all ranks (inf if replicas disagree bit-wise or a peer
+    timed out).  Every rank runs the same collectives whatever happens locally."""
     import torch.distributed as dist
 
     ctx = trainer.ctx
@@ -101,18 +122,16 @@ def verify_against_allreduce(trainer, tol: float = 1e-6) -> Optional[float]:
     torch.cuda.synchronize(ctx.device)
     r.step(1)
     r.synchronize()
-    check(trainer.xchg, " (self-test)")
+    timed_out = float(trainer.xchg.error() != 0)
     diff = (trainer.P - want).abs().max().reshape(1)
     ref = trainer.P.clone()
     dist.broadcast(ref, 0)
     mismatch = (trainer.P != ref).any().float().reshape(1)
-    stats = torch.cat([diff, mismatch])
+    stats = torch.cat([diff, mismatch, torch.tensor([timed_out], device=diff.device)])
     dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     trainer.P.copy_(P0)
     trainer.ctr.copy_(ctr0)
     trainer.stats.copy_(st0)
     reset_group(ctx, trainer.xchg)
-    d, mm = stats.tolist()
-    if mm:
-        return float("inf")
-    return d
+    d, mm, to = stats.tolist()
+    return float("inf") if (mm or to or d != d) else d

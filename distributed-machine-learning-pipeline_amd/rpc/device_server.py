@@ -40,6 +40,42 @@ class GPUDeviceServicer:
         self._fwd_cache = None
         self.counters = {"h2d_bytes": 0, "d2h_bytes": 0, "stream_bytes_in": 0,
                          "stream_bytes_out": 0, "reduces": 0, "allreduces": 0, "train_steps": 0}
+        self.server = None          # set by start_device_server (fault injection stops it)
+        self._fault_left: Optional[int] = None
+        self._fault_mode = "stop"
+        self.failed = False
+
+    # ------------------------------------------------------ fault injection --
+    def arm_fault(self, after_rpcs: int, mode: str = "stop") -> None:
+        """BASELINE config 5 hook: die on the `after_rpcs`-th data-plane RPC
+        (BeginSend / BeginReceive / StreamSend / Memcpy / Reduce / DeviceAllReduce).
+        mode "stop": stop the gRPC server (in-process clusters, like the
+        reference test's ``grpcServer.Stop()``, gpu_coordinator_server_test.go:415);
+        "exit": terminate the process abruptly (a crashed device server)."""
+        if mode not in ("stop", "exit"):
+            raise ValueError("fault mode must be 'stop' or 'exit'")
+        self._fault_left, self._fault_mode = int(after_rpcs), mode
+
+    def _tick(self, context) -> None:
+        if self.failed:
+            context.abort(grpc.StatusCode.UNAVAILABLE, "device failed (fault injection)")
+        if self._fault_left is None:
+            return
+        with self._lock:
+            self._fault_left -= 1
+            fire = self._fault_left <= 0
+        if not fire:
+            return
+        self.failed = True
+        self._fault_left = None
+        log.warning("%s: injected fault (%s)", self.name, self._fault_mode)
+        if self._fault_mode == "exit":
+            import os
+
+            os._exit(17)
+        if self.server is not None:
+            threading.Thread(target=self.server.stop, args=(0,), daemon=True).start()
+        context.abort(grpc.StatusCode.UNAVAILABLE, "device failed (fault injection)")
 
     # ------------------------------------------------------------ helpers --
     def _peer(self, address: str) -> GPUDeviceStub:
@@ -77,6 +113,7 @@ class GPUDeviceServicer:
         return pb.GetDeviceMetadataResponse(metadata=md)
 
     def BeginSend(self, request, context):
+        self._tick(context)
         addr, n = request.sendBuffAddr.value, request.numBytes
         sid = self.dev.begin_send(addr, n, request.dstRank.value)
         if request.dstAddress:
@@ -89,6 +126,7 @@ class GPUDeviceServicer:
         return pb.BeginSendResponse(initiated=True, streamId=pb.StreamId(value=sid))
 
     def BeginReceive(self, request, context):
+        self._tick(context)
         sid = request.streamId.value
         own = (sid >> 32) == self.dev.device_id
         if own and self.dev.stream(sid) is None:
@@ -101,6 +139,7 @@ class GPUDeviceServicer:
         return pb.BeginReceiveResponse(initiated=True)
 
     def StreamSend(self, request_iterator, context):
+        self._tick(context)
         first = next(request_iterator, None)
         if first is None or first.streamId == 0:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, "stream ID not provided")
@@ -122,6 +161,7 @@ class GPUDeviceServicer:
         return pb.GetStreamStatusResponse(status=self.dev.stream_status(request.streamId.value))
 
     def Memcpy(self, request, context):
+        self._tick(context)
         which = request.WhichOneof("either")
         if which == "hostToDevice":
             r = request.hostToDevice
@@ -153,6 +193,7 @@ class GPUDeviceServicer:
         return pb.WaitStreamResponse(status=self.dev.wait_stream(request.streamId.value, tmo))
 
     def Reduce(self, request, context):
+        self._tick(context)
         if request.waitStreamId:
             st = self.dev.wait_stream(request.waitStreamId, 120.0)
             if st != STATUS_SUCCESS:
@@ -276,6 +317,7 @@ class GPUDeviceServicer:
         del chunk
 
     def DeviceAllReduce(self, request, context):
+        self._tick(context)
         comm = self.comms.get(request.commId)
         if comm is None and request.commId in self.comm_meta:
             es = DT_SIZE.get(request.dtype, 0)
@@ -492,5 +534,6 @@ def start_device_server(device_id: int, mem_size: int, address: str = "127.0.0.1
     dev = make_device(device_id, mem_size, backend, gpu=gpu)
     svc = GPUDeviceServicer(dev)
     server, addr = serve("GPUDevice", svc, address, max_workers=max_workers)
+    svc.server = server
     log.info("GPU Device server listening on %s with device ID %d (%s)", addr, device_id, dev.backend)
     return server, addr, svc

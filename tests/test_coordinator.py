@@ -231,3 +231,81 @@ def test_device_failure_during_allreduce_fails_fast(algo):
         with pytest.raises(grpc.RpcError) as e:
             c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=16))
         assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+
+
+@pytest.mark.parametrize("algo", ["device-ring", "coordinator-ring"])
+def test_device_dies_mid_allreduce_fails_fast(algo):
+    """BASELINE config 5 proper: the fault fires INSIDE AllReduceRing (rank 2
+    stops on its 3rd data-plane RPC, i.e. mid-ring), not before it."""
+    n = 3
+    with cluster(n_devices=n, mem_size=1 << 20, rpc_timeout=60.0) as c:
+        cid = c.comm_init().commId
+        for i in range(n):
+            c.devices[i][2].dev.write(0x1000, np.ones(4096, np.float32).tobytes())
+        c.devices[2][2].arm_fault(3, "stop")
+        t0 = time.time()
+        with pytest.raises(grpc.RpcError) as e:
+            c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=4096 * 4, algo=algo))
+        assert time.time() - t0 < 20.0
+        assert e.value.code() == grpc.StatusCode.INTERNAL
+        assert c.devices[2][2].failed
+        assert _status(c, cid) == FAILED
+
+
+def test_crashed_device_process_detected(tmp_path):
+    """A device-server PROCESS configured with --fail-after crashes (os._exit)
+    during the ring; the all-reduce errors out and the health monitor keeps the
+    communicator FAILED."""
+    import subprocess
+    import sys
+
+    from hipdsml.cli import child_env
+    from hipdsml.rpc.coordinator import start_coordinator
+
+    ports = []
+    for _ in range(3):
+        import socket
+
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            ports.append(s.getsockname()[1])
+    procs = []
+    try:
+        for i, p in enumerate(ports):
+            extra = ["--fail-after", "4", "--fail-mode", "exit"] if i == 1 else []
+            procs.append(subprocess.Popen(
+                [sys.executable, "-m", "hipdsml", "device-server", "--ports", str(p),
+                 "--device-ids", str(i + 1), "--backend", "host", "--mem-size", str(1 << 20)] + extra,
+                env=child_env(), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        server, addr, svc = start_coordinator(health_interval=0.3, health_timeout=0.5)
+        try:
+            from hipdsml.rpc.stubs import GPUCoordinatorStub, connect
+
+            stub = GPUCoordinatorStub(connect(addr, timeout=10))
+            addrs = [f"127.0.0.1:{p}" for p in ports]
+            deadline = time.time() + 120
+            while True:
+                try:
+                    cid = stub.CommInit(pb.CommInitRequest(numDevices=3, device_addresses=addrs)).commId
+                    break
+                except grpc.RpcError:
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.5)
+            with pytest.raises(grpc.RpcError):
+                stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=1 << 16), timeout=60)
+            assert procs[1].wait(timeout=30) == 17
+            time.sleep(1.0)
+            st = stub.GetCommStatus(pb.GetCommStatusRequest(commId=cid)).status
+            assert st == FAILED
+        finally:
+            svc.stop()
+            server.stop(0)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()

@@ -104,3 +104,27 @@ def test_rccl_backend_single_device_comm():
         got = np.frombuffer(c.devices[0][2].dev.read(0x1000, 4096), dtype=np.float32)
         assert np.array_equal(got, data)
         assert stub.Abort(pb.AbortRequest(commId=cid, reason="test")).success
+
+
+def test_hip_device_dies_mid_allreduce():
+    """BASELINE config 5 on HBM-backed devices: rank 1 fails inside the ring;
+    the call fails fast, the survivors' pending streams are failed (no hang)
+    and the communicator is FAILED."""
+    import time
+
+    import grpc
+
+    n = 3
+    with cluster(n_devices=n, mem_size=8 << 20, backend="hip", rpc_timeout=60.0) as c:
+        cid = c.comm_init().commId
+        for i in range(n):
+            c.devices[i][2].dev.write(0x1000, np.ones(1 << 18, np.float32).tobytes())
+        c.devices[1][2].arm_fault(4, "stop")
+        t0 = time.time()
+        with pytest.raises(grpc.RpcError):
+            c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=4 << 18, dtype=DT_FLOAT32))
+        assert time.time() - t0 < 20.0
+        st = c.stub.GetCommStatus(pb.GetCommStatusRequest(commId=cid)).status
+        from hipdsml.rpc.proto import FAILED
+
+        assert st == FAILED
