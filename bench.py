@@ -26,6 +26,41 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 BASELINE_SAMPLES_PER_S = 819.0  # 599,680 samples / 732 s
 
 
+def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200) -> dict:
+    """Device all-reduce latency of a `nbytes` fp32 buffer across the job's GPUs
+    (the BASELINE's second metric, ring all-reduce at 1 MiB): RCCL's
+    ncclAllReduce and the one-shot xGMI peer all-reduce.  Max over ranks."""
+    import torch
+
+    from hipdsml.parallel.xchg import ExchangeUnavailable, XgmiAllReduce
+
+    out = {}
+    t = torch.zeros(nbytes // 4, device=ctx.device)
+
+    def timed(fn):
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        return round(1e6 * ctx.all_reduce_scalars(dt, op="max")[0], 2)
+
+    if comm is not None:
+        out["rccl"] = timed(lambda: comm.allreduce_(t, 0))
+    try:
+        ar = XgmiAllReduce(ctx, t.numel())
+    except ExchangeUnavailable as e:
+        out["xgmi_error"] = str(e)[:200]
+    else:
+        out["xgmi"] = timed(lambda: ar(t))
+        ar.check()
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,6 +76,8 @@ def main() -> int:
                     help="steps captured per hipGraph (0 = eager C++ launch loop); steps with an "
                          "RCCL collective always run as the eager C++ loop")
     ap.add_argument("--samples-per-rank", type=int, default=60032)
+    ap.add_argument("--no-allreduce-probe", action="store_true",
+                    help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
                          "two ranks on one GPU); use with --sync xgmi or torch")
@@ -79,6 +116,7 @@ def main() -> int:
     elapsed = ctx.all_reduce_scalars(elapsed, op="max")[0] if ctx.is_distributed else elapsed
     st = tr.read_stats(global_=True)
     n = ctx.world_size
+    ar_us = allreduce_latency_us(ctx, tr.comm) if n > 1 and not a.no_allreduce_probe else None
     samples = a.batch * n * a.steps
     value = samples / elapsed
     if ctx.rank == 0:
@@ -104,6 +142,7 @@ def main() -> int:
                 "graph_steps": a.graph_steps,
                 "lr": a.lr,
             },
+            "allreduce_1MiB_us": ar_us,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
         }

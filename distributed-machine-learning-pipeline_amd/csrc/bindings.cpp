@@ -467,6 +467,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return x.error(cur_stream());
       })
       .def("set_timeout_ms", &PeerExchange::set_timeout_ms)
+      .def("allreduce_", [](PeerExchange& x, torch::Tensor t) {
+        check_f32(t, "tensor");
+        x.allreduce(t.data_ptr<float>(), t.data_ptr<float>(), t.numel(), cur_stream());
+        return t;
+      })
+      .def("allreduce", [](PeerExchange& x, torch::Tensor in, torch::Tensor out) {
+        check_f32(in, "in");
+        check_f32(out, "out");
+        TORCH_CHECK(in.numel() == out.numel(), "in/out size mismatch");
+        x.allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cur_stream());
+        return out;
+      })
       .def_property_readonly("nranks", &PeerExchange::nranks)
       .def_property_readonly("rank", &PeerExchange::rank)
       .def_property_readonly("ntiles", &PeerExchange::ntiles)

@@ -102,6 +102,12 @@ struct XchgArgs {
   uint64_t timeout_ticks = 0;    // s_memrealtime ticks (100 MHz)
 };
 int mlp_wgrad_tiles(const MlpDesc& d);
+// Standalone one-shot all-reduce (sum) of n fp32 (n % 4 == 0, n <= x.half)
+// through the exchange buffers (kernels/xchg.hip).  `seq` >= 1 numbers the
+// calls (monotonic per exchange; parity selects the buffer half).
+int xchg_allreduce_blocks(int64_t n, int max_blocks, int* unroll);
+hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
+                              int max_blocks, uint64_t seq, hipStream_t s);
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
                               const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
 

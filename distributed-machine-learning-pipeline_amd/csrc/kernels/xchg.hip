@@ -1,0 +1,147 @@
+// One-shot all-reduce over xGMI peer memory (standalone buffers).
+//
+// The same protocol as the exchange fused into the MLP weight-gradient kernel
+// (mlp_f32.hip, XCHG path), for arbitrary fp32 buffers: every rank copies its
+// input into its own IPC-shared, uncached exchange buffer (parity = call & 1),
+// raises one flag per workgroup chunk, waits for the same chunk's flag of every
+// peer, reads the peers' chunks directly over xGMI and writes the rank-ordered
+// sum.  One kernel, one synchronisation round, N-1 concurrent links: the
+// latency-optimal shape for the small (<= a few MiB) messages of MLP training,
+// where a ring pays 2(N-1) dependent hops (reference ring: 2(n-1) gRPC rounds,
+// gpu_coordinator_server.go:338-356).
+#include "common.h"
+#include "../dsml.h"
+
+namespace dsml {
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint64_t gu64x;
+// System-coherent 16 B accesses as two 8 B relaxed atomics (global_*_dwordx2
+// sc0 sc1): compiler-visible, so the usual waitcnt tracking applies.
+__device__ __forceinline__ float4 ld_sys4(const float* p) {
+  const gu64x* q = (const gu64x*)p;
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                     __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+}
+__device__ __forceinline__ void st_sys4(float* p, float4 v) {
+  gu64x* q = (gu64x*)p;
+  const uint64_t a = (uint64_t)__float_as_uint(v.x) | ((uint64_t)__float_as_uint(v.y) << 32);
+  const uint64_t b = (uint64_t)__float_as_uint(v.z) | ((uint64_t)__float_as_uint(v.w) << 32);
+  __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_flag(const uint64_t* p) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) uint64_t*)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_flag(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)p, v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr int kXThreads = 256;
+
+// Each thread owns U float4s of the workgroup's chunk (strided by the block).
+template <int U>
+__global__ __launch_bounds__(kXThreads) void xchg_allreduce_k(const float* __restrict__ in,
+                                                              float* __restrict__ out, int64_t n,
+                                                              XchgArgs xa, uint64_t seq) {
+  const int64_t chunk = (int64_t)kXThreads * 4 * U;
+  const int64_t base = (int64_t)blockIdx.x * chunk;
+  const int64_t poff = (int64_t)(seq & 1) * xa.half;
+  const XchgTab* __restrict__ tab = xa.tab;
+  float* mine = tab->buf[xa.rank] + poff;
+  float4 own[U];
+  // n is a multiple of 4 (checked on the host): whole float4s only.
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+    own[u] = i < n ? *reinterpret_cast<const float4*>(in + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+    if (i < n) st_sys4(mine + i, own[u]);
+  }
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) st_flag(tab->flags[xa.rank] + blockIdx.x, seq);
+  if (threadIdx.x < xa.nranks && threadIdx.x != xa.rank) {
+    const uint64_t* f = tab->flags[threadIdx.x] + blockIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_flag(f) < seq) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+        __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  float4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Rank-ordered sum (identical on every rank).
+  for (int p = 0; p < xa.nranks; ++p) {
+    float4 v[U];
+    if (p == xa.rank) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = own[u];
+    } else {
+      const float* pb = tab->buf[p] + poff;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+        v[u] = ld_sys4(pb + (i < n ? i : 0));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[u].x += v[u].x;
+      acc[u].y += v[u].y;
+      acc[u].z += v[u].z;
+      acc[u].w += v[u].w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+    if (i < n) *reinterpret_cast<float4*>(out + i) = acc[u];
+  }
+}
+
+}  // namespace
+
+int xchg_allreduce_blocks(int64_t n, int max_blocks, int* unroll) {
+  // Prefer >= 256 workgroups (one per CU) for latency; grow U when the flag
+  // table would be exceeded.
+  for (int u : {1, 2, 4, 8}) {
+    const int64_t chunk = (int64_t)kXThreads * 4 * u;
+    const int64_t g = (n + chunk - 1) / chunk;
+    if (g <= max_blocks) {
+      *unroll = u;
+      return (int)(g < 1 ? 1 : g);
+    }
+  }
+  return -1;
+}
+
+hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
+                              int max_blocks, uint64_t seq, hipStream_t s) {
+  if (n % 4 || x.tab == nullptr || n > x.half || seq == 0) return hipErrorInvalidValue;
+  int u = 0;
+  const int g = xchg_allreduce_blocks(n, max_blocks, &u);
+  if (g < 0) return hipErrorInvalidValue;
+  switch (u) {
+    case 1: hipLaunchKernelGGL(xchg_allreduce_k<1>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
+    case 2: hipLaunchKernelGGL(xchg_allreduce_k<2>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
+    case 4: hipLaunchKernelGGL(xchg_allreduce_k<4>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
+    default: hipLaunchKernelGGL(xchg_allreduce_k<8>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dsml

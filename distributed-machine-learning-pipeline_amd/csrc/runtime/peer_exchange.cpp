@@ -119,7 +119,17 @@ void PeerExchange::connect_local(int rank, const std::vector<PeerExchange*>& pee
   publish_table(t, rank, n);
 }
 
+void PeerExchange::allreduce(const float* in, float* out, int64_t n, hipStream_t s) {
+  if (!connected()) throw std::runtime_error("PeerExchange::allreduce: not connected");
+  if (n % 4 || n > half_)
+    throw std::invalid_argument("PeerExchange::allreduce: n must be a multiple of 4 and <= " +
+                                std::to_string(half_));
+  DSML_HIP_CHECK(hipSetDevice(device_));
+  DSML_HIP_CHECK(xchg_allreduce_f32(in, out, n, args_, ntiles_, ++seq_, s));
+}
+
 void PeerExchange::reset(hipStream_t s) {
+  seq_ = 0;
   DSML_HIP_CHECK(hipSetDevice(device_));
   DSML_HIP_CHECK(hipMemsetAsync(flags(), 0, (size_t)ntiles_ * sizeof(uint64_t), s));
   DSML_HIP_CHECK(hipMemsetAsync(err_, 0, sizeof(uint32_t), s));

@@ -203,6 +203,9 @@ class PeerExchange {
   void reset(hipStream_t s);
   uint32_t error(hipStream_t s);
   void set_timeout_ms(double ms);
+  // One-shot all-reduce (sum) of n fp32 through the exchange (not graph-safe:
+  // the call number is a kernel argument).  out may alias in.
+  void allreduce(const float* in, float* out, int64_t n, hipStream_t s);
   bool connected() const { return args_.tab != nullptr; }
   const XchgArgs& args() const { return args_; }
   int nranks() const { return args_.nranks; }
@@ -225,6 +228,7 @@ class PeerExchange {
   XchgTab* dtab_ = nullptr;
   uint32_t* err_ = nullptr;
   XchgArgs args_;
+  uint64_t seq_ = 0;
 };
 
 // ---------------------------------------------------------------------------

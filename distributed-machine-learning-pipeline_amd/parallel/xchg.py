@@ -38,6 +38,11 @@ class ExchangeUnavailable(RuntimeError):
 
 
 def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 10000.0):
+    """Exchange sized for the fused MLP step (one flag per weight-gradient tile)."""
+    return make_exchange(ctx, layout.nparams, wgrad_tiles(layout), timeout_ms)
+
+
+def make_exchange(ctx: DistContext, half_floats: int, ntiles: int, timeout_ms: float = 10000.0):
     """Collective: returns a connected ``_C.PeerExchange`` for this rank, or
     raises :class:`ExchangeUnavailable` on EVERY rank if any rank failed (the
     outcome is agreed before anyone leaves, so no rank is left in a collective)."""
@@ -50,7 +55,7 @@ def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 
         err = "the xGMI exchange spans one node (<= 8 GPUs)"
     else:
         try:
-            x = C.PeerExchange(ctx.device.index, layout.nparams, wgrad_tiles(layout))
+            x = C.PeerExchange(ctx.device.index, half_floats, ntiles)
             x.set_timeout_ms(timeout_ms)
             h = x.ipc_handle()
         except Exception as e:  # noqa: BLE001
@@ -74,17 +79,42 @@ def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 
     return x
 
 
-def make_local_group(layout: MlpLayout, devices: List[int], timeout_ms: float = 10000.0):
+def make_local_group(layout: Optional[MlpLayout], devices: List[int], timeout_ms: float = 10000.0,
+                     half_floats: int = 0, ntiles: int = 0):
     """Exchanges for N replicas living in ONE process (tests / single-process
     multi-GPU): peers are referenced directly instead of through IPC."""
     from ..ops.native import require_native
 
     C = require_native()
-    xs = [C.PeerExchange(dev, layout.nparams, wgrad_tiles(layout)) for dev in devices]
+    if layout is not None:
+        half_floats, ntiles = layout.nparams, wgrad_tiles(layout)
+    xs = [C.PeerExchange(dev, half_floats, ntiles) for dev in devices]
     for r, x in enumerate(xs):
         x.set_timeout_ms(timeout_ms)
         x.connect_local(r, xs)
     return xs
+
+
+class XgmiAllReduce:
+    """One-shot fp32 sum all-reduce over xGMI peer memory for buffers of up to
+    `max_floats` (kernels/xchg.hip).  Collective construction; calls must be
+    issued by every rank in the same order (like any collective)."""
+
+    def __init__(self, ctx: DistContext, max_floats: int, max_blocks: int = 512,
+                 timeout_ms: float = 10000.0):
+        self.ctx = ctx
+        self.max_floats = (max_floats + 3) // 4 * 4
+        self.x = make_exchange(ctx, self.max_floats, max_blocks, timeout_ms)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        n = t.numel()
+        if n % 4 == 0 and n <= self.max_floats and t.is_contiguous():
+            return self.x.allreduce_(t)
+        raise ValueError(f"xGMI all-reduce takes contiguous fp32 of <= {self.max_floats} "
+                         "elements, a multiple of 4")
+
+    def check(self) -> None:
+        check(self.x)
 
 
 def reset_group(ctx: DistContext, x) -> None:

@@ -103,3 +103,60 @@ def test_two_processes_ipc(graph_steps):
     assert torch.equal(Ps[0], Ps[1])
     err = (Ps[0] - _reference(world, 6, 0.05, 4)).abs().max().item()
     assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("world,n", [(2, 262144), (3, 1000), (2, 4), (3, 1 << 20)])
+def test_standalone_allreduce_in_process(world, n):
+    n = n // 4 * 4
+    xs = make_local_group(None, [0] * world, 5000.0, half_floats=1 << 20, ntiles=256)
+    g = torch.Generator().manual_seed(n)
+    streams = [torch.cuda.Stream(DEV) for _ in range(world)]
+    for it in range(3):  # parity alternates; in-place on the last call
+        host = [torch.randn(n, generator=g) for _ in range(world)]
+        ins = [h.to(DEV) for h in host]
+        outs = [torch.empty_like(i) for i in ins]
+        torch.cuda.synchronize()
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                if it == 2:
+                    xs[r].allreduce_(ins[r])
+                else:
+                    xs[r].allreduce(ins[r], outs[r])
+        torch.cuda.synchronize()
+        want = host[0].clone()
+        for h in host[1:]:
+            want = want + h  # the kernel's rank-ordered sum
+        for r in range(world):
+            got = (ins[r] if it == 2 else outs[r]).cpu()
+            assert torch.equal(got, want)
+        for x in xs:
+            assert x.error() == 0
+
+
+def _ar_worker(rank, world, port, outdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from hipdsml.parallel.xchg import XgmiAllReduce
+
+    ctx = DistContext.from_env(device="cuda", backend="gloo")
+    ar = XgmiAllReduce(ctx, 1 << 18)
+    res = []
+    for it in range(4):
+        t = torch.full((1 << 18,), float(rank + 1 + it), device=ctx.device)
+        ar(t)
+        res.append(t[:8].cpu())
+    torch.cuda.synchronize()
+    ar.check()
+    torch.save({"res": torch.stack(res)}, os.path.join(outdir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+def test_standalone_allreduce_ipc():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ar_worker, args=(world, _free_port(), d), nprocs=world,
+                           start_method="spawn", join=True)
+        for r in range(world):
+            res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["res"]
+            for it in range(4):
+                assert torch.all(res[it] == float(1 + it + 2 + it))
