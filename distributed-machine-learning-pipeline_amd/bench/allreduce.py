@@ -110,15 +110,28 @@ def bench_device(a) -> None:
 
     from ..parallel.dist import DistContext, make_native_comm
 
+    from ..parallel.xchg import XgmiAllReduce
+
     ctx = DistContext.from_env(device="cuda")
     comm = make_native_comm(ctx)
     n = ctx.world_size
     sizes = [int(s) for s in a.sizes.split(",")]
+    algos = a.algos.split(",")
+    xg = XgmiAllReduce(ctx, max(sizes) // 4) if "xgmi" in algos and n > 1 else None
     for nbytes in sizes:
-        t = torch.ones(nbytes // 4, dtype=torch.float32, device=ctx.device)
-        for algo in a.algos.split(","):
-            fn = (lambda: comm.allreduce_(t, 0)) if algo == "rccl" else (
-                lambda: comm.ring_allreduce_(t, 0, a.chunk_bytes))
+        t = torch.zeros(nbytes // 4, dtype=torch.float32, device=ctx.device)
+        for algo in algos:
+            if algo == "rccl":
+                fn = lambda: comm.allreduce_(t, 0)  # noqa: E731
+            elif algo == "xgmi":
+                if xg is None:
+                    continue
+                fn = lambda: xg(t)  # noqa: E731
+            elif algo.startswith("ring"):  # ring = all rings, ring1 = single ring, ringK
+                k = int(algo[4:] or 0)
+                fn = lambda k=k: comm.ring_allreduce_(t, 0, a.chunk_bytes, k)  # noqa: E731
+            else:
+                raise ValueError(f"unknown algo {algo}")
             for _ in range(a.warmup):
                 fn()
             torch.cuda.synchronize()
@@ -151,7 +164,9 @@ def main(argv=None) -> int:
     r.add_argument("--inproc", action="store_true", help="all servers in this process (GIL-bound)")
     d = sub.add_parser("device")
     d.add_argument("--sizes", default="4096,65536,1048576,16777216,67108864")
-    d.add_argument("--algos", default="ring,rccl")
+    d.add_argument("--algos", default="xgmi,rccl,ring,ring1",
+                   help="xgmi (one-shot peer), rccl (ncclAllReduce), ring (all Hamiltonian rings), "
+                        "ring1 (single ring), ringK (K rings)")
     d.add_argument("--chunk-bytes", type=int, default=4 << 20)
     d.add_argument("--iters", type=int, default=50)
     d.add_argument("--warmup", type=int, default=10)

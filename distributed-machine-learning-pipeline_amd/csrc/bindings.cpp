@@ -441,6 +441,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return py::make_tuple(c.kchunk, c.nsplit);
       });
 
+  // ---- multi-ring schedule (pure index math; CPU-testable) -----------------
+  m.def("ring_schedule", [](int n, int rank, int64_t count, int64_t align, int64_t chunk,
+                            int max_rings) {
+    py::list steps;
+    for (const auto& g : ring_schedule(n, rank, count, align, chunk, max_rings)) {
+      py::list ops;
+      for (const auto& x : g)
+        ops.append(py::make_tuple(x.ring, x.send_peer, x.send_off, x.send_len, x.recv_peer,
+                                  x.recv_off, x.recv_len, x.reduce));
+      steps.append(ops);
+    }
+    return steps;
+  }, py::arg("n"), py::arg("rank"), py::arg("count"), py::arg("align") = 4,
+     py::arg("chunk") = 0, py::arg("max_rings") = 0);
+  m.def("directed_rings", &directed_rings, py::arg("n"), py::arg("max_rings") = 0);
+
   // ---- xGMI peer exchange (gradient all-reduce fused into K_C) -------------
   m.def("mlp_wgrad_tiles", [](const std::vector<int64_t>& desc) {
     return mlp_wgrad_tiles(desc_from_list(desc));
@@ -500,11 +516,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         check_cuda(t, "t");
         s.c->allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, cur_stream());
       }, py::arg("t"), py::arg("op") = 0)
-      .def("ring_allreduce_", [](PyComm& s, torch::Tensor t, int op, int64_t chunk_bytes) {
+      .def("ring_allreduce_", [](PyComm& s, torch::Tensor t, int op, int64_t chunk_bytes,
+                                 int max_rings) {
         check_cuda(t, "t");
         TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "tensor must be 16 B aligned");
-        s.c->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream());
-      }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20)
+        s.c->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream(),
+                            max_rings);
+      }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20,
+         py::arg("max_rings") = 0)
       .def("broadcast_", [](PyComm& s, torch::Tensor t, int root) {
         check_cuda(t, "t");
         s.c->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());

@@ -116,53 +116,42 @@ void RcclComm::allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, hi
 }
 
 void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op,
-                              int64_t chunk_bytes, hipStream_t s) {
+                              int64_t chunk_bytes, hipStream_t s, int max_rings) {
   if (aborted_) throw std::runtime_error("ring_allreduce on aborted communicator");
   const int n = nranks_;
   if (n < 2 || count == 0) return;
   const size_t es = dtype_size(dtype);
-  // Segment boundaries: equal segments rounded to 16 B so every segment start
-  // stays vector-aligned for the reduce kernel (the reference padded the whole
-  // buffer to a multiple of n instead, gpu_coordinator_server.go:299-334).
-  const int64_t align = 16 / (int64_t)es;
-  int64_t seg = (count + n - 1) / n;
-  seg = (seg + align - 1) / align * align;
-  std::vector<int64_t> off(n + 1);
-  for (int i = 0; i <= n; ++i) off[i] = std::min<int64_t>((int64_t)i * seg, count);
-  int64_t chunk = chunk_bytes > 0 ? chunk_bytes / (int64_t)es : seg;
-  chunk = std::max<int64_t>(align, chunk / align * align);
-  if (chunk > seg) chunk = seg;
-  ensure_tmp((size_t)chunk * es);
+  // Slices / segments start on 16 B boundaries (vector reduce kernel); the
+  // reference padded the whole buffer to a multiple of n instead
+  // (gpu_coordinator_server.go:299-334).
+  const int64_t align = std::max<int64_t>(1, 16 / (int64_t)es);
+  const int64_t chunk = chunk_bytes > 0 ? chunk_bytes / (int64_t)es : count;
+  const auto plan = ring_schedule(n, rank_, count, align, chunk, max_rings);
+  const int R = (int)directed_rings(n, max_rings).size();
+  int64_t maxr = 0;
+  for (const auto& g : plan)
+    for (const auto& x : g)
+      if (x.reduce) maxr = std::max(maxr, x.recv_len);
+  const size_t slot = ((size_t)maxr * es + 255) & ~(size_t)255;
+  ensure_tmp(std::max<size_t>(slot * R, 256));
   uint8_t* b = static_cast<uint8_t*>(buf);
-  const int next = (rank_ + 1) % n, prev = (rank_ + n - 1) % n;
+  uint8_t* tmp = static_cast<uint8_t*>(tmp_);
   const ncclDataType_t t = to_nccl(dtype);
-  // Reduce-scatter: step s sends segment (r - s), receives (r - s - 1) and
-  // reduces it; afterwards rank r owns the fully reduced segment (r + 1).
-  for (int st = 0; st < n - 1; ++st) {
-    const int si = ((rank_ - st) % n + n) % n;
-    const int ri = ((rank_ - st - 1) % n + n) % n;
-    const int64_t slen = off[si + 1] - off[si], rlen = off[ri + 1] - off[ri];
-    const int64_t steps = std::max<int64_t>((std::max(slen, rlen) + chunk - 1) / chunk, 1);
-    for (int64_t c = 0; c < steps; ++c) {
-      const int64_t so = c * chunk, ro = c * chunk;
-      const int64_t sn = std::max<int64_t>(0, std::min(chunk, slen - so));
-      const int64_t rn = std::max<int64_t>(0, std::min(chunk, rlen - ro));
-      check(ncclGroupStart(), "ncclGroupStart");
-      if (sn > 0) check(ncclSend(b + (off[si] + so) * es, sn, t, next, comm_, s), "ncclSend");
-      if (rn > 0) check(ncclRecv(tmp_, rn, t, prev, comm_, s), "ncclRecv");
-      check(ncclGroupEnd(), "ncclGroupEnd");
-      if (rn > 0) DSML_HIP_CHECK(reduce_inplace(b + (off[ri] + ro) * es, tmp_, rn, dtype, op, s));
-    }
-  }
-  // All-gather: step s sends segment (r + 1 - s), receives (r - s) in place.
-  for (int st = 0; st < n - 1; ++st) {
-    const int si = ((rank_ + 1 - st) % n + n) % n;
-    const int ri = ((rank_ - st) % n + n) % n;
-    const int64_t slen = off[si + 1] - off[si], rlen = off[ri + 1] - off[ri];
+  for (const auto& g : plan) {
     check(ncclGroupStart(), "ncclGroupStart");
-    if (slen > 0) check(ncclSend(b + off[si] * es, slen, t, next, comm_, s), "ncclSend");
-    if (rlen > 0) check(ncclRecv(b + off[ri] * es, rlen, t, prev, comm_, s), "ncclRecv");
+    for (const auto& x : g) {
+      if (x.send_len > 0)
+        check(ncclSend(b + x.send_off * es, x.send_len, t, x.send_peer, comm_, s), "ncclSend");
+      if (x.recv_len > 0) {
+        void* dst = x.reduce ? (void*)(tmp + slot * x.ring) : (void*)(b + x.recv_off * es);
+        check(ncclRecv(dst, x.recv_len, t, x.recv_peer, comm_, s), "ncclRecv");
+      }
+    }
     check(ncclGroupEnd(), "ncclGroupEnd");
+    for (const auto& x : g)
+      if (x.reduce && x.recv_len > 0)
+        DSML_HIP_CHECK(reduce_inplace(b + x.recv_off * es, tmp + slot * x.ring, x.recv_len, dtype,
+                                      op, s));
   }
 }
 

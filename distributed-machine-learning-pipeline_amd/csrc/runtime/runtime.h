@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../dsml.h"
+#include "ring_plan.h"
 
 namespace dsml {
 
@@ -155,11 +156,13 @@ class RcclComm {
   int nranks() const { return nranks_; }
   // RCCL's own all-reduce (multi-channel ring / LL protocols).
   void allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, hipStream_t s);
-  // In-house ring all-reduce: reduce-scatter + all-gather, 2(n-1) steps of
-  // ncclSend(next)/ncclRecv(prev) inside ncclGroupStart/End, segment reductions
-  // by dsml::reduce_inplace, pipelined over `chunk_bytes` chunks.
+  // In-house multi-ring all-reduce (ring_plan.h): one slice per directed
+  // Hamiltonian ring (up to 6 at n = 8, each on its own xGMI links),
+  // reduce-scatter + all-gather, every ring's ncclSend/ncclRecv of a step in
+  // one ncclGroup, segment reductions by dsml::reduce_inplace, `chunk_bytes`
+  // rounds.  max_rings = 0: all rings; 1: the classic single ring.
   void ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, int64_t chunk_bytes,
-                      hipStream_t s);
+                      hipStream_t s, int max_rings = 0);
   void broadcast(void* buf, int64_t count, int32_t dtype, int root, hipStream_t s);
   void send(const void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
   void recv(void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
