@@ -327,6 +327,32 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                         (int)C, (int)Cp, (float)inv_batch, bf16p(dz, "dz"), dz.stride(0), t, ldt,
                         stats.data_ptr<float>(), cur_stream()), "softmax_xent");
   });
+  m.def("head_softmax_xent", [bf16p](torch::Tensor H, torch::Tensor W, c10::optional<torch::Tensor> bias,
+                                    int64_t B, int64_t K, int64_t C, torch::Tensor labels,
+                                    double inv_batch, c10::optional<torch::Tensor> logits,
+                                    torch::Tensor dz, c10::optional<torch::Tensor> dzT,
+                                    torch::Tensor stats) {
+    TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && H.size(0) >= B && H.size(1) >= K, "H shape");
+    TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.size(0) >= C && W.size(1) >= K, "W shape");
+    check_cuda(labels, "labels"); check_f32(stats, "stats");
+    TORCH_CHECK(labels.scalar_type() == torch::kInt32 && labels.numel() >= B, "labels");
+    const float* b = nullptr;
+    if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= C, "bias"); b = bias->data_ptr<float>(); }
+    float* lg = nullptr; int64_t ldl = 0;
+    if (logits) { check_f32(*logits, "logits"); TORCH_CHECK(logits->dim() == 2 && logits->size(0) >= B && logits->size(1) >= C, "logits shape");
+                  lg = logits->data_ptr<float>(); ldl = logits->stride(0); }
+    TORCH_CHECK(dz.dim() == 2 && dz.size(0) >= B && dz.stride(1) == 1, "dz shape");
+    const int64_t Cp = dz.size(1);
+    uint16_t* t = nullptr; int64_t ldt = 0;
+    if (dzT) { TORCH_CHECK(dzT->dim() == 2 && dzT->size(0) >= Cp && dzT->size(1) >= B, "dzT shape");
+               t = bf16p(*dzT, "dzT"); ldt = dzT->stride(0); }
+    hip_ok(head_softmax_xent(bf16p(H, "H"), H.stride(0), bf16p(W, "W"), W.stride(0), b, (int)B, (int)K,
+                             (int)C, labels.data_ptr<int32_t>(), (float)inv_batch, lg, ldl,
+                             bf16p(dz, "dz"), dz.stride(0), t, ldt, (int)Cp, stats.data_ptr<float>(),
+                             cur_stream()), "head_softmax_xent");
+  }, py::arg("H"), py::arg("W"), py::arg("bias"), py::arg("B"), py::arg("K"), py::arg("C"),
+     py::arg("labels"), py::arg("inv_batch"), py::arg("logits"), py::arg("dz"), py::arg("dzT"),
+     py::arg("stats"));
   m.def("rowsum_bf16", [bf16p](torch::Tensor X, int64_t N, int64_t cols, c10::optional<torch::Tensor> out,
                               c10::optional<torch::Tensor> bias, double lr) {
     TORCH_CHECK(X.dim() == 2 && X.size(0) >= N && X.size(1) >= cols, "X shape");
@@ -342,7 +368,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                      double alpha, c10::optional<torch::Tensor> bias, bool relu,
                                      c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
                                      c10::optional<torch::Tensor> obf, c10::optional<torch::Tensor> obfT,
-                                     c10::optional<torch::Tensor> sgdW, double lr) {
+                                     c10::optional<torch::Tensor> sgdW, double lr, int64_t splits,
+                                     c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> ctr,
+                                     c10::optional<torch::Tensor> bgrad,
+                                     c10::optional<torch::Tensor> bsgd) {
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A, B 2-D rows");
     TORCH_CHECK(A.size(0) >= M && B.size(0) >= N && A.size(1) >= K && B.size(1) >= K, "A/B too small");
     auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
@@ -360,12 +389,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (obfT) { chk2(*obfT, N, M, "obfT"); e.obfT = bf16p(*obfT, "obfT"); e.ldt = obfT->stride(0); }
     if (sgdW) { chk2(*sgdW, M, N, "sgdW"); TORCH_CHECK(sgdW->scalar_type() == torch::kFloat32, "sgdW f32");
                 e.sgdW = sgdW->data_ptr<float>(); e.ldw = sgdW->stride(0); }
-    hip_ok(gemm_bf16_nt(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), nullptr, (int)M, (int)N,
-                        (int)K, 1, cur_stream(), &e), "gemm_bf16_nt_fused");
+    if (bgrad) { check_f32(*bgrad, "bgrad"); TORCH_CHECK(bgrad->numel() >= M, "bgrad"); e.bgrad = bgrad->data_ptr<float>(); }
+    if (bsgd) { check_f32(*bsgd, "bsgd"); TORCH_CHECK(bsgd->numel() >= M, "bsgd"); e.bsgd = bsgd->data_ptr<float>(); }
+    if (splits == 0) {  // batch-row kernel: full K per block, epilogue fused, no slabs
+      hip_ok(gemm_bf16_rows64(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), (int)M, (int)N,
+                              (int)K, e, cur_stream()), "gemm_bf16_rows64");
+      return 1;
+    }
+    const int S = gemm_bf16_num_splits((int)K, (int)splits);
+    float* cp = nullptr;
+    int* tc = nullptr;
+    if (S > 1) {
+      TORCH_CHECK(ws && ctr, "split-K fused GEMM needs ws (slabs) and ctr (tile counters)");
+      check_f32(*ws, "ws");
+      TORCH_CHECK(ws->numel() >= (int64_t)S * M * N, "ws too small: need ", (int64_t)S * M * N);
+      check_cuda(*ctr, "ctr");
+      TORCH_CHECK(ctr->scalar_type() == torch::kInt32 &&
+                  ctr->numel() >= ((N + 63) / 64) * ((M + 63) / 64), "ctr: int32, one per 64x64 tile");
+      cp = ws->data_ptr<float>();
+      tc = ctr->data_ptr<int32_t>();
+    }
+    hip_ok(gemm_bf16_nt(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), cp, (int)M, (int)N,
+                        (int)K, (int)splits, cur_stream(), &e, tc), "gemm_bf16_nt_fused");
+    return S;
   }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("alpha") = 1.0,
      py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("mask") = py::none(),
      py::arg("of32") = py::none(), py::arg("obf") = py::none(), py::arg("obfT") = py::none(),
-     py::arg("sgdW") = py::none(), py::arg("lr") = 0.0);
+     py::arg("sgdW") = py::none(), py::arg("lr") = 0.0, py::arg("splits") = 1,
+     py::arg("ws") = py::none(), py::arg("ctr") = py::none(), py::arg("bgrad") = py::none(),
+     py::arg("bsgd") = py::none());
   m.def("sgd_cast", [bf16p](torch::Tensor W, c10::optional<torch::Tensor> G, int64_t N, int64_t K, double lr,
                            torch::Tensor Wb, c10::optional<torch::Tensor> WbT) {
     check_f32(W, "W");

@@ -155,12 +155,22 @@ struct GemmEpi {
   float* sgdW;  // fused SGD target (fp32 [M x N], ld ldw): W -= lr * acc
   int64_t ldw;
   float lr;
+  float* bgrad;  // single split only: row sums of A over K (bias gradient of a dW GEMM)
+  float* bsgd;   // single split only: bias SGD with those row sums (b -= lr * rowsum)
 };
-// epi != nullptr: single K split, epilogue applied in-kernel (Cp unused).
+// epi == nullptr: fp32 partial slabs Cp[split] (finish with gemm_epilogue).
+// epi != nullptr: epilogue applied in-kernel; with > 1 K split the last split
+// of each tile reduces the slabs (Cp) and applies it — `tile_ctr` must hold one
+// zero int per 64x64 output tile (the kernel leaves them zero again).
 hipError_t gemm_bf16_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* Cp,
                         int M, int N, int K, int splits, hipStream_t s,
-                        const GemmEpi* epi = nullptr);
+                        const GemmEpi* epi = nullptr, int* tile_ctr = nullptr);
 int gemm_bf16_num_splits(int K, int splits);
+// Batch-row GEMM (C = A . B^T with <= 64 rows per block, 16 columns per block,
+// full K per block split across its 4 waves) with the whole epilogue fused
+// (alpha, bias, ReLU, ReLU'-mask, fp32 / bf16 / transposed bf16 outputs).
+hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M,
+                            int N, int K, const GemmEpi& epi, hipStream_t s);
 // out = epi(alpha * sum_s Cp[s] + bias): relu, ReLU'-mask (bf16 mask > 0), fp32 / bf16 /
 // transposed-bf16 outputs (each nullable).
 hipError_t gemm_epilogue(const float* Cp, int S, int M, int N, float alpha, const float* bias,
@@ -171,6 +181,12 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 hipError_t softmax_xent(const float* logits, int64_t ldl, const int32_t* labels, int B, int C,
                         int Cp, float inv_batch, uint16_t* dz, int64_t ldz, uint16_t* dzT,
                         int64_t ldt, float* stats, hipStream_t s);
+// Classifier head fused with softmax-CE (C <= 16): logits = H . W^T + b per
+// row, then the softmax_xent outputs.  `logits` may be null.
+hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,
+                             const float* bias, int B, int K, int C, const int32_t* labels,
+                             float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
+                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s);
 hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
                        float lr, hipStream_t s);
 hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,

@@ -30,11 +30,143 @@ __device__ __forceinline__ f32x4 mfma_bf16(uint4 a, uint4 b, f32x4 c) {
 __device__ __forceinline__ uint4 zero_u4() { return make_uint4(0u, 0u, 0u, 0u); }
 
 // ---------------------------------------------------------------------------
-constexpr int kGemmU = 4;  // K-steps (x32) whose loads are in flight together
+// Main kernel.  Workgroup = 64x64 output tile, 4 waves of 32x32 (2x2 MFMA
+// 16x16x32 tiles); U K-steps (x32) of operand loads in flight per batch.
+//   mode 0: write the fp32 partial of this K split to its slab (Cp[z]);
+//           a separate gemm_epilogue_k sums the slabs.
+//   mode 1: single K split, epilogue applied from the accumulators.
+//   mode 2: split-K with the epilogue fused: every split writes its slab,
+//           the LAST split to finish a tile (per-tile arrival counter, no
+//           spinning) sums all slabs in split order (deterministic) and
+//           applies the epilogue, then re-arms the counter.
+// Optional (mode 1): row sums of A over K (bias gradient of the dW GEMM,
+// A = dZ^T) written to epi.bgrad or applied as SGD to epi.bsgd.
+// ---------------------------------------------------------------------------
+constexpr int kTileLdsStride = 68;  // fp32 words per LDS row of the SGD epilogue
 
+typedef __attribute__((address_space(1))) uint32_t gu32a;
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t nu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store((gu32a*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const gu32a*)p, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ float bf16lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// Epilogue from accumulators in MFMA layout: acc[x][y][r] = C[mb+16x+4g+r][nb+16y+i].
+__device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[2][2], int mb, int nb, int i, int g,
+                                              int M, int N, const GemmEpi& epi) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int n = nb + 16 * y + i;
+      const int m4 = mb + 16 * x + 4 * g;
+      if (n >= N) continue;
+      uint16_t hb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m4 + r;
+        float v = acc[x][y][r] * epi.alpha;
+        if (m < M) {
+          if (epi.bias) v += epi.bias[n];
+          if (epi.relu) v = fmaxf(v, 0.f);
+          if (epi.mask) v = bf16_to_f32(epi.mask[(int64_t)m * epi.ldm + n]) > 0.f ? v : 0.f;
+          if (epi.sgdW) {
+            float* wp = epi.sgdW + (int64_t)m * epi.ldw + n;
+            v = *wp - epi.lr * v;
+            *wp = v;
+          }
+          if (epi.of32) epi.of32[(int64_t)m * epi.ldo + n] = v;
+          if (epi.obf) epi.obf[(int64_t)m * epi.ldb + n] = f32_to_bf16(v);
+        }
+        hb[r] = m < M ? f32_to_bf16(v) : (uint16_t)0;
+      }
+      if (epi.obfT) {
+        uint16_t* tp = epi.obfT + (int64_t)n * epi.ldt + m4;
+        if (m4 + 3 < M) {
+          *reinterpret_cast<uint2*>(tp) = make_uint2(hb[0] | ((uint32_t)hb[1] << 16),
+                                                     hb[2] | ((uint32_t)hb[3] << 16));
+        } else {
+          for (int r = 0; r < 4 && m4 + r < M; ++r) tp[r] = hb[r];
+        }
+      }
+    }
+}
+
+// Fused SGD epilogue staged through LDS so every global access is a full
+// 16 B vector along a row: W (fp32) read-modify-write as float4, the bf16 copy
+// as 8 B runs, the transposed bf16 copy as 16 B runs of 8 rows.  Requires
+// N % 4 == 0, M % 8 == 0 and 16 B-aligned rows (checked on the host).
+__device__ __forceinline__ void epilogue_sgd_lds(f32x4 (&acc)[2][2], float* tile, int m0, int n0,
+                                                 int M, int N, const GemmEpi& epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        tile[(wm + 16 * x + 4 * g + r) * kTileLdsStride + wn + 16 * y + i] = acc[x][y][r] * epi.alpha;
+  __syncthreads();
+  // row pass: 64 rows x 16 float4 -> 4 per thread
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int idx = threadIdx.x + 256 * j;
+    const int r = idx >> 4, c = (idx & 15) * 4;
+    const int m = m0 + r, n = n0 + c;
+    float* tp = tile + r * kTileLdsStride + c;
+    if (m < M && n < N) {
+      float4* wp = reinterpret_cast<float4*>(epi.sgdW + (int64_t)m * epi.ldw + n);
+      float4 wv = *wp;
+      wv.x -= epi.lr * tp[0];
+      wv.y -= epi.lr * tp[1];
+      wv.z -= epi.lr * tp[2];
+      wv.w -= epi.lr * tp[3];
+      __builtin_nontemporal_store(nf4{wv.x, wv.y, wv.z, wv.w}, reinterpret_cast<nf4*>(wp));
+      tp[0] = wv.x; tp[1] = wv.y; tp[2] = wv.z; tp[3] = wv.w;
+      if (epi.obf) {
+        const uint32_t lo = f32_to_bf16(wv.x) | ((uint32_t)f32_to_bf16(wv.y) << 16);
+        const uint32_t hi = f32_to_bf16(wv.z) | ((uint32_t)f32_to_bf16(wv.w) << 16);
+        __builtin_nontemporal_store(nu2{lo, hi},
+                                    reinterpret_cast<nu2*>(epi.obf + (int64_t)m * epi.ldb + n));
+      }
+    }
+  }
+  if (!epi.obfT) return;
+  __syncthreads();
+  // column pass: W^T rows n (64) x 8 runs of 8 m -> 2 per thread
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j;
+    const int c = idx >> 3, r8 = (idx & 7) * 8;
+    const int n = n0 + c, m = m0 + r8;
+    if (n < N && m < M) {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        q[k] = f32_to_bf16(tile[(r8 + 2 * k) * kTileLdsStride + c]) |
+               ((uint32_t)f32_to_bf16(tile[(r8 + 2 * k + 1) * kTileLdsStride + c]) << 16);
+      __builtin_nontemporal_store(nu4{q[0], q[1], q[2], q[3]},
+                                  reinterpret_cast<nu4*>(epi.obfT + (int64_t)n * epi.ldt + m));
+    }
+  }
+}
+
+template <int U>
 __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
-    float* __restrict__ Cp, int M, int N, int K, int kchunk, GemmEpi epi, int fused) {
+    float* __restrict__ Cp, int M, int N, int K, int kchunk, GemmEpi epi, int mode,
+    int* __restrict__ tile_ctr, int sgd_lds) {
+  __shared__ float tile[64 * kTileLdsStride];
+  __shared__ int s_last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int mb = blockIdx.y * 64 + (w >> 1) * 32;
@@ -52,20 +184,24 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     ra[t] = va[t] ? ra[t] : M - 1;
     rb[t] = vb[t] ? rb[t] : N - 1;
   }
-  const uint16_t* pa[2] = {A + (int64_t)ra[0] * lda + 8 * g, A + (int64_t)ra[1] * lda + 8 * g};
-  const uint16_t* pb[2] = {B + (int64_t)rb[0] * ldb + 8 * g, B + (int64_t)rb[1] * ldb + 8 * g};
+  // Row bases; each lane's K offset is clamped on its own (k + 8g may run past
+  // a short row's end when K % 32 != 0: never read past the buffer).
+  const uint16_t* pa[2] = {A + (int64_t)ra[0] * lda, A + (int64_t)ra[1] * lda};
+  const uint16_t* pb[2] = {B + (int64_t)rb[0] * ldb, B + (int64_t)rb[1] * ldb};
   f32x4 acc[2][2];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) acc[x][y] = {0.f, 0.f, 0.f, 0.f};
+  const bool want_rowsum = mode == 1 && (epi.bgrad || epi.bsgd);
+  float rs[2] = {0.f, 0.f};
 
-  for (int k0 = kb; k0 < ke; k0 += 32 * kGemmU) {
-    uint4 fa[kGemmU][2], fb[kGemmU][2];
+  for (int k0 = kb; k0 < ke; k0 += 32 * U) {
+    uint4 fa[U][2], fb[U][2];
 #pragma unroll
-    for (int u = 0; u < kGemmU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int kk = k0 + 32 * u + 8 * g;
-      const int kc = kk < ke ? k0 + 32 * u : kb;  // clamp to a valid address
+      const int kc = kk < ke ? kk : kb;  // clamp to a valid 16 B run of the row
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         fa[u][t] = *reinterpret_cast<const uint4*>(pa[t] + kc);
@@ -74,12 +210,20 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < kGemmU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const bool kv = k0 + 32 * u + 8 * g < ke;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         fa[u][t] = (kv && va[t]) ? fa[u][t] : zero_u4();
         fb[u][t] = (kv && vb[t]) ? fb[u][t] : zero_u4();
+      }
+      if (want_rowsum) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const uint4 v = fa[u][t];
+          rs[t] += bf16lo(v.x) + bf16hi(v.x) + bf16lo(v.y) + bf16hi(v.y) + bf16lo(v.z) +
+                   bf16hi(v.z) + bf16lo(v.w) + bf16hi(v.w);
+        }
       }
 #pragma unroll
       for (int x = 0; x < 2; ++x)
@@ -87,62 +231,252 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
         for (int y = 0; y < 2; ++y) acc[x][y] = mfma_bf16(fa[u][x], fb[u][y], acc[x][y]);
     }
   }
-  if (fused) {
-    // Single K split: apply the whole epilogue from the accumulators (no slab
-    // round trip).  Optional fused SGD: W[m][n] -= lr * acc, and the bf16 /
-    // transposed-bf16 outputs then receive the UPDATED weight.
+
+  if (mode == 0 || mode == 2) {
+    float* out = Cp + (int64_t)blockIdx.z * M * N;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
         const int n = nb + 16 * y + i;
-        const int m4 = mb + 16 * x + 4 * g;
-        if (n >= N) continue;
-        uint16_t hb[4];
+        if (n < N) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m4 + r;
-          float v = acc[x][y][r] * epi.alpha;
-          if (m < M) {
-            if (epi.bias) v += epi.bias[n];
-            if (epi.relu) v = fmaxf(v, 0.f);
-            if (epi.mask) v = bf16_to_f32(epi.mask[(int64_t)m * epi.ldm + n]) > 0.f ? v : 0.f;
-            if (epi.sgdW) {
-              float* wp = epi.sgdW + (int64_t)m * epi.ldw + n;
-              v = *wp - epi.lr * v;
-              *wp = v;
+          for (int r = 0; r < 4; ++r) {
+            const int m = mb + 16 * x + 4 * g + r;
+            if (m < M) {
+              if (mode == 0) out[(int64_t)m * N + n] = acc[x][y][r];
+              else st_agent(out + (int64_t)m * N + n, acc[x][y][r]);
             }
-            if (epi.of32) epi.of32[(int64_t)m * epi.ldo + n] = v;
-            if (epi.obf) epi.obf[(int64_t)m * epi.ldb + n] = f32_to_bf16(v);
-          }
-          hb[r] = m < M ? f32_to_bf16(v) : (uint16_t)0;
-        }
-        if (epi.obfT) {
-          uint16_t* tp = epi.obfT + (int64_t)n * epi.ldt + m4;
-          if (m4 + 3 < M) {
-            *reinterpret_cast<uint2*>(tp) = make_uint2(hb[0] | ((uint32_t)hb[1] << 16),
-                                                       hb[2] | ((uint32_t)hb[3] << 16));
-          } else {
-            for (int r = 0; r < 4 && m4 + r < M; ++r) tp[r] = hb[r];
           }
         }
       }
-    return;
+    if (mode == 0) return;
+    // ---- split-K arrival: the last split of this tile finishes it ----------
+    // Slabs are written and read with device-coherent (sc1) accesses, so no
+    // L2 writeback / invalidate fence is needed (those cost ~10s of us with
+    // hundreds of workgroups): completing the stores before the counter
+    // increment is enough.
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int tid = blockIdx.y * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(tile_ctr + tid, 1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.z - 1;
+    __syncthreads();
+    if (!s_last) return;
+    const int S = gridDim.z;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < S; z += 4) {  // split order: bit-identical to the 2-kernel path
+      float v[4][2][2][4];
+#pragma unroll
+      for (int zz = 0; zz < 4; ++zz) {
+        const float* sp = Cp + (int64_t)min(z + zz, S - 1) * M * N;
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const int n = min(nb + 16 * y + i, N - 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = min(mb + 16 * x + 4 * g + r, M - 1);
+              v[zz][x][y][r] = ld_agent(sp + (int64_t)m * N + n);
+            }
+          }
+      }
+#pragma unroll
+      for (int zz = 0; zz < 4; ++zz)
+        if (z + zz < S) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[x][y][r] += v[zz][x][y][r];
+        }
+    }
+    if (threadIdx.x == 0)  // re-arm for the next GEMM using the counters
+      __hip_atomic_store(tile_ctr + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  float* out = Cp + (int64_t)blockIdx.z * M * N;
+
+  if (want_rowsum) {
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+    for (int t = 0; t < 2; ++t) {
+      rs[t] += __shfl_xor(rs[t], 16, 64);
+      rs[t] += __shfl_xor(rs[t], 32, 64);
+    }
+    if (blockIdx.x == 0 && (w & 1) == 0 && g == 0) {
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      const int n = nb + 16 * y + i;
-      if (n < N) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mb + 16 * x + 4 * g + r;
-          if (m < M) out[(int64_t)m * N + n] = acc[x][y][r];
+      for (int t = 0; t < 2; ++t) {
+        const int m = mb + 16 * t + i;
+        if (m < M) {
+          if (epi.bsgd) epi.bsgd[m] -= epi.lr * epi.alpha * rs[t];
+          else epi.bgrad[m] = epi.alpha * rs[t];
         }
       }
     }
+  }
+  if (sgd_lds) {
+    epilogue_sgd_lds(acc, tile, blockIdx.y * 64, blockIdx.x * 64, M, N, epi);
+  } else {
+    epilogue_regs(acc, mb, nb, i, g, M, N, epi);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Skinny GEMM for the batch-row products (M <= 64 rows per block: the batch):
+// C[64 x 16] per workgroup over the FULL K, the 4 waves splitting K four ways
+// and combining through LDS — no cross-workgroup split-K, so no slabs, no
+// counters and the whole epilogue in the same launch.  N / 16 workgroups
+// (256 for N = 4096 = one per CU); each streams its 16 weight rows once and
+// the 64-row activation block through L2.
+// ---------------------------------------------------------------------------
+constexpr int kR64Pad = 17;  // LDS row stride (floats) of a 16-wide partial tile
+
+template <int U, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __restrict__ A, int64_t lda,
+                                                     const uint16_t* __restrict__ B, int64_t ldb,
+                                                     int M, int N, int K, GemmEpi epi, int vec) {
+  constexpr int NT = 64 * WAVES;
+  __shared__ float red[WAVES * 64 * kR64Pad];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 64;
+  const int kq = ((K + WAVES - 1) / WAVES + 31) / 32 * 32;
+  const int kb = w * kq, ke = min(K, kb + kq);
+  int ra[4];
+  bool va[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    ra[t] = m0 + 16 * t + i;
+    va[t] = ra[t] < M;
+    ra[t] = va[t] ? ra[t] : M - 1;
+  }
+  const bool vb = n0 + i < N;
+  const uint16_t* pb = B + (int64_t)(vb ? n0 + i : N - 1) * ldb;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += 32 * U) {
+    uint4 fa[U][4], fb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = k0 + 32 * u + 8 * g;
+      const int kc = kk < ke ? kk : kb;  // per-lane clamp: never past the row
+      fb[u] = *reinterpret_cast<const uint4*>(pb + kc);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        fa[u][t] = *reinterpret_cast<const uint4*>(A + (int64_t)ra[t] * lda + kc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool kv = k0 + 32 * u + 8 * g < ke;
+      const uint4 b = (kv && vb) ? fb[u] : zero_u4();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = mfma_bf16((kv && va[t]) ? fa[u][t] : zero_u4(), b, acc[t]);
+    }
+  }
+  // partials -> LDS, then the fixed-order 4-way sum (deterministic)
+  float* mine = red + w * 64 * kR64Pad;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mine[(16 * t + 4 * g + r) * kR64Pad + i] = acc[t][r];
+  __syncthreads();
+  constexpr int PER = 1024 / NT;  // outputs of the 64x16 tile per thread
+  float v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + NT * j;
+    const int mr = e >> 4, nc = e & 15;
+    const int o = mr * kR64Pad + nc;
+    float x = red[o];
+#pragma unroll
+    for (int q = 1; q < WAVES; ++q) x += red[q * 64 * kR64Pad + o];
+    const int m = m0 + mr, n = n0 + nc;
+    x *= epi.alpha;
+    if (m < M && n < N) {
+      if (epi.bias) x += epi.bias[n];
+      if (epi.relu) x = fmaxf(x, 0.f);
+      if (epi.mask) x = bf16_to_f32(epi.mask[(int64_t)m * epi.ldm + n]) > 0.f ? x : 0.f;
+    } else {
+      x = 0.f;
+    }
+    v[j] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + NT * j;
+    red[(e >> 4) * kR64Pad + (e & 15)] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 256) return;  // stores below use 256 threads
+  if (vec) {
+    // rows: thread -> (m = t / 4, 4 consecutive n)
+    const int mr = threadIdx.x >> 2, nc = (threadIdx.x & 3) * 4;
+    const int m = m0 + mr, n = n0 + nc;
+    if (m < M && n < N) {
+      const float* s4 = red + mr * kR64Pad + nc;
+      if (epi.of32)
+        *reinterpret_cast<float4*>(epi.of32 + (int64_t)m * epi.ldo + n) =
+            make_float4(s4[0], s4[1], s4[2], s4[3]);
+      if (epi.obf)
+        *reinterpret_cast<uint2*>(epi.obf + (int64_t)m * epi.ldb + n) =
+            make_uint2(f32_to_bf16(s4[0]) | ((uint32_t)f32_to_bf16(s4[1]) << 16),
+                       f32_to_bf16(s4[2]) | ((uint32_t)f32_to_bf16(s4[3]) << 16));
+    }
+    // transposed: thread -> (n = t / 16, 4 consecutive m)
+    if (epi.obfT) {
+      const int nr = threadIdx.x >> 4, mc = (threadIdx.x & 15) * 4;
+      const int nn = n0 + nr, mm = m0 + mc;
+      if (nn < N && mm < M) {
+        uint16_t h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = f32_to_bf16(red[(mc + r) * kR64Pad + nr]);
+        *reinterpret_cast<uint2*>(epi.obfT + (int64_t)nn * epi.ldt + mm) =
+            make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int mr = e >> 4, nc = e & 15;
+      const int m = m0 + mr, n = n0 + nc;
+      if (m < M && n < N) {
+        const float x = red[mr * kR64Pad + nc];
+        if (epi.of32) epi.of32[(int64_t)m * epi.ldo + n] = x;
+        if (epi.obf) epi.obf[(int64_t)m * epi.ldb + n] = f32_to_bf16(x);
+        if (epi.obfT) epi.obfT[(int64_t)n * epi.ldt + m] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M,
+                            int N, int K, const GemmEpi& epi, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K & 7) || (lda & 7) || (ldb & 7)) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)B) & 15) return hipErrorInvalidValue;
+  if (epi.sgdW || epi.bgrad || epi.bsgd) return hipErrorInvalidValue;
+  // vector stores when every written row run is aligned and whole
+  const int vec = ((N % 4) == 0 && (M % 4) == 0 && (!epi.of32 || ((epi.ldo % 4) == 0 && ((uintptr_t)epi.of32 & 15) == 0)) &&
+                   (!epi.obf || ((epi.ldb % 4) == 0 && ((uintptr_t)epi.obf & 7) == 0)) &&
+                   (!epi.obfT || ((epi.ldt % 4) == 0 && ((uintptr_t)epi.obfT & 7) == 0))) ? 1 : 0;
+  dim3 grid((N + 15) / 16, (M + 63) / 64);
+  // Long K: 8 waves (512 threads) each streaming K/8 with 8 K-steps of loads
+  // in flight: twice the bytes in flight per CU of the 4-wave form.
+  if (K >= 8 * 32 * 8)
+    hipLaunchKernelGGL((gemm_rows64_k<8, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  else if (K >= 4 * 32 * 4)
+    hipLaunchKernelGGL((gemm_rows64_k<4, 4>), grid, dim3(256), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  else
+    hipLaunchKernelGGL((gemm_rows64_k<2, 4>), grid, dim3(256), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -162,7 +496,13 @@ __global__ __launch_bounds__(256) void gemm_epilogue_k(
     const int m = m0 + mr;
     float v = 0.f;
     if (m < M && n < N) {
-      for (int s = 0; s < S; ++s) v += Cp[((int64_t)s * M + m) * N + n];
+      int s = 0;
+      for (; s + 4 <= S; s += 4) {
+        const float a0 = Cp[((int64_t)s * M + m) * N + n], a1 = Cp[((int64_t)(s + 1) * M + m) * N + n];
+        const float a2 = Cp[((int64_t)(s + 2) * M + m) * N + n], a3 = Cp[((int64_t)(s + 3) * M + m) * N + n];
+        v += a0; v += a1; v += a2; v += a3;
+      }
+      for (; s < S; ++s) v += Cp[((int64_t)s * M + m) * N + n];
       v *= alpha;
       if (bias) v += bias[n];
       if (relu) v = fmaxf(v, 0.f);
@@ -305,21 +645,37 @@ __global__ __launch_bounds__(256) void sgd_cast_k(float* __restrict__ W, const f
 
 // ---------------------------------------------------------------------------
 hipError_t gemm_bf16_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* Cp,
-                        int M, int N, int K, int splits, hipStream_t s, const GemmEpi* epi) {
+                        int M, int N, int K, int splits, hipStream_t s, const GemmEpi* epi,
+                        int* tile_ctr) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return hipErrorInvalidValue;
   if ((K & 7) || (lda & 7) || (ldb & 7)) return hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B) & 15) return hipErrorInvalidValue;
   int kchunk = (K + splits - 1) / splits;
   kchunk = (kchunk + 31) / 32 * 32;
   const int S = (K + kchunk - 1) / kchunk;
-  if (epi != nullptr && S != 1) return hipErrorInvalidValue;  // fused epilogue needs one split
-  if (epi != nullptr && epi->obfT && (epi->ldt & 3)) return hipErrorInvalidValue;
+  int mode = 0;
+  if (epi != nullptr) {
+    mode = S == 1 ? 1 : 2;
+    if (mode == 2 && (tile_ctr == nullptr || Cp == nullptr)) return hipErrorInvalidValue;
+    if (mode == 2 && (epi->bgrad || epi->bsgd)) return hipErrorInvalidValue;
+    if (epi->obfT && (epi->ldt & 3)) return hipErrorInvalidValue;
+  }
   GemmEpi e{};
   e.alpha = 1.f;
   if (epi) e = *epi;
+  // Vectorised SGD epilogue when every row access is 16 B aligned.
+  const int sgd_lds = (epi && e.sgdW && !e.mask && !e.of32 && !e.bias && !e.relu && (N % 4) == 0 &&
+                       (M % 8) == 0 && (e.ldw % 4) == 0 && (!e.obf || (e.ldb % 4) == 0) &&
+                       (!e.obfT || (e.ldt % 8) == 0) && ((uintptr_t)e.sgdW & 15) == 0 &&
+                       (!e.obf || ((uintptr_t)e.obf & 7) == 0) &&
+                       (!e.obfT || ((uintptr_t)e.obfT & 15) == 0)) ? 1 : 0;
   dim3 grid((N + 63) / 64, (M + 63) / 64, S);
-  hipLaunchKernelGGL(gemm_bf16_nt_k, grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N, K, kchunk, e,
-                     epi != nullptr ? 1 : 0);
+  if (kchunk >= 256)
+    hipLaunchKernelGGL(gemm_bf16_nt_k<8>, grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N, K,
+                       kchunk, e, mode, tile_ctr, sgd_lds);
+  else
+    hipLaunchKernelGGL(gemm_bf16_nt_k<4>, grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N, K,
+                       kchunk, e, mode, tile_ctr, sgd_lds);
   return hipGetLastError();
 }
 
@@ -342,6 +698,88 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
                           int64_t ldo, uint16_t* YT, int64_t ldt, hipStream_t s) {
   dim3 grid((Kp + 31) / 32, (M + 31) / 32);
   hipLaunchKernelGGL(cast_transpose_k, grid, dim3(256), 0, s, X, ldi, M, K, Kp, Y, ldo, YT, ldt);
+  return hipGetLastError();
+}
+
+// Fused classifier head: logits[m][c] = H[m] . W[c] + b[c] for C <= 16
+// classes, then softmax-CE as softmax_xent_k — one 256-thread block per row.
+// Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
+constexpr int kHeadMaxC = 16;
+__global__ __launch_bounds__(256) void head_softmax_xent_k(
+    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
+    const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
+    float inv_batch, float* __restrict__ logits, int64_t ldl, uint16_t* __restrict__ dz,
+    int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats) {
+  __shared__ float part[4][kHeadMaxC];
+  const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint16_t* hr = H + (int64_t)m * ldh;
+  float acc[kHeadMaxC];
+#pragma unroll
+  for (int c = 0; c < kHeadMaxC; ++c) acc[c] = 0.f;
+  for (int k = t * 8; k < K; k += 256 * 8) {
+    const uint4 hv = *reinterpret_cast<const uint4*>(hr + k);
+    const float h[8] = {bf16lo(hv.x), bf16hi(hv.x), bf16lo(hv.y), bf16hi(hv.y),
+                        bf16lo(hv.z), bf16hi(hv.z), bf16lo(hv.w), bf16hi(hv.w)};
+#pragma unroll
+    for (int c = 0; c < kHeadMaxC; ++c) {
+      if (c < C) {
+        const uint4 wv = *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k);
+        acc[c] += h[0] * bf16lo(wv.x) + h[1] * bf16hi(wv.x) + h[2] * bf16lo(wv.y) +
+                  h[3] * bf16hi(wv.y) + h[4] * bf16lo(wv.z) + h[5] * bf16hi(wv.z) +
+                  h[6] * bf16lo(wv.w) + h[7] * bf16hi(wv.w);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < kHeadMaxC; ++c) {
+    float v = acc[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0 && c < C) part[w][c] = v;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const int c = lane;
+  const bool cv = c < C;
+  float z = -3.402823466e38f;
+  if (cv) z = part[0][c] + part[1][c] + part[2][c] + part[3][c] + (bias ? bias[c] : 0.f);
+  if (cv && logits) logits[(int64_t)m * ldl + c] = z;
+  const int y = labels[m];
+  float mx = z;
+  int am = cv ? c : 0x7fffffff;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    argmax_combine(mx, am, om, oa);
+  }
+  const float e = cv ? expf(z - mx) : 0.f;
+  float se = e;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+  const float p = e / se;
+  const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
+  if (c < Cp) {
+    const uint16_t hq = f32_to_bf16(gr);
+    dz[(int64_t)m * ldz + c] = hq;
+    if (dzT) dzT[(int64_t)c * ldt + m] = hq;
+  }
+  if (c == y && stats) {
+    atomicAdd(stats + 0, -logf(p + 1e-10f));
+    atomicAdd(stats + 1, am == y ? 1.f : 0.f);
+    atomicAdd(stats + 2, 1.f);
+  }
+}
+
+hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,
+                             const float* bias, int B, int K, int C, const int32_t* labels,
+                             float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
+                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s) {
+  if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || (ldh & 7) || (ldw & 7) ||
+      (((uintptr_t)H | (uintptr_t)W) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_softmax_xent_k, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
+                     labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats);
   return hipGetLastError();
 }
 

@@ -7,10 +7,13 @@ gradients), fp32 accumulation, fp32 gradients all-reduced across replicas.
 
 Every product is a bf16 "NT" GEMM on v_mfma_f32_16x16x32_bf16
 (kernels/gemm_bf16.hip), split-K for the skinny (M = batch) GEMMs so a step
-fills the 256 CUs, then one epilogue kernel (bias / ReLU / ReLU'-mask / casts /
-transposed copy).  Per step, with L layers: 1 input cast, L forward GEMMs,
-softmax-CE, 2L-1 backward GEMMs, L bias reductions, the all-reduce and L
-update kernels.
+fills the 256 CUs; the epilogue (bias / ReLU / ReLU'-mask / casts / transposed
+copy) runs inside the GEMM, on the last K split of each tile to arrive.  The
+weight-gradient GEMMs carry the SGD update (fp32 master W and the bf16 W / W^T
+copies, vectorised through LDS) and the bias step (row sums of dZ^T) when there
+is one replica.  Per step, with L layers: 1 input cast, L forward GEMMs,
+softmax-CE, 2L-1 backward GEMMs (+ the all-reduce and L update kernels with
+several replicas).
 """
 from __future__ import annotations
 
@@ -32,7 +35,8 @@ def _rup(x: int, m: int) -> int:
 class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
-                 sync: str = "rccl", target_wgs: int = 512, graph: bool = True):
+                 sync: str = "rccl", target_wgs: int = 512, graph: bool = True,
+                 gemm: str = "rows64"):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -43,7 +47,9 @@ class WideMlpTrainer:
             raise ValueError("batch must be a multiple of 8 (16 B bf16 rows)")
         if spec.dims[-1] > 64:
             raise ValueError("softmax kernel supports <= 64 classes")
-        self.spec, self.batch, self.lr, self.sync = spec, batch, lr, sync
+        if gemm not in ("rows64", "splitk"):
+            raise ValueError("gemm must be 'rows64' (full-K batch-row kernel) or 'splitk'")
+        self.spec, self.batch, self.lr, self.sync, self.gemm = spec, batch, lr, sync, gemm
         self.device = dev = self.ctx.device
         self.target_wgs = target_wgs
         d = spec.dims
@@ -67,15 +73,18 @@ class WideMlpTrainer:
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self.views = self.layout.views(self.P)
         self.gviews = self.layout.views(self.G)
-        # GEMM plans: (A, B, M, N, K, splits)
+        # split-K plans of the batch-row GEMMs: name -> (M, N, K, splits); the
+        # weight-gradient GEMMs (K = batch) run unsplit with the SGD epilogue
         self.plans: Dict[str, tuple] = {}
         ws = 0
         for l in range(L):
             ws = max(ws, self._plan(f"f{l}", batch, d[l + 1], self.pd[l]))
-            ws = max(ws, self._plan(f"w{l}", d[l + 1], d[l], batch))
             if l > 0:
                 ws = max(ws, self._plan(f"b{l}", batch, d[l], self.pd[l + 1]))
-        self.Cp = torch.zeros(ws, dtype=torch.float32, device=dev)
+        self.Cp = torch.zeros(ws if gemm == "splitk" else 16, dtype=torch.float32, device=dev)
+        # split-K arrival counters (one per 64x64 tile; every GEMM leaves them 0)
+        tiles = max(math.ceil(M / 64) * math.ceil(N / 64) for (M, N, _, _) in self.plans.values())
+        self.tctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
         self.steps_done = 0
         # One hipGraph per epoch (every batch offset baked in): replaying it
         # removes the ~25 host launches per step.  Single replica only (the
@@ -91,30 +100,42 @@ class WideMlpTrainer:
 
     def _plan(self, name: str, M: int, N: int, K: int) -> int:
         tiles = math.ceil(M / 64) * math.ceil(N / 64)
-        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128)))
+        # <= 8 K splits: the last split of a tile sums the slabs in two batches
+        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128), 8))
         S = self.C.gemm_num_splits(K, splits)
         self.plans[name] = (M, N, K, splits)
         return S * M * N
 
-    def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor) -> int:
+    def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor, **epi) -> int:
+        """One GEMM with its epilogue fused (split-K reduced in-kernel by the
+        last split of each tile)."""
         M, N, K, splits = self.plans[name]
-        return self.C.gemm_bf16_nt(A, B, self.Cp, M, N, K, splits)
+        if self.gemm == "rows64":  # full K per block, no slabs
+            return self.C.gemm_bf16_nt_fused(A, B, M, N, K, splits=0, **epi)
+        return self.C.gemm_bf16_nt_fused(A, B, M, N, K, splits=splits, ws=self.Cp, ctr=self.tctr,
+                                         **epi)
 
     # ----------------------------------------------------------------- step --
     def _step(self) -> None:
         C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
         r0 = (self.steps_done % self.nbatches) * Bt
         C.cast_transpose(self.X[r0:r0 + Bt], Bt, d[0], self.H[0], self.HT[0])
-        for l in range(L):
-            S = self._gemm(f"f{l}", self.H[l], self.Wb[l])
+        fused_head = d[L] <= 16 and self.gemm == "rows64"
+        for l in range(L - 1 if fused_head else L):
             _, b = self.views[l]
             if l < L - 1:
-                C.gemm_epilogue(self.Cp, S, Bt, d[l + 1], bias=b, relu=True, obf=self.H[l + 1],
-                                obfT=self.HT[l + 1])
+                self._gemm(f"f{l}", self.H[l], self.Wb[l], bias=b, relu=True, obf=self.H[l + 1],
+                           obfT=self.HT[l + 1])
             else:
-                C.gemm_epilogue(self.Cp, S, Bt, d[l + 1], bias=b, of32=self.logits)
-        C.softmax_xent(self.logits, self.y[r0:r0 + Bt], Bt, d[L], 1.0 / Bt, self.dZ[L], self.dZT[L],
-                       self.stats)
+                self._gemm(f"f{l}", self.H[l], self.Wb[l], bias=b, of32=self.logits)
+        if fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row)
+            _, b = self.views[L - 1]
+            C.head_softmax_xent(self.H[L - 1], self.Wb[L - 1], b, Bt, self.pd[L - 1], d[L],
+                                self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], self.dZT[L],
+                                self.stats)
+        else:
+            C.softmax_xent(self.logits, self.y[r0:r0 + Bt], Bt, d[L], 1.0 / Bt, self.dZ[L],
+                           self.dZT[L], self.stats)
         world = self.ctx.world_size
         fused_sgd = world == 1
         scale = self.lr / world
@@ -122,17 +143,16 @@ class WideMlpTrainer:
             W, b = self.views[l]
             gW, gb = self.gviews[l]
             if l > 0:  # activation gradient first: it needs the pre-update W_l^T
-                S = self._gemm(f"b{l}", self.dZ[l + 1], self.WbT[l])
-                C.gemm_epilogue(self.Cp, S, Bt, d[l], mask=self.H[l], obf=self.dZ[l], obfT=self.dZT[l])
+                self._gemm(f"b{l}", self.dZ[l + 1], self.WbT[l], mask=self.H[l], obf=self.dZ[l],
+                           obfT=self.dZT[l])
             if fused_sgd:
-                # dW_l = dZ^T H_l with SGD fused in the GEMM epilogue: W -= lr*dW and
-                # the bf16 W / W^T copies are refreshed from the accumulators.
+                # dW_l = dZ^T H_l with SGD fused in the GEMM epilogue: W -= lr*dW, the bf16
+                # W / W^T copies refreshed, and the bias step from the row sums of dZ^T.
                 C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, sgdW=W,
-                                     lr=scale, obf=self.Wb[l], obfT=self.WbT[l])
-                C.rowsum_bf16(self.dZT[l + 1], d[l + 1], Bt, bias=b, lr=scale)
+                                     lr=scale, obf=self.Wb[l], obfT=self.WbT[l], bsgd=b)
             else:
-                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, of32=gW)
-                C.rowsum_bf16(self.dZT[l + 1], d[l + 1], Bt, out=gb)
+                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, of32=gW,
+                                     bgrad=gb)
         if not fused_sgd:
             if self.comm is not None:
                 (self.comm.ring_allreduce_(self.G, 0, 4 << 20) if self.sync == "ring"

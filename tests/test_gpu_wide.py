@@ -76,6 +76,74 @@ def test_wide_training_converges(graph):
     assert last.accuracy > 90.0
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 4096, 4096), (64, 10, 4096), (64, 4096, 16), (50, 70, 520),
+                                   (64, 4096, 784), (130, 48, 96)])
+def test_gemm_rows64_epilogues(M, N, K):
+    """Batch-row kernel (full K per block, 4-way in-block K split) vs fp32."""
+    C = require_native()
+    g = torch.Generator().manual_seed(M + 7 * N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g)
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16)
+    ref = A.float() @ B.float().t()
+    tol = 1e-3 * K ** 0.5
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    o32 = torch.empty(M, N, device=DEV)
+    ob = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    Mt = (M + 15) // 16 * 16
+    obT = torch.zeros(N, Mt, dtype=torch.bfloat16, device=DEV)
+    C.gemm_bf16_nt_fused(Ad, Bd, M, N, K, bias=bias.to(DEV), relu=True, of32=o32, obf=ob,
+                         obfT=obT, splits=0)
+    torch.cuda.synchronize()
+    want = torch.relu(ref + bias)
+    assert (o32.cpu() - want).abs().max().item() < tol
+    assert torch.equal(ob.cpu(), o32.cpu().to(torch.bfloat16))
+    assert torch.equal(obT.cpu()[:, :M].t(), ob.cpu())
+    C.gemm_bf16_nt_fused(Ad, Bd, M, N, K, mask=mask.to(DEV), of32=o32, splits=0)
+    torch.cuda.synchronize()
+    assert (o32.cpu() - ref * (mask.float() > 0)).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("C_,K", [(10, 4096), (16, 784), (3, 64)])
+def test_head_softmax_xent(C_, K):
+    C = require_native()
+    B = 64
+    g = torch.Generator().manual_seed(C_ * K)
+    H = torch.randn(B, K, generator=g).to(torch.bfloat16)
+    W = (0.05 * torch.randn(C_, K, generator=g)).to(torch.bfloat16)
+    b = torch.randn(C_, generator=g)
+    y = torch.randint(0, C_, (B,), generator=g, dtype=torch.int32)
+    logits = torch.empty(B, C_, device=DEV)
+    Cp = (C_ + 15) // 16 * 16
+    dz = torch.zeros(B, Cp, dtype=torch.bfloat16, device=DEV)
+    dzT = torch.zeros(Cp, B, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(4, device=DEV)
+    C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
+                        dzT, stats)
+    torch.cuda.synchronize()
+    z = H.float() @ W.float().t() + b
+    assert (logits.cpu() - z).abs().max().item() < 1e-3
+    p = torch.softmax(z, 1)
+    onehot = torch.nn.functional.one_hot(y.long(), C_).float()
+    want = (p - onehot) / B
+    assert (dz.cpu()[:, :C_].float() - want).abs().max().item() < 1e-3
+    assert torch.equal(dzT.cpu()[:C_].t(), dz.cpu()[:, :C_])
+    assert stats[2].item() == B
+    loss = -torch.log(p.gather(1, y.long().view(-1, 1)) + 1e-10).sum().item()
+    assert abs(stats[0].item() - loss) / loss < 1e-3
+
+
+@pytest.mark.parametrize("gemm", ["rows64", "splitk"])
+def test_wide_gemm_variants_train_identically_close(gemm):
+    spec = MlpSpec((784, 512, 256, 10))
+    ds = synthetic_mnist(64 * 4, seed=8)
+    t = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=4, graph=False, gemm=gemm)
+    t.train_steps(8)
+    st = t.read_stats()
+    assert st.count == 8 * 64 and st.avg_loss < 2.5
+
+
 def test_wide_graph_matches_eager():
     spec = MlpSpec((784, 256, 128, 10))
     ds = synthetic_mnist(64 * 4, seed=5)
@@ -85,3 +153,68 @@ def test_wide_graph_matches_eager():
     b.train_steps(10)
     a.synchronize(); b.synchronize()
     assert torch.equal(a.P.cpu(), b.P.cpu())
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(64, 4096, 4096, 8), (64, 10, 4096, 32), (50, 70, 520, 3),
+                                          (64, 784, 64, 1), (33, 130, 1024, 5)])
+def test_gemm_splitk_fused_epilogue_matches_two_kernel_path(M, N, K, splits):
+    """In-kernel split-K reduction (last split per tile) == slabs + gemm_epilogue,
+    bit for bit, and the tile counters are left re-armed."""
+    C = require_native()
+    g = torch.Generator().manual_seed(M * N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).to(DEV)
+    S = C.gemm_num_splits(K, splits)
+    Cp = torch.zeros(S * M * N, device=DEV)
+    ctr = torch.zeros(((M + 63) // 64) * ((N + 63) // 64), dtype=torch.int32, device=DEV)
+    tr = M % 4 == 0  # transposed bf16 output needs 8 B runs along M
+    for relu, use_mask in ((True, False), (False, True)):
+        want32 = torch.empty(M, N, device=DEV)
+        wantT = torch.zeros(N, M, dtype=torch.bfloat16, device=DEV) if tr else None
+        C.gemm_bf16_nt(A, B, Cp, M, N, K, splits)
+        C.gemm_epilogue(Cp, S, M, N, bias=bias, relu=relu, mask=mask if use_mask else None,
+                        of32=want32, obfT=wantT)
+        got32 = torch.empty(M, N, device=DEV)
+        gotT = torch.zeros(N, M, dtype=torch.bfloat16, device=DEV) if tr else None
+        assert C.gemm_bf16_nt_fused(A, B, M, N, K, bias=bias, relu=relu,
+                                    mask=mask if use_mask else None, of32=got32, obfT=gotT,
+                                    splits=splits, ws=Cp, ctr=ctr) == S
+        torch.cuda.synchronize()
+        assert torch.equal(got32.cpu(), want32.cpu())
+        if tr:
+            assert torch.equal(gotT.cpu(), wantT.cpu())
+        assert int(ctr.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("M,N", [(4096, 784), (256, 512), (10, 4096), (40, 36)])
+def test_dw_gemm_fused_sgd_and_bias(M, N):
+    """dW GEMM with fused SGD (LDS-vectorised path when aligned), bf16 W / W^T
+    refresh and the bias step from the row sums of dZ^T."""
+    C = require_native()
+    K = 64
+    g = torch.Generator().manual_seed(M + N)
+    dZT = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    HT = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(M, N, generator=g)
+    b = torch.randn(M, generator=g)
+    lr = 0.01
+    Wd, bd = W.to(DEV), b.to(DEV)
+    Wb = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    WbT = torch.zeros(N, (M + 15) // 16 * 16, dtype=torch.bfloat16, device=DEV)  # padded like the engine
+    C.gemm_bf16_nt_fused(dZT.to(DEV), HT.to(DEV), M, N, K, sgdW=Wd, lr=lr, obf=Wb, obfT=WbT, bsgd=bd)
+    torch.cuda.synchronize()
+    gW = dZT.float() @ HT.float().t()
+    wantW = W - lr * gW
+    assert (Wd.cpu() - wantW).abs().max().item() < 1e-5
+    assert torch.equal(Wb.cpu(), Wd.cpu().to(torch.bfloat16))
+    assert torch.equal(WbT.cpu()[:, :M].t(), Wb.cpu())
+    wantb = b - lr * dZT.float().sum(1)
+    assert (bd.cpu() - wantb).abs().max().item() < 1e-5
+    gb = torch.zeros(M, device=DEV)
+    G = torch.zeros(M, N, device=DEV)
+    C.gemm_bf16_nt_fused(dZT.to(DEV), HT.to(DEV), M, N, K, of32=G, bgrad=gb)
+    torch.cuda.synchronize()
+    assert (G.cpu() - gW).abs().max().item() < 1e-3
+    assert (gb.cpu() - dZT.float().sum(1)).abs().max().item() < 1e-4
