@@ -402,7 +402,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (S > 1) {
       TORCH_CHECK(ws && ctr, "split-K fused GEMM needs ws (slabs) and ctr (tile counters)");
       check_f32(*ws, "ws");
-      TORCH_CHECK(ws->numel() >= (int64_t)S * M * N, "ws too small: need ", (int64_t)S * M * N);
+      const int64_t tiles = ((N + 63) / 64) * ((M + 63) / 64);
+      TORCH_CHECK(ws->numel() >= (int64_t)S * tiles * 4096, "ws too small: need ", (int64_t)S * tiles * 4096);
       check_cuda(*ctr, "ctr");
       TORCH_CHECK(ctr->scalar_type() == torch::kInt32 &&
                   ctr->numel() >= ((N + 63) / 64) * ((M + 63) / 64), "ctr: int32, one per 64x64 tile");

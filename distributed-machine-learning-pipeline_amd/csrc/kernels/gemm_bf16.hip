@@ -165,8 +165,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float* __restrict__ Cp, int M, int N, int K, int kchunk, GemmEpi epi, int mode,
     int* __restrict__ tile_ctr, int sgd_lds) {
-  __shared__ float tile[64 * kTileLdsStride];
-  __shared__ int s_last;
+  __shared__ float tile[64 * kTileLdsStride];  // the ONE LDS array (also the last-arriver flag)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int mb = blockIdx.y * 64 + (w >> 1) * 32;
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     }
   }
 
-  if (mode == 0 || mode == 2) {
+  if (mode == 0) {
     float* out = Cp + (int64_t)blockIdx.z * M * N;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -243,48 +242,51 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = mb + 16 * x + 4 * g + r;
-            if (m < M) {
-              if (mode == 0) out[(int64_t)m * N + n] = acc[x][y][r];
-              else st_agent(out + (int64_t)m * N + n, acc[x][y][r]);
-            }
+            if (m < M) out[(int64_t)m * N + n] = acc[x][y][r];
           }
         }
       }
-    if (mode == 0) return;
-    // ---- split-K arrival: the last split of this tile finishes it ----------
-    // Slabs are written and read with device-coherent (sc1) accesses, so no
-    // L2 writeback / invalidate fence is needed (those cost ~10s of us with
-    // hundreds of workgroups): completing the stores before the counter
-    // increment is enough.
+    return;
+  }
+  if (mode == 2) {
+    // ---- split-K, last arriver finishes the tile -------------------------
+    // Slabs in the MFMA-native layout (16 floats per thread per split, 16 B
+    // runs): written WRITE-THROUGH (sc1, raw_buffer_store_b128 aux 16) so no
+    // release fence is needed, and read back by the last arriver with sc1
+    // loads (placement-independent; cdna_hip_programming.md split-K recipe).
+    const int T = gridDim.x * gridDim.y;
+    const int tid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int S = gridDim.z;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(Cp, (short)0, 0x7fffffff, 0x00020000);
+    const int base = ((blockIdx.z * T + tid) * 256 + threadIdx.x) * 64;  // bytes
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4, acc[x][y]), rs,
+                                               base + (x * 2 + y) * 16, 0, 16);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int tid = blockIdx.y * gridDim.x + blockIdx.x;
     if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(tile_ctr + tid, 1, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.z - 1;
+      tile[0] = __hip_atomic_fetch_add(tile_ctr + tid, 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == S - 1 ? 1.f : 0.f;
     __syncthreads();
-    if (!s_last) return;
-    const int S = gridDim.z;
+    if (tile[0] == 0.f) return;
+    __syncthreads();  // tile[] is reused by the SGD epilogue below
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) acc[x][y] = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < S; z += 4) {  // split order: bit-identical to the 2-kernel path
-      float v[4][2][2][4];
+    for (int z = 0; z < S; z += 4) {  // split order: deterministic
+      nu4 v[4][4];
 #pragma unroll
       for (int zz = 0; zz < 4; ++zz) {
-        const float* sp = Cp + (int64_t)min(z + zz, S - 1) * M * N;
+        const int zc = min(z + zz, S - 1);
+        const int b = ((zc * T + tid) * 256 + threadIdx.x) * 64;
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-          for (int y = 0; y < 2; ++y) {
-            const int n = min(nb + 16 * y + i, N - 1);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int m = min(mb + 16 * x + 4 * g + r, M - 1);
-              v[zz][x][y][r] = ld_agent(sp + (int64_t)m * N + n);
-            }
-          }
+        for (int p = 0; p < 4; ++p)
+          v[zz][p] = __builtin_amdgcn_raw_buffer_load_b128(rs, b + p * 16, 0, 16);
       }
 #pragma unroll
       for (int zz = 0; zz < 4; ++zz)
@@ -292,9 +294,13 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
 #pragma unroll
           for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 2; ++y)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) acc[x][y][r] += v[zz][x][y][r];
+            for (int y = 0; y < 2; ++y) {
+              const f32x4 f = __builtin_bit_cast(f32x4, v[zz][x * 2 + y]);
+              acc[x][y][0] += f[0];
+              acc[x][y][1] += f[1];
+              acc[x][y][2] += f[2];
+              acc[x][y][3] += f[3];
+            }
         }
     }
     if (threadIdx.x == 0)  // re-arm for the next GEMM using the counters

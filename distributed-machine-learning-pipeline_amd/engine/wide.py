@@ -35,7 +35,7 @@ def _rup(x: int, m: int) -> int:
 class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
-                 sync: str = "rccl", target_wgs: int = 512, graph: bool = True,
+                 sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
                  gemm: str = "rows64"):
         from ..ops.native import require_native
 
@@ -100,11 +100,12 @@ class WideMlpTrainer:
 
     def _plan(self, name: str, M: int, N: int, K: int) -> int:
         tiles = math.ceil(M / 64) * math.ceil(N / 64)
-        # <= 8 K splits: the last split of a tile sums the slabs in two batches
-        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128), 8))
+        # ~one workgroup per CU, <= 4 K splits: the last split of a tile reads
+        # the other slabs in one batch (per-CU bytes, not HBM, bound these GEMMs)
+        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128), 4))
         S = self.C.gemm_num_splits(K, splits)
         self.plans[name] = (M, N, K, splits)
-        return S * M * N
+        return S * tiles * 4096  # slabs: one 64x64 fp32 tile per split
 
     def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor, **epi) -> int:
         """One GEMM with its epilogue fused (split-K reduced in-kernel by the

@@ -167,8 +167,9 @@ def test_gemm_splitk_fused_epilogue_matches_two_kernel_path(M, N, K, splits):
     bias = torch.randn(N, generator=g).to(DEV)
     mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).to(DEV)
     S = C.gemm_num_splits(K, splits)
-    Cp = torch.zeros(S * M * N, device=DEV)
-    ctr = torch.zeros(((M + 63) // 64) * ((N + 63) // 64), dtype=torch.int32, device=DEV)
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    Cp = torch.zeros(max(S * M * N, S * tiles * 4096), device=DEV)
+    ctr = torch.zeros(tiles, dtype=torch.int32, device=DEV)
     tr = M % 4 == 0  # transposed bf16 output needs 8 B runs along M
     for relu, use_mask in ((True, False), (False, True)):
         want32 = torch.empty(M, N, device=DEV)
