@@ -9,8 +9,9 @@ random-init weights of the same architecture; fp32 compute like the reference.
 
 Weak scaling: each rank trains batch 64 on its own shard; global batch = 64*N.
 Every timed step is a full optimizer step: fused forward/backward HIP kernels,
-gradient all-reduce (N>1: fused into the weight-gradient kernel as a one-shot
-exchange over xGMI, or RCCL — chosen at init by a self-test + timing), SGD update.
+gradient sync (N>1: activation exchange or one-shot gradient exchange fused into
+the weight-gradient kernel over xGMI, or RCCL — chosen at init by a self-test +
+timing), SGD update.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: launched by torch.distributed.run, one rank per GPU)
@@ -69,9 +70,12 @@ def main() -> int:
     ap.add_argument("--model", default="784-128-64-10")
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--sync", default="auto", choices=["auto", "xgmi", "rccl", "ring", "torch"],
-                    help="gradient all-reduce (N>1): auto = the fused xGMI peer exchange if it "
-                         "passes its self-test and beats RCCL at init, else RCCL")
+    ap.add_argument("--sync", default="auto", choices=["auto", "xact", "xgmi", "rccl", "ring", "torch"],
+                    help="gradient sync (N>1): xact = activation exchange over xGMI (every GPU "
+                         "pushes its activations and computes the global-batch weight gradients), "
+                         "xgmi = one-shot gradient exchange fused into the weight-gradient kernel, "
+                         "rccl = ncclAllReduce; auto = the fastest of the three measured at init "
+                         "(exchanges only after passing a self-test against an all-reduce)")
     ap.add_argument("--graph-steps", type=int, default=50,
                     help="steps captured per hipGraph (0 = eager C++ launch loop); steps with an "
                          "RCCL collective always run as the eager C++ loop")
@@ -80,7 +84,7 @@ def main() -> int:
                     help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
-                         "two ranks on one GPU); use with --sync xgmi or torch")
+                         "two ranks on one GPU); use with --sync xact, xgmi or torch")
     a = ap.parse_args()
 
     import torch
@@ -139,6 +143,7 @@ def main() -> int:
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "sync": tr.sync_active,
+                "sync_candidates_us": tr.sync_times or None,
                 "graph_steps": a.graph_steps,
                 "lr": a.lr,
             },

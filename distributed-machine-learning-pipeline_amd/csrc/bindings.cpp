@@ -488,7 +488,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       }, py::arg("comm"), py::arg("algo") = 0, py::arg("chunk_bytes") = 1 << 20)
       .def("set_exchange", [](PyMlpRunner& s, PeerExchange* x) { s.r->set_exchange(x); },
            py::arg("exchange").none(true), py::keep_alive<1, 2>())
+      .def("set_act_exchange", [](PyMlpRunner& s, PeerExchange* x, torch::Tensor Xall,
+                                  int64_t xstride) {
+        check_f32(Xall, "Xall");
+        TORCH_CHECK(Xall.is_contiguous(), "Xall must be contiguous");
+        TORCH_CHECK(x == nullptr || Xall.numel() >= (int64_t)x->nranks() * xstride,
+                    "Xall holds fewer than nranks shards");
+        s.r->set_act_exchange(x, Xall.data_ptr<float>(), xstride);
+      }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
+      .def("exchange_mode", [](PyMlpRunner& s) { return s.r->exchange_mode(); })
       .def("plan", [](PyMlpRunner& s) {
         const MlpLaunchCfg c = s.r->cfg();
         return py::make_tuple(c.kchunk, c.nsplit);
@@ -514,6 +524,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_wgrad_tiles", [](const std::vector<int64_t>& desc) {
     return mlp_wgrad_tiles(desc_from_list(desc));
   });
+  m.def("mlp_xact_payload", [](const std::vector<int64_t>& desc) {
+    return mlp_xact_payload(desc_from_list(desc));
+  });
+  m.def("mlp_xact_supported", [](const std::vector<int64_t>& desc) {
+    return mlp_xact_supported(desc_from_list(desc));
+  });
   py::class_<PeerExchange>(m, "PeerExchange")
       .def(py::init<int, int64_t, int>(), py::arg("device"), py::arg("half_floats"),
            py::arg("ntiles"))
@@ -531,6 +547,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       })
       .def("connect_local", &PeerExchange::connect_local)
       .def("reset", [](PeerExchange& x) { x.reset(cur_stream()); })
+      // Probe/debug only: preset every flag of this exchange (e.g. to a value
+      // no step reaches, so a lone replica measures its kernels without waits).
+      .def("fill_flags", [](PeerExchange& x, uint64_t v) {
+        std::vector<uint64_t> h((size_t)x.ntiles(), v);
+        DSML_HIP_CHECK(hipMemcpy(x.flags(), h.data(), h.size() * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice));
+      })
       .def("error", [](PeerExchange& x) {
         py::gil_scoped_release nogil;
         return x.error(cur_stream());

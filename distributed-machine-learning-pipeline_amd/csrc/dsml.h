@@ -108,6 +108,20 @@ int mlp_wgrad_tiles(const MlpDesc& d);
 int xchg_allreduce_blocks(int64_t n, int max_blocks, int* unroll);
 hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
                               int max_blocks, uint64_t seq, hipStream_t s);
+// Activation exchange (kernels/mlp_f32_xact.hip): K_C variant that pushes this
+// replica's activations and activation gradients (H_l, dZ_l, in MFMA fragment
+// order: mlp_xact_payload floats) to every rank and computes the global-batch
+// weight gradients from all N images, SGD with lr / N.  Xswz holds every
+// rank's input shard in fragment order (rank r at Xswz + r * xstride; see
+// parallel/xchg.py swizzle_inputs).  Exchange buffers: half >= nranks *
+// payload, ntiles = nranks * payload / 1024 (one flag per rank and strip).
+// Needs batch <= 64 and every layer input dim a multiple of 16
+// (mlp_xact_supported).
+int mlp_xact_payload(const MlpDesc& d);
+bool mlp_xact_supported(const MlpDesc& d);
+hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
+                              int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
+                              hipStream_t s);
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
                               const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
 

@@ -1,0 +1,330 @@
+// Activation-exchange data parallelism for the fused fp32 MLP step ("xact").
+//
+// The gradient all-reduce the reference performs every step
+// (gpu_coordinator_server.go:272-566, client.go:614-640) moves
+// the whole 437 KB weight gradient of 784-128-64-10.  With a 64-row batch per
+// GPU that is the wrong thing to put on an xGMI link: every weight gradient is
+// dW_l = dZ_l^T . H_{l-1} over the batch rows, and the factors are far smaller
+// than the product (dZ_1 is 64 x 128, dW_1 is 128 x 784).  So instead of
+// reducing dW, every replica PUSHES its activations and activation gradients
+// (H_1, dZ_1, H_2, dZ_2, dZ_3: the workspace image written by K_B, 100 KB) into
+// every peer's receive buffer, and every replica then computes the weight
+// gradients of the WHOLE global batch itself:
+//
+//     dW_l = sum_r dZ_{l,r}^T . H_{l-1,r}       (r = 0..N-1 in rank order)
+//
+// with H_0 = X read from the replicated dataset shard of rank r (MNIST-scale
+// data fits every GPU's HBM many times over).  Per step each xGMI link carries
+// 100 KB instead of 437 KB (one-shot) and no reduction crosses a link; the
+// price is N x the (tiny) weight-gradient FLOPs on every GPU, which MFMA
+// absorbs.  Sums run in the same order on every rank, so replicas stay
+// bit-identical, and the result equals the all-reduced gradient up to fp32
+// summation order.
+//
+// One launch replaces K_C:
+//   blocks [0, S)           pushers: block s loads 16-column strip s of this
+//                           rank's H_l / dZ_l from the workspace (coalesced),
+//                           transposes it through LDS into fragment order and
+//                           writes it into every rank's receive slot for this
+//                           rank (itself included, so tile blocks read all N
+//                           images the same way) with 16 B system-scope stores
+//                           (sc0 sc1) over xGMI, drains them and raises flag
+//                           (me, s) in each rank's memory.  Pushers never wait.
+//   blocks [S, ...)         one 16(n) x 32(k) tile of some dW_l per block,
+//                           4 waves splitting the N x B/4 MFMA k-steps; they
+//                           poll only LOCAL flags, and only those of the <= 3
+//                           strips they read, load the N images from local HBM
+//                           with sc0 sc1 16 B loads, reduce the 4 wave partials
+//                           through LDS in wave order, apply SGD (lr / N).
+// Pushers have the lowest block ids, so they are dispatched before any tile
+// block can occupy a CU: a GPU never waits on work it has not started.
+// Receive slots alternate by step parity (a peer is at most one step ahead).
+//
+// Fragment-order images.  A replica's image is not the workspace layout: the
+// pushers gather it into the MFMA operand order of v_mfma_f32_16x16x4_f32, so
+// a tile wave fetches its 4 k-steps of a 16-column strip with ONE 16 B load
+// per lane.  For an activation matrix M [B x D] (B <= 64 rows, zero-padded),
+// strip t (columns 16t..16t+15) is 1024 floats laid out [w][lane][j]:
+//     img[t][w][lane = 16q + i][j] = M[row = 4w + 16j + q][col = 16t + i]
+// i.e. wave w's k-steps are s = w + 4j (rows 4s + q), lane (i, q) holds the
+// operand value of k-step s.  The input batch X is kept in the same order on
+// the host side (parallel/xchg.py swizzle_inputs), shard by shard.
+#include "common.h"
+#include "../dsml.h"
+
+namespace dsml {
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint64_t xa_u64;
+typedef float xa_f4 __attribute__((ext_vector_type(4)));
+constexpr int kSys = 1 | 16;  // buffer aux: sc0 | sc1 = system scope
+
+__device__ __forceinline__ uint64_t xa_ld_flag(const uint64_t* p) {
+  return __hip_atomic_load((const xa_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void xa_st_flag(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((xa_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t xa_ctr(const int64_t* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xa_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+
+constexpr int kXaWaves = 4;
+constexpr int kStrip = 1024;  // floats of one 16-column strip of an image matrix
+
+__host__ __device__ inline int xa_strips(int D) { return (D + 15) >> 4; }
+
+// Image segment of layer l's matrix: which = 0 -> H_l (1 <= l < L), 1 -> dZ_l (1 <= l <= L).
+// Returns its float offset; segments follow ws order (H_1, dZ_1, H_2, dZ_2, ..., dZ_L).
+__host__ __device__ inline int64_t xa_seg_off(const MlpDesc& d, int l, int which) {
+  int64_t off = 0;
+  for (int m = 1; m <= d.nlayers; ++m) {
+    const int64_t sz = (int64_t)xa_strips(d.dims[m]) * kStrip;
+    if (m < d.nlayers) {
+      if (m == l && which == 0) return off;
+      off += sz;
+    }
+    if (m == l && which == 1) return off;
+    off += sz;
+  }
+  return off;  // total
+}
+
+// Segment of image strip s: layer m's H (which 0) or dZ (which 1), strip t of it.
+__device__ __forceinline__ void xa_strip_seg(const MlpDesc& d, int s, int& m, int& which,
+                                             int& t) {
+  int base = 0;
+  for (m = 1; m <= d.nlayers; ++m) {
+    const int n = xa_strips(d.dims[m]);
+    if (m < d.nlayers) {
+      if (s < base + n) { which = 0; t = s - base; return; }
+      base += n;
+    }
+    if (s < base + n) { which = 1; t = s - base; return; }
+    base += n;
+  }
+  m = d.nlayers; which = 1; t = 0;  // unreachable for s < nstrips
+}
+
+__global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
+    const float* __restrict__ Xswz, int64_t xstride, float* __restrict__ P,
+    const float* __restrict__ ws, int64_t* __restrict__ ctr, MlpDesc d, float lr, XchgArgs xa,
+    int nstrips) {
+  __shared__ float red[kXaWaves][9][64];  // pushers reuse it as the 64 x 17 transpose tile
+  __shared__ int flag_ok;
+  const uint64_t step = xa_ctr(ctr) - 1;  // K_A advanced A to step + 1
+  const uint64_t want = step + 1;
+  const int N = xa.nranks, me = xa.rank;
+  const XchgTab* __restrict__ tab = xa.tab;
+  const int64_t par = (int64_t)(step & 1) * xa.half;
+  const int64_t payload = (int64_t)nstrips * kStrip;
+  const int tid = threadIdx.x;
+  const int B = d.batch;
+
+  if ((int)blockIdx.x < nstrips) {
+    // ------------------------------------------------------------- pusher --
+    // Block s: strip s of this rank's image -> every rank (itself included).
+    const int s = blockIdx.x;
+    int m, which, t;
+    xa_strip_seg(d, s, m, which, t);
+    const int D = d.dims[m];
+    const float* src = ws + (which ? d.dz_off[m] : d.act_off[m]);
+    float* tile = &red[0][0][0];
+    {  // 64 rows x 16 columns, one float4 per thread, zero-padded
+      const int row = tid >> 2, c0 = 16 * t + 4 * (tid & 3);
+      float v[4];
+      if (row < B && (D & 3) == 0 && c0 + 3 < D) {
+        const float4 x = *reinterpret_cast<const float4*>(src + (int64_t)row * D + c0);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = (row < B && c0 + k < D) ? src[(int64_t)row * D + c0 + k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tile[row * 17 + 4 * (tid & 3) + k] = v[k];
+    }
+    __syncthreads();
+    const int w = tid >> 6, ln = tid & 63, i = ln & 15, q = ln >> 4;
+    xa_f4 f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = tile[(4 * w + 16 * j + q) * 17 + i];
+    const int64_t off = (int64_t)me * payload + (int64_t)s * kStrip + tid * 4;  // floats
+    for (int dst = 0; dst < N; ++dst)
+      __builtin_amdgcn_raw_buffer_store_b128(f, xa_rsrc(tab->buf[dst] + par), (int)(off * 4), 0,
+                                             kSys);
+    // every storing wave drains its stores, then one lane per rank raises the flag
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < N) xa_st_flag(tab->flags[tid] + me * nstrips + s, want);
+    if (blockIdx.x == 0 && tid == 0) {
+      // step-counter hand-off B = A (the tile blocks never read B)
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(ctr + 1), xa_ctr(ctr), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ tile --
+  int bid = blockIdx.x - nstrips;
+  int l = 0;
+  for (; l < d.nlayers - 1; ++l) {
+    const int nt = ((d.dims[l + 1] + 15) >> 4) * ((d.dims[l] + 31) >> 5);
+    if (bid < nt) break;
+    bid -= nt;
+  }
+  const int Nn = d.dims[l + 1], K = d.dims[l];
+  const int ntk = (K + 31) >> 5;
+  const int tn = bid / ntk, tk = bid - tn * ntk;
+  const int lane = tid & 63, w = tid >> 6, i = lane & 15, q = lane >> 4;
+  const int n = tn * 16 + i;
+  const int k0 = tk * 32 + i, k1 = k0 + 16;
+  const bool nv = n < Nn, k0v = k0 < K, k1v = k1 < K;
+  const bool s1v = 32 * tk + 16 < K;  // second 16-column strip of the tile exists
+  const int nc = nv ? n : Nn - 1, k0c = k0v ? k0 : K - 1, k1c = k1v ? k1 : K - 1;
+  const int64_t woff = d.w_off[l];
+
+  // old weights of this tile (wave 0 applies the update) — issued early
+  float wold[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  float bold = 0.f;
+  if (w == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = tn * 16 + 4 * q + r;
+      const float* wr = P + woff + (int64_t)(row < Nn ? row : Nn - 1) * K;
+      wold[r][0] = wr[k0c];
+      wold[r][1] = wr[k1c];
+    }
+    bold = P[d.b_off[l] + nc];
+  }
+
+  // wait for the strips this tile reads, from every rank (local flags):
+  // threads [0,64) poll dZ_{l+1} strip tn, [64,128) H_l strip 2tk, [128,192) 2tk+1
+  const int sdz = (int)(xa_seg_off(d, l + 1, 1) / kStrip) + tn;
+  const int sh = l == 0 ? -1 : (int)(xa_seg_off(d, l, 0) / kStrip) + 2 * tk;
+  if (tid == 0) flag_ok = 1;
+  __syncthreads();
+  {
+    const int part = tid >> 6, src = tid & 63;
+    const int strip = part == 0 ? sdz : (sh < 0 || (part == 2 && !s1v) ? -1 : sh + part - 1);
+    if (part < 3 && src < N && strip >= 0) {
+      const uint64_t* f = tab->flags[me] + src * nstrips + strip;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (xa_ld_flag(f) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          flag_ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
+
+  // Every rank's operands: one 16 B fragment load per matrix strip and lane.
+  const __amdgpu_buffer_rsrc_t rv = xa_rsrc(tab->buf[me] + par);
+  const int64_t frag = (int64_t)w * 256 + lane * 4;  // floats within a strip
+  const int64_t dzo = (int64_t)sdz * kStrip + frag;
+  const int64_t ao = l == 0 ? 0 : (int64_t)sh * kStrip - (int64_t)(2 * tk) * kStrip;
+  const int64_t bat = (int64_t)(step % (uint64_t)d.nbatches) * xa_strips(K) * kStrip;
+  const int64_t s0 = (int64_t)(2 * tk) * kStrip + frag, s1 = s0 + kStrip;
+  xa_f4 av[kMaxPeers], b0[kMaxPeers], b1[kMaxPeers];
+#pragma unroll
+  for (int r = 0; r < kMaxPeers; ++r) {
+    if (r < N) {
+      const int64_t img = (int64_t)r * payload;
+      av[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + dzo) * 4), 0, kSys);
+      if (l == 0) {
+        const float* xr = Xswz + (int64_t)r * xstride + bat;
+        b0[r] = *reinterpret_cast<const xa_f4*>(xr + s0);
+        b1[r] = s1v ? *reinterpret_cast<const xa_f4*>(xr + s1) : xa_f4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        b0[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + ao + s0) * 4), 0, kSys);
+        b1[r] = s1v ? __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + ao + s1) * 4), 0, kSys)
+                    : xa_f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+#pragma unroll
+  for (int r = 0; r < kMaxPeers; ++r) {
+    if (r < N) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // zero padding rows/columns contribute 0
+        dbacc += av[r][j];
+        acc0 = mfma_f32_16x16x4(av[r][j], b0[r][j], acc0);
+        acc1 = mfma_f32_16x16x4(av[r][j], b1[r][j], acc1);
+      }
+    }
+  }
+  dbacc += __shfl_xor(dbacc, 16, 64);
+  dbacc += __shfl_xor(dbacc, 32, 64);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[w][r][lane] = acc0[r];
+    red[w][4 + r][lane] = acc1[r];
+  }
+  red[w][8][lane] = dbacc;
+  __syncthreads();
+  if (w != 0 || !flag_ok) return;  // a timed-out peer: leave the weights alone
+  float s0v[4], s1v4[4], sb = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s0v[r] = s1v4[r] = 0.f;
+#pragma unroll
+  for (int v = 0; v < kXaWaves; ++v) {  // wave order: identical on every rank
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s0v[r] += red[v][r][lane];
+      s1v4[r] += red[v][4 + r][lane];
+    }
+    sb += red[v][8][lane];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = tn * 16 + 4 * q + r;
+    if (row < Nn) {
+      float* wr = P + woff + (int64_t)row * K;
+      if (k0v) wr[k0] = wold[r][0] - lr * s0v[r];
+      if (k1v) wr[k1] = wold[r][1] - lr * s1v4[r];
+    }
+  }
+  if (tk == 0 && q == 0 && nv) P[d.b_off[l] + n] = bold - lr * sb;
+}
+
+}  // namespace
+
+int mlp_xact_payload(const MlpDesc& d) { return (int)xa_seg_off(d, d.nlayers + 1, 0); }
+
+bool mlp_xact_supported(const MlpDesc& d) {
+  if (d.batch > 64) return false;
+  for (int l = 0; l < d.nlayers; ++l)
+    if (d.dims[l] % 16) return false;  // K of every weight gradient: whole 16-column strips
+  return true;
+}
+
+hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
+                              int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
+                              hipStream_t s) {
+  const int payload = mlp_xact_payload(d);
+  const int nstrips = payload / kStrip;
+  if (ctr == nullptr || x.tab == nullptr || x.err == nullptr || x.nranks < 1 ||
+      x.nranks > kMaxPeers || x.rank < 0 || x.rank >= x.nranks || !mlp_xact_supported(d) ||
+      x.half < (int64_t)x.nranks * payload || (int64_t)2 * x.half * 4 > 0x7fffffffLL ||
+      xstride < (int64_t)d.nbatches * xa_strips(d.dims[0]) * kStrip)
+    return hipErrorInvalidValue;
+  dim3 grid(nstrips + mlp_wgrad_tiles(d));
+  hipLaunchKernelGGL(mlp_f32_wgrad_xact_k, grid, dim3(64 * kXaWaves), 0, s, Xswz, xstride, P, ws,
+                     ctr, d, lr_over_n, x, nstrips);
+  return hipGetLastError();
+}
+
+}  // namespace dsml

@@ -229,6 +229,31 @@ void MlpRunner::set_exchange(PeerExchange* x) {
       throw std::invalid_argument("set_exchange: exchange buffers sized for another model");
   }
   xchg_ = x;
+  xact_ = false;
+  reset_graph();
+}
+
+void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride) {
+  if (x == nullptr) {
+    set_exchange(nullptr);
+    return;
+  }
+  if (!x->connected()) throw std::invalid_argument("set_act_exchange: exchange not connected");
+  if (mom_ != 0.f || wd_ != 0.f)
+    throw std::invalid_argument("the activation exchange implements plain SGD only");
+  const int n = x->nranks();
+  if (n < 2) throw std::invalid_argument("set_act_exchange: needs >= 2 ranks");
+  if (!mlp_xact_supported(d_))
+    throw std::invalid_argument("set_act_exchange: needs batch <= 64 and layer inputs % 16 == 0");
+  if (x->ntiles() != n * (mlp_xact_payload(d_) / 1024) ||
+      x->half() < (int64_t)n * mlp_xact_payload(d_))
+    throw std::invalid_argument("set_act_exchange: exchange buffers sized for another model");
+  if (Xall == nullptr || xstride < (int64_t)d_.nbatches * 64 * d_.dims[0])
+    throw std::invalid_argument("set_act_exchange: replicated input shards too small");
+  xchg_ = x;
+  xact_ = true;
+  xall_ = Xall;
+  xstride_ = xstride;
   reset_graph();
 }
 
@@ -264,8 +289,12 @@ void MlpRunner::enqueue_step(hipStream_t s) {
     DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, b_.labels, b_.ws, s));
     DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
                                     b_.stats, 1, 1.0f / (float)d_.batch, s));
-    DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
-                                      lr_ / (float)xchg_->nranks(), xchg_->args(), s));
+    if (xact_)
+      DSML_HIP_CHECK(mlp_f32_wgrad_xact(xall_, xstride_, b_.P, b_.ws, b_.ctr, d_,
+                                        lr_ / (float)xchg_->nranks(), xchg_->args(), s));
+    else
+      DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
+                                        lr_ / (float)xchg_->nranks(), xchg_->args(), s));
     return;
   }
   const bool multi = comm_ != nullptr && comm_->nranks() > 1;

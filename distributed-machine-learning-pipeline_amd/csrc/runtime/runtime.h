@@ -260,7 +260,13 @@ class MlpRunner {
   // Gradient all-reduce fused into the weight-gradient kernel over xGMI
   // (plain SGD only).  Takes precedence over the RCCL communicator.
   void set_exchange(PeerExchange* x);
+  // Activation exchange (kernels/mlp_f32_xact.hip): K_C pushes this replica's
+  // activations to every rank and computes the global-batch weight gradients;
+  // Xall holds every rank's input shard in MFMA fragment order (rank r at
+  // Xall + r * xstride).  Replaces set_exchange's mode while set.
+  void set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride);
   bool exchange_active() const { return xchg_ != nullptr; }
+  int exchange_mode() const { return xchg_ == nullptr ? 0 : (xact_ ? 2 : 1); }
   // Enqueue one full step on stream s (no host sync).
   void enqueue_step(hipStream_t s);
   // Enqueue only fwd/bwd (grads -> G, no update) — used by the DP engine when
@@ -288,6 +294,9 @@ class MlpRunner {
   float lr_, mom_, wd_;
   RcclComm* comm_ = nullptr;
   PeerExchange* xchg_ = nullptr;
+  bool xact_ = false;
+  const float* xall_ = nullptr;
+  int64_t xstride_ = 0;
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;

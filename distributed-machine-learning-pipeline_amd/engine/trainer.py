@@ -26,7 +26,8 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("auto", "xgmi", "rccl", "ring", "torch")
+SYNC_MODES = ("auto", "xact", "xgmi", "rccl", "ring", "torch")
+EXCHANGE_MODES = ("xact", "xgmi")  # fused into K_C over xGMI peer memory
 
 
 @dataclass
@@ -101,6 +102,9 @@ class MlpTrainer:
         self.capture_collectives = capture_collectives
         self.xchg_timeout_ms = xchg_timeout_ms
         self.sync_active = "none"
+        self.sync_times: Dict[str, float] = {}
+        self.Xall: Optional[torch.Tensor] = None
+        self._exchanges: Dict[str, object] = {}
         self.runner = None
         if self.device.type == "cuda":
             self._init_hip(ring_chunk_bytes)
@@ -132,73 +136,156 @@ class MlpTrainer:
             self.sync_active = "torch"
             return
         plain = not (self.momentum or self.weight_decay)
-        if self.sync == "xgmi" and not plain:
-            raise ValueError("sync='xgmi' implements plain SGD; use rccl for momentum/weight decay")
-        if self.sync != "xgmi":  # xgmi is strict: no RCCL fallback communicator
+        if self.sync in EXCHANGE_MODES and not plain:
+            raise ValueError(f"sync='{self.sync}' implements plain SGD; use rccl for momentum/"
+                             "weight decay")
+        if self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
-        if self.sync == "xgmi" or (self.sync == "auto" and plain and _xgmi_eligible(self.ctx)):
-            self._init_xgmi(strict=self.sync == "xgmi")
+        if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain
+                                           and _xgmi_eligible(self.ctx)):
+            self._init_exchanges()
 
-    def _init_xgmi(self, strict: bool) -> None:
-        """Set up the fused xGMI exchange, check one step against a
-        torch.distributed all-reduce, and (sync='auto') keep it only if it is
-        also faster than the RCCL step.  Every decision is collective."""
+    # ------------------------------------------------------ xGMI exchanges --
+    def _gather_inputs(self) -> torch.Tensor:
+        """Every rank's input shard, replicated on this GPU in MFMA fragment
+        order (parallel/xchg.py swizzle_inputs) — the activation exchange reads
+        every rank's batch rows locally.  Collective."""
+        import torch.distributed as dist
+
+        from ..parallel.xchg import ExchangeUnavailable
+
+        ctx = self.ctx
+        rows = self.nbatches * self.batch
+        lo = ctx.all_reduce_scalars(float(rows), op="min")[0]
+        hi = ctx.all_reduce_scalars(float(rows), op="max")[0]
+        if lo != hi:
+            raise ExchangeUnavailable("ranks hold different numbers of batches")
+        own = self.X[:rows, : self.spec.dims[0]].contiguous()
+        if ctx.backend == "nccl":
+            out = torch.empty((ctx.world_size,) + tuple(own.shape), dtype=own.dtype,
+                              device=self.device)
+            dist.all_gather_into_tensor(out, own)
+        else:
+            parts = [torch.empty(own.shape, dtype=own.dtype) for _ in range(ctx.world_size)]
+            dist.all_gather(parts, own.cpu())
+            out = torch.stack(parts).to(self.device)
+        from ..parallel.xchg import swizzle_inputs
+
+        return swizzle_inputs(out, self.batch)
+
+    def _activate(self, mode: Optional[str]) -> None:
+        if mode is None:
+            self.runner.set_exchange(None)
+            self.xchg = None
+        elif mode == "xgmi":
+            self.xchg = self._exchanges["xgmi"]
+            self.runner.set_exchange(self.xchg)
+        else:
+            self.xchg = self._exchanges["xact"]
+            self.runner.set_act_exchange(self.xchg, self.Xall, self.Xall[0].numel())  # fragment order
+
+    def _setup_exchange(self, mode: str) -> str:
+        """Collective: build `mode`'s buffers, check one step against a
+        torch.distributed all-reduce.  Returns '' or the (agreed) error."""
         from ..parallel import xchg as X
 
-        err = ""
         try:
-            self.xchg = X.make_peer_exchange(self.ctx, self.layout, self.xchg_timeout_ms)
+            if mode == "xact":
+                if not X.act_supported(self.layout):
+                    raise X.ExchangeUnavailable("activation exchange needs batch <= 64 and "
+                                                "layer input dims that are multiples of 16")
+                if self.Xall is None:
+                    self.Xall = self._gather_inputs()
+                x = X.make_act_exchange(self.ctx, self.layout, self.xchg_timeout_ms)
+            else:
+                x = X.make_peer_exchange(self.ctx, self.layout, self.xchg_timeout_ms)
         except X.ExchangeUnavailable as e:  # agreed on every rank
-            err = str(e)
-        if not err:
-            self.runner.set_exchange(self.xchg)
-            diff = X.verify_against_allreduce(self)  # collective, same result on all ranks
-            if not diff <= 1e-5:
-                err = f"self-test mismatch {diff}"
-        bad = bool(err)
-        if not bad and self.sync == "auto":
-            t_x = self._time_steps(20)
-            self.runner.set_exchange(None)
-            t_r = self._time_steps(20)
-            if t_x < t_r:
-                self.runner.set_exchange(self.xchg)
-            log.info("sync auto: xgmi %.1f us/step, rccl %.1f us/step", 1e6 * t_x, 1e6 * t_r)
-        elif bad:
-            if strict:
-                raise RuntimeError(f"xGMI exchange unavailable: {err or 'failed on a peer'}")
-            log.warning("xGMI exchange disabled (%s); using RCCL", err or "failed on a peer")
-            self.runner.set_exchange(None)
-        self.sync_active = "xgmi" if (not bad and self._xchg_on()) else self.sync_active
-        if not self._xchg_on():
-            self.xchg = None
+            return str(e)
+        self._exchanges[mode] = x
+        self._activate(mode)
+        diff = X.verify_against_allreduce(self)  # collective, same result on all ranks
+        self._activate(None)
+        return "" if diff <= 1e-5 else f"self-test mismatch {diff}"
 
-    def _xchg_on(self) -> bool:
-        return bool(self.runner.exchange_active())
+    def _init_exchanges(self) -> None:
+        """Set up the fused xGMI exchanges, self-test each against a
+        torch.distributed all-reduce and keep (sync='auto') the fastest of
+        {xact, xgmi, rccl} measured on this node.  Every decision is collective.
+
+        * xact — activation exchange: each GPU pushes its 100 KB of activations
+          and activation gradients to every peer and computes the global-batch
+          weight gradients itself (kernels/mlp_f32_xact.hip);
+        * xgmi — one-shot gradient exchange: each GPU reads every peer's 437 KB
+          of weight-gradient tiles (kernels/mlp_f32.hip XCHG path);
+        * rccl — ncclAllReduce of the gradient between fwd/bwd and the update."""
+        self._exchanges: Dict[str, object] = {}
+        self.Xall = None
+        strict = self.sync in EXCHANGE_MODES
+        modes = [self.sync] if strict else ["xact", "xgmi"]
+        ok = []
+        for m in modes:
+            err = self._setup_exchange(m)
+            if err:
+                if strict:
+                    raise RuntimeError(f"{m} exchange unavailable: {err}")
+                log.warning("%s exchange disabled (%s)", m, err)
+            else:
+                ok.append(m)
+        choice = ok[0] if ok else None
+        if self.sync == "auto" and ok:
+            times = {}
+            for m in ok + [None]:
+                self._activate(m)
+                times[m or "rccl"] = self._time_steps(20)
+            choice = min(times, key=times.get)
+            choice = None if choice == "rccl" else choice
+            log.info("sync auto: %s", ", ".join(f"{k} {1e6 * v:.1f} us/step"
+                                                for k, v in times.items()))
+            self.sync_times = {k: round(1e6 * v, 2) for k, v in times.items()}
+        self._activate(choice)  # drops any graph captured while timing
+        self._captured = False
+        if choice is not None:
+            self.sync_active = choice
+        if choice != "xact":
+            self.Xall = None  # the replicated inputs are only read by xact
 
     def _time_steps(self, n: int) -> float:
-        """Max-over-ranks wall time per step of `n` eager steps; state restored."""
+        """Max-over-ranks wall time per step, run the way train_steps will run
+        the active mode (graph replay for the fused exchanges, the eager C++
+        loop for a step with an RCCL collective); state restored."""
         from ..parallel import xchg as X
 
         P0, ctr0, st0 = self.P.clone(), self.ctr.clone(), self.stats.clone()
-        self.runner.step(2)
+        if self.graph_steps > 0 and self.runner.exchange_active():
+            self.runner.capture(self.graph_steps, True)
+            reps = max(1, n // self.graph_steps)
+            n = reps * self.graph_steps
+
+            def run():
+                self.runner.replay(reps)
+            self.runner.replay(1)  # warm-up
+        else:
+            def run():
+                self.runner.step(n)
+            self.runner.step(2)
         self.runner.synchronize()
         self.ctx.barrier()
         t0 = time.perf_counter()
-        self.runner.step(n)
+        run()
         self.runner.synchronize()
         dt = (time.perf_counter() - t0) / n
         dt = self.ctx.all_reduce_scalars(dt, op="max")[0]
         self.P.copy_(P0)
         self.ctr.copy_(ctr0)
         self.stats.copy_(st0)
-        if self.xchg is not None:
-            X.reset_group(self.ctx, self.xchg)
-        else:
-            torch.cuda.synchronize(self.device)
-            self.ctx.barrier()
+        # the counters went back: rewind every exchange's flags (collective)
+        for x in getattr(self, "_exchanges", {}).values():
+            X.reset_group(self.ctx, x)
+        torch.cuda.synchronize(self.device)
+        self.ctx.barrier()
         return dt
 
     def _hip_step_torch_sync(self, n: int) -> None:

@@ -42,6 +42,52 @@ def make_peer_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 
     return make_exchange(ctx, layout.nparams, wgrad_tiles(layout), timeout_ms)
 
 
+def act_payload(layout: MlpLayout) -> int:
+    """Floats of one replica's pushed image (H_l, dZ_l in MFMA fragment order)."""
+    from ..ops.native import require_native
+
+    return require_native().mlp_xact_payload(layout.desc_list())
+
+
+def act_supported(layout: MlpLayout) -> bool:
+    d = layout.spec.dims
+    return layout.batch <= 64 and all(x % 16 == 0 for x in d[:-1])
+
+
+def swizzle_inputs(X: torch.Tensor, batch: int) -> torch.Tensor:
+    """Input shards [N, rows, >= K] -> MFMA fragment order for the activation
+    exchange (kernels/mlp_f32_xact.hip): per batch b and 16-column strip t,
+    ``[w][lane = 16q + i][j] = X[b*batch + 4w + 16j + q][16t + i]`` with rows
+    past the batch zero-padded to 64.  Returns [N, nbatches, K/16, 4, 64, 4]."""
+    N, rows, _ = X.shape
+    nb = rows // batch
+    K = X.shape[2]
+    if K % 16 or batch > 64:
+        raise ValueError("fragment order needs K % 16 == 0 and batch <= 64")
+    x = X[:, : nb * batch].reshape(N, nb, batch, K)
+    if batch < 64:
+        x = torch.nn.functional.pad(x, (0, 0, 0, 64 - batch))
+    x = x.reshape(N, nb, 4, 4, 4, K // 16, 16)        # [N, nb, j, w, q, t, i]
+    x = x.permute(0, 1, 5, 3, 4, 6, 2).contiguous()   # [N, nb, t, w, q, i, j]
+    return x.reshape(N, nb, K // 16, 4, 64, 4)
+
+
+def make_act_exchange(ctx: DistContext, layout: MlpLayout, timeout_ms: float = 10000.0):
+    """Receive buffers for the activation exchange (kernels/mlp_f32_xact.hip):
+    per parity one slot of ``act_payload`` floats per source rank, and one
+    flag per (source rank, 16-column strip)."""
+    n = ctx.world_size
+    p = act_payload(layout)
+    return make_exchange(ctx, n * p, n * (p // 1024), timeout_ms)
+
+
+def make_local_act_group(layout: MlpLayout, devices: List[int], timeout_ms: float = 10000.0):
+    """Activation-exchange buffers for N replicas living in one process."""
+    n = len(devices)
+    p = act_payload(layout)
+    return make_local_group(None, devices, timeout_ms, half_floats=n * p, ntiles=n * (p // 1024))
+
+
 def make_exchange(ctx: DistContext, half_floats: int, ntiles: int, timeout_ms: float = 10000.0):
     """Collective: returns a connected ``_C.PeerExchange`` for this rank, or
     raises :class:`ExchangeUnavailable` on EVERY rank if any rank failed (the

@@ -43,7 +43,7 @@ class TrainConfig:
     data: str = "synthetic"               # synthetic | mnist (idx files under data_dir)
     data_dir: str = ""
     samples: int = 60032                  # synthetic samples per replica
-    sync: str = "rccl"                    # rccl | ring | torch
+    sync: str = "rccl"                    # auto | xact | xgmi | rccl | ring | torch
     ring_chunk_bytes: int = 1 << 20
     graph_steps: int = 50                 # steps per hipGraph (single replica); 0 = eager
     backend: str = "auto"                 # torch.distributed backend: auto | nccl | gloo

@@ -14,7 +14,7 @@ from hipdsml.data.mnist import synthetic_mnist
 from hipdsml.engine.trainer import MlpTrainer
 from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
 from hipdsml.parallel.dist import DistContext
-from hipdsml.parallel.xchg import make_local_group
+from hipdsml.parallel.xchg import make_local_act_group, make_local_group, swizzle_inputs
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -74,30 +74,75 @@ def test_missing_peer_times_out_instead_of_hanging():
     assert xs[0].error() == 0
 
 
+def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0):
+    """Activation exchange between `world` replicas of one process."""
+    trs = [MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * nb, seed=300 + r), batch=64, lr=0.05,
+                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps)
+           for r in range(world)]
+    rows = nb * 64
+    Xall = swizzle_inputs(torch.stack([t.X[:rows] for t in trs]), 64)
+    xs = make_local_act_group(trs[0].layout, [0] * world, timeout_ms)
+    for t, x in zip(trs, xs):
+        t.runner.set_act_exchange(x, Xall, Xall[0].numel())
+        t.xchg = x
+        assert t.runner.exchange_mode() == 2
+    return trs, xs
+
+
+@pytest.mark.parametrize("world,graph_steps", [(2, 0), (3, 0), (3, 5), (2, 5)])
+def test_local_act_group_matches_reference(world, graph_steps):
+    nb, steps = 4, 10
+    trs, xs = _local_act_group(world, nb, graph_steps)
+    for chunk in (5, 5):
+        for t in trs:
+            t.train_steps(chunk)
+        for t in trs:
+            t.synchronize()  # raises if a peer timed out
+    Ps = [t.P.cpu() for t in trs]
+    for P in Ps[1:]:
+        assert torch.equal(P, Ps[0])  # every replica computes the same global-batch sums
+    want = _reference(world, steps, 0.05, nb)
+    err = (Ps[0] - want).abs().max().item()
+    assert err < 2e-5, err
+
+
+def test_act_exchange_missing_peer_times_out():
+    trs, xs = _local_act_group(2, 2, 0, timeout_ms=200.0)
+    P0 = trs[0].P.clone()
+    trs[0].train_steps(1)  # rank 1 never pushes
+    with pytest.raises(RuntimeError, match="timed out"):
+        trs[0].synchronize()
+    # a timed-out tile leaves its weights alone
+    assert torch.equal(trs[0].P, P0)
+    xs[0].reset()
+    torch.cuda.synchronize()
+    assert xs[0].error() == 0
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def _ipc_worker(rank, world, port, outdir, graph_steps):
+def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     ctx = DistContext.from_env(device="cuda", backend="gloo")
     tr = MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * 4, seed=300 + rank), batch=64, lr=0.05,
-                    ctx=ctx, seed=7, sync="xgmi", graph_steps=graph_steps, xchg_timeout_ms=5000.0)
-    assert tr.sync_active == "xgmi"
+                    ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0)
+    assert tr.sync_active == sync
     tr.train_steps(6)
     tr.synchronize()
     torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
     ctx.destroy()
 
 
-@pytest.mark.parametrize("graph_steps", [0, 3])
-def test_two_processes_ipc(graph_steps):
+@pytest.mark.parametrize("graph_steps,sync", [(0, "xgmi"), (3, "xgmi"), (0, "xact"), (3, "xact")])
+def test_two_processes_ipc(graph_steps, sync):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps), nprocs=world,
+        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync), nprocs=world,
                            start_method="spawn", join=True)
         Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
     assert torch.equal(Ps[0], Ps[1])
