@@ -18,8 +18,8 @@ from typing import Dict, Optional
 import grpc
 import torch
 
-from ..runtime.device import (DT_SIZE, STATUS_FAILED, STATUS_SUCCESS, TORCH_DTYPES, OutOfRange,
-                              _Device, make_device)
+from ..runtime.device import (DT_SIZE, STATUS_FAILED, STATUS_IN_PROGRESS, STATUS_SUCCESS,
+                              TORCH_DTYPES, OutOfRange, _Device, make_device)
 from .proto import pb
 from .stubs import GPUDeviceStub, connect, serve
 
@@ -34,6 +34,7 @@ class GPUDeviceServicer:
         self.name = name or f"device-{device.device_id}"
         self.comms: Dict[int, object] = {}      # commId -> native RcclComm
         self.comm_meta: Dict[int, dict] = {}    # commId -> {"rank", "nranks", "peers"}
+        self._aborted_comms: set = set()        # Abort is sticky for its communicator
         self._peer_stubs: Dict[str, GPUDeviceStub] = {}
         self._lock = threading.Lock()
         self.trainer = None
@@ -153,7 +154,7 @@ class GPUDeviceServicer:
                 nbytes[0] += len(c.data)
                 yield c.data
 
-        ok = self.dev.receive_chunks(sid, gen())
+        ok = self.dev.receive_chunks(sid, gen(), abort=lambda: self._sid_aborted(sid))
         self.counters["stream_bytes_in"] += nbytes[0]
         return pb.StreamSendResponse(success=ok)
 
@@ -237,6 +238,30 @@ class GPUDeviceServicer:
         self.comm_meta[cid] = meta
         return pb.CommSetupResponse(success=True, backend=backend)
 
+    @staticmethod
+    def _ring_sid(cid: int, seq: int, step: int, src: int) -> int:
+        """Deterministic stream id of a device-ring transfer (bit 62 tags ring streams)."""
+        return ((1 << 62) | ((cid & 0xFFFF) << 44) | ((seq & 0xFFFFF) << 24) | ((step & 0xFFF) << 12)
+                | (src & 0xFFF))
+
+    def _sid_aborted(self, sid: int) -> bool:
+        return bool((sid >> 62) & 1) and ((sid >> 44) & 0xFFFF) in {
+            c & 0xFFFF for c in self._aborted_comms}
+
+    def _wait_ring_stream(self, cid: int, sid: int, timeout: float = 120.0) -> int:
+        """wait_stream in short slices, giving up as soon as the communicator is
+        aborted (a peer failed): an Abort that lands between two ring steps must
+        not leave this device blocked on a receive no one will send."""
+        t_end = time.monotonic() + timeout
+        while True:
+            st = self.dev.wait_stream(sid, 0.05)
+            if st != STATUS_IN_PROGRESS:
+                return st
+            if cid in self._aborted_comms:
+                raise RuntimeError(f"communicator {cid} aborted")
+            if time.monotonic() > t_end:
+                return STATUS_FAILED
+
     def _rpc_ring(self, cid: int, addr: int, count: int, dtype: int, op: int, chunk: int) -> None:
         """Device-driven ring all-reduce over gRPC streams (CPU / no-RCCL path).
 
@@ -258,7 +283,7 @@ class GPUDeviceServicer:
         scratch = self.dev.scratch_addr
 
         def sid_of(step, src):
-            return (1 << 62) | ((cid & 0xFFFF) << 44) | ((seq & 0xFFFFF) << 24) | ((step & 0xFFF) << 12) | (src & 0xFFF)
+            return self._ring_sid(cid, seq, step, src)
 
         def push(sid, lo, ln):
             data = self.dev.read(addr + lo, ln, internal=True)
@@ -276,6 +301,8 @@ class GPUDeviceServicer:
             si, ri = (r - s_) % n, (r - s_ - 1) % n
             sl, rl = off[si + 1] - off[si], off[ri + 1] - off[ri]
             sid_in = sid_of(step, prv)
+            if cid in self._aborted_comms:
+                raise RuntimeError(f"communicator {cid} aborted")
             if rl:
                 self.dev.begin_receive(sid_in, scratch, rl, prv)
             err = []
@@ -284,7 +311,7 @@ class GPUDeviceServicer:
                 t = threading.Thread(target=_capture, args=(err, push, sid_of(step, r), off[si], sl))
                 t.start()
             if rl:
-                if self.dev.wait_stream(sid_in, 120.0) != STATUS_SUCCESS:
+                if self._wait_ring_stream(cid, sid_in) != STATUS_SUCCESS:
                     raise RuntimeError(f"ring step {step}: receive from rank {prv} failed")
                 self.dev.drop_stream(sid_in)
                 self.dev.reduce(addr + off[ri], scratch, rl, dtype, op)
@@ -298,6 +325,8 @@ class GPUDeviceServicer:
             si, ri = (r + 1 - s_) % n, (r - s_) % n
             sl, rl = off[si + 1] - off[si], off[ri + 1] - off[ri]
             sid_in = sid_of(step, prv)
+            if cid in self._aborted_comms:
+                raise RuntimeError(f"communicator {cid} aborted")
             if rl:
                 self.dev.begin_receive(sid_in, addr + off[ri], rl, prv)
             err = []
@@ -306,7 +335,7 @@ class GPUDeviceServicer:
                 t = threading.Thread(target=_capture, args=(err, push, sid_of(step, r), off[si], sl))
                 t.start()
             if rl:
-                if self.dev.wait_stream(sid_in, 120.0) != STATUS_SUCCESS:
+                if self._wait_ring_stream(cid, sid_in) != STATUS_SUCCESS:
                     raise RuntimeError(f"ring step {step}: receive from rank {prv} failed")
                 self.dev.drop_stream(sid_in)
             if t:
@@ -368,7 +397,10 @@ class GPUDeviceServicer:
         return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
 
     def Abort(self, request, context):
-        # unblock any device-driven ring step waiting on a peer that died
+        # unblock any device-driven ring step waiting on a peer that died, and
+        # keep failing that communicator's later ring steps (sticky)
+        if request.commId in self.comm_meta or request.commId in self.comms:
+            self._aborted_comms.add(request.commId)
         self.dev.fail_pending_streams()
         ids = [request.commId] if request.commId in self.comms else list(self.comms)
         for cid in ids:

@@ -19,6 +19,7 @@ freed after completion (Q11).
 from __future__ import annotations
 
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -131,17 +132,20 @@ class _Device:
         st = self.stream(sid)
         return STATUS_FAILED if st is None else st.status
 
-    def receive_chunks(self, sid: int, chunks, wait_s: float = 30.0) -> bool:
+    def receive_chunks(self, sid: int, chunks, wait_s: float = 30.0, abort=None) -> bool:
         """Write streamed chunks at the bound receive address.  A sender that
-        races ahead of BeginReceive waits (bounded) for the binding."""
+        races ahead of BeginReceive waits (bounded, and no longer than until
+        `abort()` turns true) for the binding."""
         st = self.stream(sid)
         if st is None:
             with self._lock:
                 st = self._streams.setdefault(sid, _Stream())
-        if not st.bound.wait(wait_s):
-            st.status = STATUS_FAILED
-            st.done.set()
-            return False
+        t_end = time.monotonic() + wait_s
+        while not st.bound.wait(0.05):
+            if time.monotonic() > t_end or (abort is not None and abort()):
+                st.status = STATUS_FAILED
+                st.done.set()
+                return False
         off = 0
         ok = True
         for data in chunks:
