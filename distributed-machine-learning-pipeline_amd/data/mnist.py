@@ -21,6 +21,18 @@ import torch
 IMAGE_MAGIC = 2051
 LABEL_MAGIC = 2049
 REFERENCE_DATA_DIR = "/root/reference/DSML/data"
+# The reference's own t10k files, shipped with the tests so the real-digit
+# checks also run where the reference tree is absent (e.g. the GPU box).
+FIXTURE_DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "tests", "fixtures", "mnist")
+
+
+def default_data_dir(split: str = "t10k") -> str:
+    """The reference's data directory when present, else the test fixtures."""
+    for d in (REFERENCE_DATA_DIR, FIXTURE_DATA_DIR):
+        if os.path.exists(os.path.join(d, f"{split}-images-idx3-ubyte.gz")):
+            return d
+    return REFERENCE_DATA_DIR
 
 
 def _open(path: str):
@@ -98,8 +110,9 @@ def synthetic_mnist(n: int, seed: int = 0, dim: int = 784, nclasses: int = 10,
     return Dataset(torch.from_numpy(X), torch.from_numpy(y), "synthetic")
 
 
-def load_mnist(data_dir: str = REFERENCE_DATA_DIR, split: str = "t10k",
+def load_mnist(data_dir: Optional[str] = None, split: str = "t10k",
                limit: Optional[int] = None) -> Dataset:
+    data_dir = data_dir or default_data_dir(split)
     img = os.path.join(data_dir, f"{split}-images-idx3-ubyte.gz")
     lab = os.path.join(data_dir, f"{split}-labels-idx1-ubyte.gz")
     X = load_idx_images(img)
@@ -111,7 +124,8 @@ def load_mnist(data_dir: str = REFERENCE_DATA_DIR, split: str = "t10k",
     return Dataset(torch.from_numpy(np.ascontiguousarray(X)), torch.from_numpy(y), f"mnist-{split}")
 
 
-def mnist_available(data_dir: str = REFERENCE_DATA_DIR, split: str = "t10k") -> bool:
+def mnist_available(data_dir: Optional[str] = None, split: str = "t10k") -> bool:
+    data_dir = data_dir or default_data_dir(split)
     return os.path.exists(os.path.join(data_dir, f"{split}-images-idx3-ubyte.gz"))
 
 
