@@ -204,6 +204,24 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
     bold = P[d.b_off[l] + nc];
   }
 
+  // Layer 0's B operand is this step's input rows of every rank, read from the
+  // local replicated shards: no peer involved, so those loads go out BEFORE the
+  // flag poll and land while it waits.
+  const int64_t frag = (int64_t)w * 256 + lane * 4;  // floats within a strip
+  const int64_t s0 = (int64_t)(2 * tk) * kStrip + frag, s1 = s0 + kStrip;
+  xa_f4 av[kMaxPeers], b0[kMaxPeers], b1[kMaxPeers];
+  if (l == 0) {
+    const int64_t bat = (int64_t)(step % (uint64_t)d.nbatches) * xa_strips(K) * kStrip;
+#pragma unroll
+    for (int r = 0; r < kMaxPeers; ++r) {
+      if (r < N) {
+        const float* xr = Xswz + (int64_t)r * xstride + bat;
+        b0[r] = *reinterpret_cast<const xa_f4*>(xr + s0);
+        b1[r] = s1v ? *reinterpret_cast<const xa_f4*>(xr + s1) : xa_f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+
   // wait for the strips this tile reads, from every rank (local flags):
   // threads [0,64) poll dZ_{l+1} strip tn, [64,128) H_l strip 2tk, [128,192) 2tk+1
   const int sdz = (int)(xa_seg_off(d, l + 1, 1) / kStrip) + tn;
@@ -229,24 +247,16 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
 
-  // Every rank's operands: one 16 B fragment load per matrix strip and lane.
+  // The exchanged operands: one 16 B fragment load per matrix strip and lane.
   const __amdgpu_buffer_rsrc_t rv = xa_rsrc(tab->buf[me] + par);
-  const int64_t frag = (int64_t)w * 256 + lane * 4;  // floats within a strip
   const int64_t dzo = (int64_t)sdz * kStrip + frag;
   const int64_t ao = l == 0 ? 0 : (int64_t)sh * kStrip - (int64_t)(2 * tk) * kStrip;
-  const int64_t bat = (int64_t)(step % (uint64_t)d.nbatches) * xa_strips(K) * kStrip;
-  const int64_t s0 = (int64_t)(2 * tk) * kStrip + frag, s1 = s0 + kStrip;
-  xa_f4 av[kMaxPeers], b0[kMaxPeers], b1[kMaxPeers];
 #pragma unroll
   for (int r = 0; r < kMaxPeers; ++r) {
     if (r < N) {
       const int64_t img = (int64_t)r * payload;
       av[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + dzo) * 4), 0, kSys);
-      if (l == 0) {
-        const float* xr = Xswz + (int64_t)r * xstride + bat;
-        b0[r] = *reinterpret_cast<const xa_f4*>(xr + s0);
-        b1[r] = s1v ? *reinterpret_cast<const xa_f4*>(xr + s1) : xa_f4{0.f, 0.f, 0.f, 0.f};
-      } else {
+      if (l != 0) {
         b0[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + ao + s0) * 4), 0, kSys);
         b1[r] = s1v ? __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + ao + s1) * 4), 0, kSys)
                     : xa_f4{0.f, 0.f, 0.f, 0.f};
