@@ -489,13 +489,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_exchange", [](PyMlpRunner& s, PeerExchange* x) { s.r->set_exchange(x); },
            py::arg("exchange").none(true), py::keep_alive<1, 2>())
       .def("set_act_exchange", [](PyMlpRunner& s, PeerExchange* x, torch::Tensor Xall,
-                                  int64_t xstride) {
+                                  int64_t xstride, int waves) {
         check_f32(Xall, "Xall");
         TORCH_CHECK(Xall.is_contiguous(), "Xall must be contiguous");
         TORCH_CHECK(x == nullptr || Xall.numel() >= (int64_t)x->nranks() * xstride,
                     "Xall holds fewer than nranks shards");
-        s.r->set_act_exchange(x, Xall.data_ptr<float>(), xstride);
-      }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"),
+        s.r->set_act_exchange(x, Xall.data_ptr<float>(), xstride, waves);
+      }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"), py::arg("waves") = 0,
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
       .def("exchange_mode", [](PyMlpRunner& s) { return s.r->exchange_mode(); })

@@ -119,9 +119,10 @@ hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const Xchg
 // (mlp_xact_supported).
 int mlp_xact_payload(const MlpDesc& d);
 bool mlp_xact_supported(const MlpDesc& d);
+// waves: 4 or 8 per tile block, 0 = 8 from 4 ranks on.
 hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
                               int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
-                              hipStream_t s);
+                              int waves, hipStream_t s);
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
                               const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
 

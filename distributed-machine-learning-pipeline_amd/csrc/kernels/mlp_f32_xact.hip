@@ -75,7 +75,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xa_rsrc(const void* p) {
                                            0x00020000);
 }
 
-constexpr int kXaWaves = 4;
+// Waves per block: 4, or 8 from N = 4 ranks on (the wave halves then split the
+// ranks, halving each wave's loads and MFMA chain; pushers split the ranks).
 constexpr int kStrip = 1024;  // floats of one 16-column strip of an image matrix
 
 __host__ __device__ inline int xa_strips(int D) { return (D + 15) >> 4; }
@@ -112,11 +113,13 @@ __device__ __forceinline__ void xa_strip_seg(const MlpDesc& d, int s, int& m, in
   m = d.nlayers; which = 1; t = 0;  // unreachable for s < nstrips
 }
 
-__global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
+template <int WV>
+__global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
     const float* __restrict__ Xswz, int64_t xstride, float* __restrict__ P,
     const float* __restrict__ ws, int64_t* __restrict__ ctr, MlpDesc d, float lr, XchgArgs xa,
     int nstrips) {
-  __shared__ float red[kXaWaves][9][64];  // pushers reuse it as the 64 x 17 transpose tile
+  constexpr int NH = WV / 4;  // rank phases: wave w serves ranks r with r % NH == w / 4
+  __shared__ float red[WV][9][64];  // pushers reuse it as the 64 x 17 transpose tile
   __shared__ int flag_ok;
   const uint64_t step = xa_ctr(ctr) - 1;  // K_A advanced A to step + 1
   const uint64_t want = step + 1;
@@ -136,7 +139,8 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
     const int D = d.dims[m];
     const float* src = ws + (which ? d.dz_off[m] : d.act_off[m]);
     float* tile = &red[0][0][0];
-    {  // 64 rows x 16 columns, one float4 per thread, zero-padded
+    const int t2 = tid & 255, half = tid >> 8;
+    if (half == 0) {  // 64 rows x 16 columns, one float4 per thread, zero-padded
       const int row = tid >> 2, c0 = 16 * t + 4 * (tid & 3);
       float v[4];
       if (row < B && (D & 3) == 0 && c0 + 3 < D) {
@@ -151,12 +155,12 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
       for (int k = 0; k < 4; ++k) tile[row * 17 + 4 * (tid & 3) + k] = v[k];
     }
     __syncthreads();
-    const int w = tid >> 6, ln = tid & 63, i = ln & 15, q = ln >> 4;
+    const int w = t2 >> 6, ln = t2 & 63, i = ln & 15, q = ln >> 4;
     xa_f4 f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) f[j] = tile[(4 * w + 16 * j + q) * 17 + i];
-    const int64_t off = (int64_t)me * payload + (int64_t)s * kStrip + tid * 4;  // floats
-    for (int dst = 0; dst < N; ++dst)
+    const int64_t off = (int64_t)me * payload + (int64_t)s * kStrip + t2 * 4;  // floats
+    for (int dst = half; dst < N; dst += NH)
       __builtin_amdgcn_raw_buffer_store_b128(f, xa_rsrc(tab->buf[dst] + par), (int)(off * 4), 0,
                                              kSys);
     // every storing wave drains its stores, then one lane per rank raises the flag
@@ -183,6 +187,7 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
   const int ntk = (K + 31) >> 5;
   const int tn = bid / ntk, tk = bid - tn * ntk;
   const int lane = tid & 63, w = tid >> 6, i = lane & 15, q = lane >> 4;
+  const int wq = w & 3, hr = w >> 2;  // fragment row group; rank phase
   const int n = tn * 16 + i;
   const int k0 = tk * 32 + i, k1 = k0 + 16;
   const bool nv = n < Nn, k0v = k0 < K, k1v = k1 < K;
@@ -207,14 +212,14 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
   // Layer 0's B operand is this step's input rows of every rank, read from the
   // local replicated shards: no peer involved, so those loads go out BEFORE the
   // flag poll and land while it waits.
-  const int64_t frag = (int64_t)w * 256 + lane * 4;  // floats within a strip
+  const int64_t frag = (int64_t)wq * 256 + lane * 4;  // floats within a strip
   const int64_t s0 = (int64_t)(2 * tk) * kStrip + frag, s1 = s0 + kStrip;
   xa_f4 av[kMaxPeers], b0[kMaxPeers], b1[kMaxPeers];
   if (l == 0) {
     const int64_t bat = (int64_t)(step % (uint64_t)d.nbatches) * xa_strips(K) * kStrip;
 #pragma unroll
     for (int r = 0; r < kMaxPeers; ++r) {
-      if (r < N) {
+      if (r < N && r % NH == hr) {
         const float* xr = Xswz + (int64_t)r * xstride + bat;
         b0[r] = *reinterpret_cast<const xa_f4*>(xr + s0);
         b1[r] = s1v ? *reinterpret_cast<const xa_f4*>(xr + s1) : xa_f4{0.f, 0.f, 0.f, 0.f};
@@ -253,7 +258,7 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
   const int64_t ao = l == 0 ? 0 : (int64_t)sh * kStrip - (int64_t)(2 * tk) * kStrip;
 #pragma unroll
   for (int r = 0; r < kMaxPeers; ++r) {
-    if (r < N) {
+    if (r < N && r % NH == hr) {
       const int64_t img = (int64_t)r * payload;
       av[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)((img + dzo) * 4), 0, kSys);
       if (l != 0) {
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
   float dbacc = 0.f;
 #pragma unroll
   for (int r = 0; r < kMaxPeers; ++r) {
-    if (r < N) {
+    if (r < N && r % NH == hr) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // zero padding rows/columns contribute 0
         dbacc += av[r][j];
@@ -290,7 +295,7 @@ __global__ __launch_bounds__(64 * kXaWaves) void mlp_f32_wgrad_xact_k(
 #pragma unroll
   for (int r = 0; r < 4; ++r) s0v[r] = s1v4[r] = 0.f;
 #pragma unroll
-  for (int v = 0; v < kXaWaves; ++v) {  // wave order: identical on every rank
+  for (int v = 0; v < WV; ++v) {  // wave order: identical on every rank
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       s0v[r] += red[v][r][lane];
@@ -323,17 +328,22 @@ bool mlp_xact_supported(const MlpDesc& d) {
 
 hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
                               int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
-                              hipStream_t s) {
+                              int waves, hipStream_t s) {
   const int payload = mlp_xact_payload(d);
   const int nstrips = payload / kStrip;
   if (ctr == nullptr || x.tab == nullptr || x.err == nullptr || x.nranks < 1 ||
       x.nranks > kMaxPeers || x.rank < 0 || x.rank >= x.nranks || !mlp_xact_supported(d) ||
       x.half < (int64_t)x.nranks * payload || (int64_t)2 * x.half * 4 > 0x7fffffffLL ||
-      xstride < (int64_t)d.nbatches * xa_strips(d.dims[0]) * kStrip)
+      xstride < (int64_t)d.nbatches * xa_strips(d.dims[0]) * kStrip ||
+      (waves != 0 && waves != 4 && waves != 8))
     return hipErrorInvalidValue;
   dim3 grid(nstrips + mlp_wgrad_tiles(d));
-  hipLaunchKernelGGL(mlp_f32_wgrad_xact_k, grid, dim3(64 * kXaWaves), 0, s, Xswz, xstride, P, ws,
-                     ctr, d, lr_over_n, x, nstrips);
+  if (waves == 8 || (waves == 0 && x.nranks >= 4))
+    hipLaunchKernelGGL(mlp_f32_wgrad_xact_k<8>, grid, dim3(512), 0, s, Xswz, xstride, P, ws, ctr,
+                       d, lr_over_n, x, nstrips);
+  else
+    hipLaunchKernelGGL(mlp_f32_wgrad_xact_k<4>, grid, dim3(256), 0, s, Xswz, xstride, P, ws, ctr,
+                       d, lr_over_n, x, nstrips);
   return hipGetLastError();
 }
 

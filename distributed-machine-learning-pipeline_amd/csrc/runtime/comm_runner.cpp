@@ -233,7 +233,7 @@ void MlpRunner::set_exchange(PeerExchange* x) {
   reset_graph();
 }
 
-void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride) {
+void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride, int waves) {
   if (x == nullptr) {
     set_exchange(nullptr);
     return;
@@ -252,8 +252,11 @@ void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xst
     throw std::invalid_argument("set_act_exchange: replicated input shards too small");
   xchg_ = x;
   xact_ = true;
+  if (waves != 0 && waves != 4 && waves != 8)
+    throw std::invalid_argument("set_act_exchange: waves must be 0 (auto), 4 or 8");
   xall_ = Xall;
   xstride_ = xstride;
+  xact_waves_ = waves;
   reset_graph();
 }
 
@@ -291,7 +294,8 @@ void MlpRunner::enqueue_step(hipStream_t s) {
                                     b_.stats, 1, 1.0f / (float)d_.batch, s));
     if (xact_)
       DSML_HIP_CHECK(mlp_f32_wgrad_xact(xall_, xstride_, b_.P, b_.ws, b_.ctr, d_,
-                                        lr_ / (float)xchg_->nranks(), xchg_->args(), s));
+                                        lr_ / (float)xchg_->nranks(), xchg_->args(),
+                                        xact_waves_, s));
     else
       DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
                                         lr_ / (float)xchg_->nranks(), xchg_->args(), s));

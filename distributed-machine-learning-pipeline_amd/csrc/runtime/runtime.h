@@ -264,7 +264,7 @@ class MlpRunner {
   // activations to every rank and computes the global-batch weight gradients;
   // Xall holds every rank's input shard in MFMA fragment order (rank r at
   // Xall + r * xstride).  Replaces set_exchange's mode while set.
-  void set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride);
+  void set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride, int waves = 0);
   bool exchange_active() const { return xchg_ != nullptr; }
   int exchange_mode() const { return xchg_ == nullptr ? 0 : (xact_ ? 2 : 1); }
   // Enqueue one full step on stream s (no host sync).
@@ -297,6 +297,7 @@ class MlpRunner {
   bool xact_ = false;
   const float* xall_ = nullptr;
   int64_t xstride_ = 0;
+  int xact_waves_ = 0;
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;

@@ -69,7 +69,8 @@ class MlpTrainer:
                  momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
                  ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
                  params: Optional[torch.Tensor] = None, external_comm=None,
-                 capture_collectives: bool = False, xchg_timeout_ms: float = 10000.0):
+                 capture_collectives: bool = False, xchg_timeout_ms: float = 10000.0,
+                 xact_waves: int = 0):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -101,6 +102,7 @@ class MlpTrainer:
         self.xchg = None
         self.capture_collectives = capture_collectives
         self.xchg_timeout_ms = xchg_timeout_ms
+        self.xact_waves = int(xact_waves)  # 0: 8-wave tile blocks from 4 ranks on, else 4
         self.sync_active = "none"
         self.sync_times: Dict[str, float] = {}
         self.Xall: Optional[torch.Tensor] = None
@@ -185,7 +187,8 @@ class MlpTrainer:
             self.runner.set_exchange(self.xchg)
         else:
             self.xchg = self._exchanges["xact"]
-            self.runner.set_act_exchange(self.xchg, self.Xall, self.Xall[0].numel())  # fragment order
+            self.runner.set_act_exchange(self.xchg, self.Xall, self.Xall[0].numel(),
+                                         self.xact_waves)
 
     def _setup_exchange(self, mode: str) -> str:
         """Collective: build `mode`'s buffers, check one step against a

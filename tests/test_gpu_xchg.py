@@ -74,7 +74,7 @@ def test_missing_peer_times_out_instead_of_hanging():
     assert xs[0].error() == 0
 
 
-def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0):
+def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0, waves=0):
     """Activation exchange between `world` replicas of one process."""
     trs = [MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * nb, seed=300 + r), batch=64, lr=0.05,
                       seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps)
@@ -83,16 +83,21 @@ def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0):
     Xall = swizzle_inputs(torch.stack([t.X[:rows] for t in trs]), 64)
     xs = make_local_act_group(trs[0].layout, [0] * world, timeout_ms)
     for t, x in zip(trs, xs):
-        t.runner.set_act_exchange(x, Xall, Xall[0].numel())
+        t.runner.set_act_exchange(x, Xall, Xall[0].numel(), waves)
         t.xchg = x
         assert t.runner.exchange_mode() == 2
     return trs, xs
 
 
-@pytest.mark.parametrize("world,graph_steps", [(2, 0), (3, 0), (3, 5), (2, 5)])
-def test_local_act_group_matches_reference(world, graph_steps):
+# in-process groups stay at <= 3 replicas: with 4 HIP hardware queues per
+# process, a 4th replica stream could queue behind a spinning peer
+# 8-wave tile blocks (the form used from 4 ranks on): two replicas are the most
+# whose spinning launches (2 x 243 blocks of 512 threads) fit one GPU together
+@pytest.mark.parametrize("world,graph_steps,waves", [(2, 0, 0), (3, 0, 0), (3, 5, 0), (2, 5, 0),
+                                                    (2, 0, 8), (2, 5, 8)])
+def test_local_act_group_matches_reference(world, graph_steps, waves):
     nb, steps = 4, 10
-    trs, xs = _local_act_group(world, nb, graph_steps)
+    trs, xs = _local_act_group(world, nb, graph_steps, waves=waves)
     for chunk in (5, 5):
         for t in trs:
             t.train_steps(chunk)
@@ -125,12 +130,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi"):
+def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=0):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     ctx = DistContext.from_env(device="cuda", backend="gloo")
     tr = MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * 4, seed=300 + rank), batch=64, lr=0.05,
-                    ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0)
+                    ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0,
+                    xact_waves=xact_waves)
     assert tr.sync_active == sync
     tr.train_steps(6)
     tr.synchronize()
@@ -138,14 +144,23 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi"):
     ctx.destroy()
 
 
-@pytest.mark.parametrize("graph_steps,sync", [(0, "xgmi"), (3, "xgmi"), (0, "xact"), (3, "xact")])
-def test_two_processes_ipc(graph_steps, sync):
-    world = 2
+@pytest.mark.parametrize("world,graph_steps,sync", [(2, 0, "xgmi"), (2, 3, "xgmi"), (2, 0, "xact"),
+                                                    (2, 3, "xact"), (3, 3, "xact"), (4, 3, "xgmi"),
+                                                    (8, 3, "xgmi")])
+def test_two_processes_ipc(world, graph_steps, sync):
+    """N processes sharing the GPU through IPC handles: the flag protocols at
+    the group sizes of a node.  Sharing one GPU, every process's spinning
+    weight-gradient launch must fit on the chip at once, so the activation
+    exchange runs 4-wave tile blocks and at most 3 processes (729 of 1,024
+    block slots); the 8-wave form is covered in-process above.  On a node each
+    GPU runs one launch."""
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync), nprocs=world,
+        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync,
+                                              4 if sync == "xact" else 0), nprocs=world,
                            start_method="spawn", join=True)
         Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
-    assert torch.equal(Ps[0], Ps[1])
+    for P in Ps[1:]:
+        assert torch.equal(Ps[0], P)
     err = (Ps[0] - _reference(world, 6, 0.05, 4)).abs().max().item()
     assert err < 2e-5, err
 
