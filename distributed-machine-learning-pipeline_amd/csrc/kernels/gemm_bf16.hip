@@ -160,8 +160,11 @@ __device__ __forceinline__ void epilogue_sgd_lds(f32x4 (&acc)[2][2], float* tile
   }
 }
 
-template <int U>
-__global__ __launch_bounds__(256) void gemm_bf16_nt_k(
+// SPLIT = false compiles the split-K paths (modes 0 and 2) out: the
+// weight-gradient GEMMs (K = batch, mode 1) then need few enough registers to
+// keep 6 waves per SIMD, and their fused SGD epilogue is a streaming RMW of W.
+template <int U, bool SPLIT = true>
+__global__ __launch_bounds__(256, SPLIT ? 1 : 6) void gemm_bf16_nt_k(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float* __restrict__ Cp, int M, int N, int K, int kchunk, GemmEpi epi, int mode,
     int* __restrict__ tile_ctr, int sgd_lds) {
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
     }
   }
 
-  if (mode == 0) {
+  if (SPLIT && mode == 0) {
     float* out = Cp + (int64_t)blockIdx.z * M * N;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_nt_k(
       }
     return;
   }
-  if (mode == 2) {
+  if (SPLIT && mode == 2) {
     // ---- split-K, last arriver finishes the tile -------------------------
     // Slabs in the MFMA-native layout (16 floats per thread per split, 16 B
     // runs): written WRITE-THROUGH (sc1, raw_buffer_store_b128 aux 16) so no
@@ -679,6 +682,9 @@ hipError_t gemm_bf16_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64
   if (kchunk >= 256)
     hipLaunchKernelGGL(gemm_bf16_nt_k<8>, grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N, K,
                        kchunk, e, mode, tile_ctr, sgd_lds);
+  else if (kchunk <= 64 && mode == 1)  // weight-gradient GEMMs (K = batch): more blocks per CU
+    hipLaunchKernelGGL((gemm_bf16_nt_k<2, false>), grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N,
+                       K, kchunk, e, mode, tile_ctr, sgd_lds);
   else
     hipLaunchKernelGGL(gemm_bf16_nt_k<4>, grid, dim3(256), 0, s, A, lda, B, ldb, Cp, M, N, K,
                        kchunk, e, mode, tile_ctr, sgd_lds);
