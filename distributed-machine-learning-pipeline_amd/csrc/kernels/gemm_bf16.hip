@@ -717,44 +717,60 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 // classes, then softmax-CE as softmax_xent_k — one 256-thread block per row.
 // Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
 constexpr int kHeadMaxC = 16;
+constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
 __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
     float inv_batch, float* __restrict__ logits, int64_t ldl, uint16_t* __restrict__ dz,
     int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats) {
-  __shared__ float part[4][kHeadMaxC];
+  __shared__ float part[kHeadMaxC][257];  // per-thread partial dot products, per class
+  __shared__ float zsum[kHeadMaxC];
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* hr = H + (int64_t)m * ldh;
+  // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
+  uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][kHeadMaxC];
+#pragma unroll
+  for (int j = 0; j < kHeadMaxK8; ++j) {
+    const int k = (t + 256 * j) * 8;
+    const bool kv = k < K;
+    hv[j] = kv ? *reinterpret_cast<const uint4*>(hr + k) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int c = 0; c < kHeadMaxC; ++c)
+      wv[j][c] = (kv && c < C) ? *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k)
+                               : make_uint4(0u, 0u, 0u, 0u);
+  }
   float acc[kHeadMaxC];
 #pragma unroll
   for (int c = 0; c < kHeadMaxC; ++c) acc[c] = 0.f;
-  for (int k = t * 8; k < K; k += 256 * 8) {
-    const uint4 hv = *reinterpret_cast<const uint4*>(hr + k);
-    const float h[8] = {bf16lo(hv.x), bf16hi(hv.x), bf16lo(hv.y), bf16hi(hv.y),
-                        bf16lo(hv.z), bf16hi(hv.z), bf16lo(hv.w), bf16hi(hv.w)};
+#pragma unroll
+  for (int j = 0; j < kHeadMaxK8; ++j) {
+    const float h[8] = {bf16lo(hv[j].x), bf16hi(hv[j].x), bf16lo(hv[j].y), bf16hi(hv[j].y),
+                        bf16lo(hv[j].z), bf16hi(hv[j].z), bf16lo(hv[j].w), bf16hi(hv[j].w)};
 #pragma unroll
     for (int c = 0; c < kHeadMaxC; ++c) {
-      if (c < C) {
-        const uint4 wv = *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k);
-        acc[c] += h[0] * bf16lo(wv.x) + h[1] * bf16hi(wv.x) + h[2] * bf16lo(wv.y) +
-                  h[3] * bf16hi(wv.y) + h[4] * bf16lo(wv.z) + h[5] * bf16hi(wv.z) +
-                  h[6] * bf16lo(wv.w) + h[7] * bf16hi(wv.w);
-      }
+      const uint4 x = wv[j][c];
+      acc[c] += h[0] * bf16lo(x.x) + h[1] * bf16hi(x.x) + h[2] * bf16lo(x.y) + h[3] * bf16hi(x.y) +
+                h[4] * bf16lo(x.z) + h[5] * bf16hi(x.z) + h[6] * bf16lo(x.w) + h[7] * bf16hi(x.w);
     }
   }
+  // block reduction per class: LDS transpose, then one 16-lane DPP row per class
 #pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c) {
-    float v = acc[c];
+  for (int c = 0; c < kHeadMaxC; ++c) part[c][t] = acc[c];
+  __syncthreads();
+  {
+    const int c = t >> 4, sg = t & 15;  // class c = row of 16 lanes; 16 partials per lane
+    float v = 0.f;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0 && c < C) part[w][c] = v;
+    for (int u = 0; u < 16; ++u) v += part[c][16 * sg + u];
+    v = row16_sum(v);
+    if (sg == 0) zsum[c] = v;
   }
   __syncthreads();
   if (w != 0) return;
   const int c = lane;
   const bool cv = c < C;
   float z = -3.402823466e38f;
-  if (cv) z = part[0][c] + part[1][c] + part[2][c] + part[3][c] + (bias ? bias[c] : 0.f);
+  if (cv) z = zsum[c] + (bias ? bias[c] : 0.f);
   if (cv && logits) logits[(int64_t)m * ldl + c] = z;
   const int y = labels[m];
   float mx = z;
@@ -787,7 +803,8 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              const float* bias, int B, int K, int C, const int32_t* labels,
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s) {
-  if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || (ldh & 7) || (ldw & 7) ||
+  if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
+      (ldw & 7) ||
       (((uintptr_t)H | (uintptr_t)W) & 15))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_softmax_xent_k, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,

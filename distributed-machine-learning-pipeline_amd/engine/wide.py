@@ -121,7 +121,7 @@ class WideMlpTrainer:
         C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
         r0 = (self.steps_done % self.nbatches) * Bt
         C.cast_transpose(self.X[r0:r0 + Bt], Bt, d[0], self.H[0], self.HT[0])
-        fused_head = d[L] <= 16 and self.gemm == "rows64"
+        fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096 and self.gemm == "rows64"
         for l in range(L - 1 if fused_head else L):
             _, b = self.views[l]
             if l < L - 1:
