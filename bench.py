@@ -84,7 +84,8 @@ def main() -> int:
                     help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
-                         "two ranks on one GPU); use with --sync xact, xgmi or torch")
+                         "two ranks on one GPU); --sync auto then weighs the exchanges against "
+                         "a torch.distributed all-reduce instead of RCCL")
     a = ap.parse_args()
 
     import torch
@@ -105,7 +106,8 @@ def main() -> int:
     spec = MlpSpec.parse(a.model)
     ds = synthetic_mnist(a.samples_per_rank, seed=1000 + ctx.rank, dim=spec.dims[0])
     tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,
-                    graph_steps=a.graph_steps)
+                    graph_steps=a.graph_steps,
+                    auto_fallback="torch" if a.rehearse_one_gpu else "rccl")
     tr.train_steps(a.warmup)
     tr.synchronize()
     ctx.barrier()

@@ -45,13 +45,13 @@ class StepStats:
         return 100.0 * self.correct / max(self.count, 1.0)
 
 
-def _xgmi_eligible(ctx: DistContext) -> bool:
+def _xgmi_eligible(ctx: DistContext, need_nccl: bool = True) -> bool:
     """All ranks on one node, one GPU each, <= 8: the fused exchange applies."""
     import os
 
     local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size))
-    return ctx.device.type == "cuda" and ctx.backend == "nccl" and 1 < ctx.world_size <= 8 \
-        and local == ctx.world_size
+    return ctx.device.type == "cuda" and (ctx.backend == "nccl" or not need_nccl) \
+        and 1 < ctx.world_size <= 8 and local == ctx.world_size
 
 
 def _pad_cols(X: torch.Tensor, mult: int = 4) -> torch.Tensor:
@@ -70,7 +70,7 @@ class MlpTrainer:
                  ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
                  params: Optional[torch.Tensor] = None, external_comm=None,
                  capture_collectives: bool = False, xchg_timeout_ms: float = 10000.0,
-                 xact_waves: int = 0):
+                 xact_waves: int = 0, auto_fallback: str = "rccl"):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -103,6 +103,12 @@ class MlpTrainer:
         self.capture_collectives = capture_collectives
         self.xchg_timeout_ms = xchg_timeout_ms
         self.xact_waves = int(xact_waves)  # 0: 8-wave tile blocks from 4 ranks on, else 4
+        # sync='auto' without RCCL (one-GPU rehearsals, where RCCL refuses two
+        # ranks on a device): the non-exchange candidate is a torch.distributed
+        # all-reduce between fwd/bwd and the update
+        if auto_fallback not in ("rccl", "torch"):
+            raise ValueError("auto_fallback must be 'rccl' or 'torch'")
+        self.auto_fallback = auto_fallback
         self.sync_active = "none"
         self.sync_times: Dict[str, float] = {}
         self.Xall: Optional[torch.Tensor] = None
@@ -141,13 +147,16 @@ class MlpTrainer:
         if self.sync in EXCHANGE_MODES and not plain:
             raise ValueError(f"sync='{self.sync}' implements plain SGD; use rccl for momentum/"
                              "weight decay")
-        if self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
+        torch_fallback = self.sync == "auto" and self.auto_fallback == "torch"
+        if torch_fallback:
+            self.sync_active = "torch"
+        elif self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
-        if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain
-                                           and _xgmi_eligible(self.ctx)):
+        if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain and _xgmi_eligible(
+                self.ctx, need_nccl=not torch_fallback)):
             self._init_exchanges()
 
     # ------------------------------------------------------ xGMI exchanges --
@@ -240,11 +249,12 @@ class MlpTrainer:
         choice = ok[0] if ok else None
         if self.sync == "auto" and ok:
             times = {}
+            fallback = self.sync_active  # rccl / ring, or torch (rehearsals)
             for m in ok + [None]:
                 self._activate(m)
-                times[m or "rccl"] = self._time_steps(20)
+                times[m or fallback] = self._time_steps(20)
             choice = min(times, key=times.get)
-            choice = None if choice == "rccl" else choice
+            choice = None if choice == fallback else choice
             log.info("sync auto: %s", ", ".join(f"{k} {1e6 * v:.1f} us/step"
                                                 for k, v in times.items()))
             self.sync_times = {k: round(1e6 * v, 2) for k, v in times.items()}
@@ -270,6 +280,10 @@ class MlpTrainer:
             def run():
                 self.runner.replay(reps)
             self.runner.replay(1)  # warm-up
+        elif self.comm is None and self.sync_active == "torch":
+            def run():
+                self._hip_step_torch_sync(n)
+            self._hip_step_torch_sync(2)
         else:
             def run():
                 self.runner.step(n)
