@@ -136,8 +136,12 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
     ctx = DistContext.from_env(device="cuda", backend="gloo")
     tr = MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * 4, seed=300 + rank), batch=64, lr=0.05,
                     ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0,
-                    xact_waves=xact_waves)
-    assert tr.sync_active == sync
+                    xact_waves=xact_waves, auto_fallback="torch")
+    if sync == "auto":  # every candidate self-tested and timed; any may win on a shared GPU
+        assert tr.sync_active in ("xact", "xgmi", "torch"), tr.sync_active
+        assert set(tr.sync_times) == {"xact", "xgmi", "torch"}, tr.sync_times
+    else:
+        assert tr.sync_active == sync
     tr.train_steps(6)
     tr.synchronize()
     torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
@@ -145,18 +149,19 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
 
 
 @pytest.mark.parametrize("world,graph_steps,sync", [(2, 0, "xgmi"), (2, 3, "xgmi"), (2, 0, "xact"),
-                                                    (2, 3, "xact"), (3, 3, "xact"), (4, 3, "xgmi"),
-                                                    (8, 3, "xgmi")])
+                                                    (2, 3, "xact"), (3, 3, "xact"), (3, 3, "xgmi"),
+                                                    (2, 3, "auto")])
 def test_two_processes_ipc(world, graph_steps, sync):
-    """N processes sharing the GPU through IPC handles: the flag protocols at
-    the group sizes of a node.  Sharing one GPU, every process's spinning
-    weight-gradient launch must fit on the chip at once, so the activation
-    exchange runs 4-wave tile blocks and at most 3 processes (729 of 1,024
-    block slots); the 8-wave form is covered in-process above.  On a node each
-    GPU runs one launch."""
+    """N processes sharing the GPU through IPC handles.  Sharing one GPU, every
+    process's spinning weight-gradient launch must be resident at once: the
+    activation exchange runs 4-wave tile blocks (3 x 243 of 1,024 block slots;
+    the 8-wave form is covered in-process above), and groups stay at <= 3
+    processes — with 4 or more, the hardware scheduler can leave a process's
+    queue unmapped while its peers spin (seen as a timed-out self-test).  On a
+    node each GPU runs one process and one launch."""
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync,
-                                              4 if sync == "xact" else 0), nprocs=world,
+                                              4 if sync in ("xact", "auto") else 0), nprocs=world,
                            start_method="spawn", join=True)
         Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
     for P in Ps[1:]:
