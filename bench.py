@@ -30,7 +30,8 @@ BASELINE_SAMPLES_PER_S = 819.0  # 599,680 samples / 732 s
 def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200) -> dict:
     """Device all-reduce latency of a `nbytes` fp32 buffer across the job's GPUs
     (the BASELINE's second metric, ring all-reduce at 1 MiB): RCCL's
-    ncclAllReduce and the one-shot xGMI peer all-reduce.  Max over ranks."""
+    ncclAllReduce and the one-shot and two-shot xGMI peer all-reduces.  Max
+    over ranks."""
     import torch
 
     from hipdsml.parallel.xchg import ExchangeUnavailable, XgmiAllReduce
@@ -52,13 +53,14 @@ def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200) -> 
 
     if comm is not None:
         out["rccl"] = timed(lambda: comm.allreduce_(t, 0))
-    try:
-        ar = XgmiAllReduce(ctx, t.numel())
-    except ExchangeUnavailable as e:
-        out["xgmi_error"] = str(e)[:200]
-    else:
-        out["xgmi"] = timed(lambda: ar(t))
-        ar.check()
+    for name, algo in (("xgmi", "oneshot"), ("xgmi_2shot", "twoshot")):
+        try:
+            ar = XgmiAllReduce(ctx, t.numel(), algo=algo)
+        except ExchangeUnavailable as e:
+            out[f"{name}_error"] = str(e)[:200]
+        else:
+            out[name] = timed(lambda: ar(t))
+            ar.check()
     return out
 
 

@@ -559,18 +559,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return x.error(cur_stream());
       })
       .def("set_timeout_ms", &PeerExchange::set_timeout_ms)
-      .def("allreduce_", [](PeerExchange& x, torch::Tensor t) {
+      .def("allreduce_", [](PeerExchange& x, torch::Tensor t, int algo) {
         check_f32(t, "tensor");
-        x.allreduce(t.data_ptr<float>(), t.data_ptr<float>(), t.numel(), cur_stream());
+        x.allreduce(t.data_ptr<float>(), t.data_ptr<float>(), t.numel(), cur_stream(), algo);
         return t;
-      })
-      .def("allreduce", [](PeerExchange& x, torch::Tensor in, torch::Tensor out) {
+      }, py::arg("t"), py::arg("algo") = 0)
+      .def("allreduce", [](PeerExchange& x, torch::Tensor in, torch::Tensor out, int algo) {
         check_f32(in, "in");
         check_f32(out, "out");
         TORCH_CHECK(in.numel() == out.numel(), "in/out size mismatch");
-        x.allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cur_stream());
+        x.allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cur_stream(), algo);
         return out;
-      })
+      }, py::arg("in"), py::arg("out"), py::arg("algo") = 0)
       .def_property_readonly("nranks", &PeerExchange::nranks)
       .def_property_readonly("rank", &PeerExchange::rank)
       .def_property_readonly("ntiles", &PeerExchange::ntiles)

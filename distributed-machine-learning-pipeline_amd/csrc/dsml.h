@@ -108,6 +108,10 @@ int mlp_wgrad_tiles(const MlpDesc& d);
 int xchg_allreduce_blocks(int64_t n, int max_blocks, int* unroll);
 hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
                               int max_blocks, uint64_t seq, hipStream_t s);
+// Two-shot (reduce-scatter + all-gather) over the same buffers: 2n/N bytes per
+// link.  Needs x.half >= n + ceil(n / N) and uses max_blocks / 2 flags per phase.
+hipError_t xchg_allreduce2_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
+                               int max_blocks, uint64_t seq, hipStream_t s);
 // Activation exchange (kernels/mlp_f32_xact.hip): K_C variant that pushes this
 // replica's activations and activation gradients (H_l, dZ_l, in MFMA fragment
 // order: mlp_xact_payload floats) to every rank and computes the global-batch

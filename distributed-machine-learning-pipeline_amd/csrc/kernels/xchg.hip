@@ -113,6 +113,112 @@ __global__ __launch_bounds__(kXThreads) void xchg_allreduce_k(const float* __res
   }
 }
 
+
+// Two-shot variant: reduce-scatter then all-gather over the same peer memory.
+// Rank r owns chunk r (ceil(n / N) floats, float4-aligned).  Phase 1: every
+// rank publishes its whole input (local stores) and raises flag1; the owner of
+// each chunk reads that chunk from every peer, sums in rank order, publishes
+// the reduced chunk and raises flag2.  Phase 2: every rank reads each peer's
+// reduced chunk.  Per link 2 n / N bytes instead of the one-shot's n — the
+// form for larger messages and wider groups (1 MiB at N = 8: 256 KB per link
+// instead of 1 MiB).  Blocks own the same float4 slice of every chunk, so all
+// hand-offs stay inside a block (no cross-block dependency on a GPU).
+// Exchange buffer (per parity half): [0, n) input copy, [n, n + cs) reduced chunk;
+// flags: [0, fo) phase 1, [fo, 2 fo) phase 2.
+template <int U>
+__global__ __launch_bounds__(kXThreads) void xchg_allreduce2_k(const float* __restrict__ in,
+                                                               float* __restrict__ out, int64_t n,
+                                                               int64_t cs, XchgArgs xa, uint64_t seq,
+                                                               int fo) {
+  const int N = xa.nranks, me = xa.rank;
+  const int64_t poff = (int64_t)(seq & 1) * xa.half;
+  const XchgTab* __restrict__ tab = xa.tab;
+  float* mine = tab->buf[me] + poff;
+  const int64_t slice = (int64_t)blockIdx.x * kXThreads * 4 * U;  // float offset within a chunk
+  auto chunk_len = [&](int c) -> int64_t {
+    const int64_t b = (int64_t)c * cs;
+    return b >= n ? 0 : (n - b < cs ? n - b : cs);
+  };
+  auto wait_flags = [&](int base) {
+    if (threadIdx.x < N && threadIdx.x != me) {
+      const uint64_t* f = tab->flags[threadIdx.x] + base + blockIdx.x;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (ld_flag(f) < seq) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+  };
+  // ---- phase 1a: publish this block's slice of every chunk ----
+  float4 own[U];
+  for (int c = 0; c < N; ++c) {
+    const int64_t len = chunk_len(c), cb = (int64_t)c * cs;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = slice + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+      if (i < len) {
+        const float4 v = *reinterpret_cast<const float4*>(in + cb + i);
+        st_sys4(mine + cb + i, v);
+        if (c == me) own[u] = v;
+      }
+    }
+  }
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) st_flag(tab->flags[me] + blockIdx.x, seq);
+  wait_flags(0);
+  // ---- phase 1b: reduce my chunk's slice in rank order, publish it ----
+  const int64_t mlen = chunk_len(me), mcb = (int64_t)me * cs;
+  float4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int p = 0; p < N; ++p) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = slice + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < mlen) v[u] = p == me ? own[u] : ld_sys4(tab->buf[p] + poff + mcb + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = slice + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+    if (i < mlen) {
+      st_sys4(mine + n + i, acc[u]);
+      *reinterpret_cast<float4*>(out + mcb + i) = acc[u];
+    }
+  }
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) st_flag(tab->flags[me] + fo + blockIdx.x, seq);
+  wait_flags(fo);
+  // ---- phase 2: gather every peer's reduced slice ----
+  for (int p = 0; p < N; ++p) {
+    if (p == me) continue;
+    const int64_t len = chunk_len(p), cb = (int64_t)p * cs;
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = slice + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+      if (i < len) v[u] = ld_sys4(tab->buf[p] + poff + n + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = slice + ((int64_t)u * kXThreads + threadIdx.x) * 4;
+      if (i < len) *reinterpret_cast<float4*>(out + cb + i) = v[u];
+    }
+  }
+}
+
 }  // namespace
 
 int xchg_allreduce_blocks(int64_t n, int max_blocks, int* unroll) {
@@ -140,6 +246,25 @@ hipError_t xchg_allreduce_f32(const float* in, float* out, int64_t n, const Xchg
     case 2: hipLaunchKernelGGL(xchg_allreduce_k<2>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
     case 4: hipLaunchKernelGGL(xchg_allreduce_k<4>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
     default: hipLaunchKernelGGL(xchg_allreduce_k<8>, dim3(g), dim3(kXThreads), 0, s, in, out, n, x, seq); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t xchg_allreduce2_f32(const float* in, float* out, int64_t n, const XchgArgs& x,
+                               int max_blocks, uint64_t seq, hipStream_t s) {
+  // flags: max_blocks / 2 per phase (the exchange holds max_blocks flags)
+  const int fo = max_blocks / 2;
+  if (n % 4 || x.tab == nullptr || seq == 0 || x.nranks < 1 || fo < 1) return hipErrorInvalidValue;
+  const int64_t cs = ((n + x.nranks - 1) / x.nranks + 3) / 4 * 4;
+  if (n + cs > x.half) return hipErrorInvalidValue;
+  int u = 0;
+  const int g = xchg_allreduce_blocks(cs, fo, &u);
+  if (g < 0) return hipErrorInvalidValue;
+  switch (u) {
+    case 1: hipLaunchKernelGGL(xchg_allreduce2_k<1>, dim3(g), dim3(kXThreads), 0, s, in, out, n, cs, x, seq, fo); break;
+    case 2: hipLaunchKernelGGL(xchg_allreduce2_k<2>, dim3(g), dim3(kXThreads), 0, s, in, out, n, cs, x, seq, fo); break;
+    case 4: hipLaunchKernelGGL(xchg_allreduce2_k<4>, dim3(g), dim3(kXThreads), 0, s, in, out, n, cs, x, seq, fo); break;
+    default: hipLaunchKernelGGL(xchg_allreduce2_k<8>, dim3(g), dim3(kXThreads), 0, s, in, out, n, cs, x, seq, fo); break;
   }
   return hipGetLastError();
 }

@@ -119,13 +119,18 @@ void PeerExchange::connect_local(int rank, const std::vector<PeerExchange*>& pee
   publish_table(t, rank, n);
 }
 
-void PeerExchange::allreduce(const float* in, float* out, int64_t n, hipStream_t s) {
+void PeerExchange::allreduce(const float* in, float* out, int64_t n, hipStream_t s, int algo) {
   if (!connected()) throw std::runtime_error("PeerExchange::allreduce: not connected");
-  if (n % 4 || n > half_)
-    throw std::invalid_argument("PeerExchange::allreduce: n must be a multiple of 4 and <= " +
-                                std::to_string(half_));
+  const int64_t cs = ((n + args_.nranks - 1) / args_.nranks + 3) / 4 * 4;
+  const int64_t need = algo == 1 ? n + cs : n;
+  if (n % 4 || need > half_)
+    throw std::invalid_argument("PeerExchange::allreduce: n must be a multiple of 4 and fit the "
+                                "exchange (" + std::to_string(half_) + " floats)");
   DSML_HIP_CHECK(hipSetDevice(device_));
-  DSML_HIP_CHECK(xchg_allreduce_f32(in, out, n, args_, ntiles_, ++seq_, s));
+  if (algo == 1)
+    DSML_HIP_CHECK(xchg_allreduce2_f32(in, out, n, args_, ntiles_, ++seq_, s));
+  else
+    DSML_HIP_CHECK(xchg_allreduce_f32(in, out, n, args_, ntiles_, ++seq_, s));
 }
 
 void PeerExchange::reset(hipStream_t s) {

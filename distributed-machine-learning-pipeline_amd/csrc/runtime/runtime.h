@@ -208,7 +208,9 @@ class PeerExchange {
   void set_timeout_ms(double ms);
   // One-shot all-reduce (sum) of n fp32 through the exchange (not graph-safe:
   // the call number is a kernel argument).  out may alias in.
-  void allreduce(const float* in, float* out, int64_t n, hipStream_t s);
+  // algo 0: one-shot (every rank reads every peer's whole buffer); 1: two-shot
+  // (reduce-scatter + all-gather, 2n/N bytes per link).
+  void allreduce(const float* in, float* out, int64_t n, hipStream_t s, int algo = 0);
   bool connected() const { return args_.tab != nullptr; }
   const XchgArgs& args() const { return args_; }
   int nranks() const { return args_.nranks; }

@@ -142,20 +142,29 @@ def make_local_group(layout: Optional[MlpLayout], devices: List[int], timeout_ms
 
 
 class XgmiAllReduce:
-    """One-shot fp32 sum all-reduce over xGMI peer memory for buffers of up to
-    `max_floats` (kernels/xchg.hip).  Collective construction; calls must be
-    issued by every rank in the same order (like any collective)."""
+    """fp32 sum all-reduce over xGMI peer memory for buffers of up to
+    `max_floats` (kernels/xchg.hip): ``algo="oneshot"`` (every rank reads every
+    peer's whole buffer: one synchronisation, n bytes per link) or
+    ``"twoshot"`` (reduce-scatter + all-gather: two synchronisations, 2n/N
+    bytes per link).  Collective construction; calls must be issued by every
+    rank in the same order (like any collective)."""
+
+    ALGOS = {"oneshot": 0, "twoshot": 1}
 
     def __init__(self, ctx: DistContext, max_floats: int, max_blocks: int = 512,
-                 timeout_ms: float = 10000.0):
+                 timeout_ms: float = 10000.0, algo: str = "oneshot"):
+        if algo not in self.ALGOS:
+            raise ValueError(f"algo must be one of {sorted(self.ALGOS)}")
         self.ctx = ctx
+        self.algo = algo
         self.max_floats = (max_floats + 3) // 4 * 4
-        self.x = make_exchange(ctx, self.max_floats, max_blocks, timeout_ms)
+        # the two-shot form also holds the reduced chunk: n + ceil(n / N) per parity half
+        self.x = make_exchange(ctx, 2 * self.max_floats, max_blocks, timeout_ms)
 
     def __call__(self, t: torch.Tensor) -> torch.Tensor:
         n = t.numel()
         if n % 4 == 0 and n <= self.max_floats and t.is_contiguous():
-            return self.x.allreduce_(t)
+            return self.x.allreduce_(t, self.ALGOS[self.algo])
         raise ValueError(f"xGMI all-reduce takes contiguous fp32 of <= {self.max_floats} "
                          "elements, a multiple of 4")
 

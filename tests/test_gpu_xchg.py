@@ -170,12 +170,25 @@ def test_two_processes_ipc(world, graph_steps, sync):
     assert err < 2e-5, err
 
 
-@pytest.mark.parametrize("world,n", [(2, 262144), (3, 1000), (2, 4), (3, 1 << 20)])
-def test_standalone_allreduce_in_process(world, n):
+_STREAMS = []
+
+
+def _replica_streams(n):
+    """One stream per in-process replica, created once: HIP maps streams onto
+    4 hardware queues, and two replicas whose streams landed on the same queue
+    would serialise (the later kernel queued behind its spinning peer)."""
+    while len(_STREAMS) < n:
+        _STREAMS.append(torch.cuda.Stream(DEV))
+    return _STREAMS[:n]
+
+
+@pytest.mark.parametrize("algo", [0, 1])  # one-shot, two-shot
+@pytest.mark.parametrize("world,n", [(2, 262144), (3, 1000), (2, 4), (3, 1 << 20), (3, 12)])
+def test_standalone_allreduce_in_process(world, n, algo):
     n = n // 4 * 4
-    xs = make_local_group(None, [0] * world, 5000.0, half_floats=1 << 20, ntiles=256)
+    xs = make_local_group(None, [0] * world, 5000.0, half_floats=2 << 20, ntiles=256)
     g = torch.Generator().manual_seed(n)
-    streams = [torch.cuda.Stream(DEV) for _ in range(world)]
+    streams = _replica_streams(world)
     for it in range(3):  # parity alternates; in-place on the last call
         host = [torch.randn(n, generator=g) for _ in range(world)]
         ins = [h.to(DEV) for h in host]
@@ -184,27 +197,30 @@ def test_standalone_allreduce_in_process(world, n):
         for r in range(world):
             with torch.cuda.stream(streams[r]):
                 if it == 2:
-                    xs[r].allreduce_(ins[r])
+                    xs[r].allreduce_(ins[r], algo)
                 else:
-                    xs[r].allreduce(ins[r], outs[r])
+                    xs[r].allreduce(ins[r], outs[r], algo)
         torch.cuda.synchronize()
+        assert [x.error() for x in xs] == [0] * world, f"iteration {it}: a peer timed out"
         want = host[0].clone()
         for h in host[1:]:
             want = want + h  # the kernel's rank-ordered sum
         for r in range(world):
             got = (ins[r] if it == 2 else outs[r]).cpu()
-            assert torch.equal(got, want)
+            bad = (got != want).nonzero().flatten()
+            assert bad.numel() == 0, (it, r, bad.numel(), bad[:4].tolist(), got[bad[:4]].tolist(),
+                                      want[bad[:4]].tolist())
         for x in xs:
             assert x.error() == 0
 
 
-def _ar_worker(rank, world, port, outdir):
+def _ar_worker(rank, world, port, outdir, algo="oneshot"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from hipdsml.parallel.xchg import XgmiAllReduce
 
     ctx = DistContext.from_env(device="cuda", backend="gloo")
-    ar = XgmiAllReduce(ctx, 1 << 18)
+    ar = XgmiAllReduce(ctx, 1 << 18, algo=algo)
     res = []
     for it in range(4):
         t = torch.full((1 << 18,), float(rank + 1 + it), device=ctx.device)
@@ -216,10 +232,11 @@ def _ar_worker(rank, world, port, outdir):
     ctx.destroy()
 
 
-def test_standalone_allreduce_ipc():
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot"])
+def test_standalone_allreduce_ipc(algo):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ar_worker, args=(world, _free_port(), d), nprocs=world,
+        mp.start_processes(_ar_worker, args=(world, _free_port(), d, algo), nprocs=world,
                            start_method="spawn", join=True)
         for r in range(world):
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["res"]
