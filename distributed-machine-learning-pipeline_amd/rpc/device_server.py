@@ -550,6 +550,8 @@ class GPUDeviceServicer:
         d = dict(self.counters)
         d.update({"device_id": self.dev.device_id, "backend": self.dev.backend,
                   "comms": sorted(self.comms), "steps_done": getattr(self.trainer, "steps_done", 0)})
+        d["rpc_latency"] = {m: h.summary() for m, h in getattr(self, "rpc_latency", {}).items()
+                            if h.n}
         return pb.GetStatsResponse(json=json.dumps(d))
 
 

@@ -2,11 +2,13 @@
 generated at import time from ``rpc/proto.py`` (no codegen step)."""
 from __future__ import annotations
 
+import time
 from concurrent import futures
 from typing import Optional, Tuple
 
 import grpc
 
+from ..utils.metrics import Histogram
 from .proto import method_path, service_methods
 
 # gRPC's default 4 MiB message cap (SURVEY §5) would cap a Memcpy at ~4 MiB;
@@ -40,17 +42,35 @@ class GPUCoordinatorStub(_Stub):
     _service = "GPUCoordinator"
 
 
+def _timed(fn, hist: Histogram):
+    def handler(request, context):
+        t0 = time.perf_counter()
+        try:
+            return fn(request, context)
+        finally:  # aborted calls (context.abort raises) are timed too
+            hist.add(time.perf_counter() - t0)
+    return handler
+
+
 def add_servicer(server: grpc.Server, service: str, servicer) -> None:
     """Register `servicer` (an object with one method per RPC, signature
     ``(request, context)``; client-streaming ones get the request iterator).
     Methods the servicer lacks answer UNIMPLEMENTED, like the Go
-    ``Unimplemented*`` defaults (gpu_sim_grpc.pb.go:560-562)."""
+    ``Unimplemented*`` defaults (gpu_sim_grpc.pb.go:560-562).  Every
+    implemented RPC is timed into ``servicer.rpc_latency[method]`` (a log2
+    :class:`~hipdsml.utils.metrics.Histogram`; the reference only logs)."""
     handlers = {}
+    lat = getattr(servicer, "rpc_latency", None)
+    if lat is None:
+        lat = {}
+        servicer.rpc_latency = lat
     for meth, req, resp, cstream in service_methods(service):
         impl = getattr(servicer, meth, None)
         if impl is None:
             def impl(request, context, _m=meth):  # noqa: E306
                 context.abort(grpc.StatusCode.UNIMPLEMENTED, f"method {_m} not implemented")
+        else:
+            impl = _timed(impl, lat.setdefault(meth, Histogram(meth)))
         if cstream:
             h = grpc.stream_unary_rpc_method_handler(impl, request_deserializer=req.FromString,
                                                      response_serializer=resp.SerializeToString)

@@ -28,6 +28,24 @@ def test_get_device_metadata(dev):  # TestGetDeviceMetadata (:46-63)
     assert md.backend == "host"
 
 
+def test_rpc_latency_histograms(dev):
+    """Every served RPC is timed per method (log2 histogram), reported by GetStats."""
+    import json
+
+    stub, svc, _ = dev
+    for _ in range(5):
+        stub.GetDeviceMetadata(pb.GetDeviceMetadataRequest())
+    with pytest.raises(grpc.RpcError):  # aborted calls are timed too
+        stub.GetStreamStatus(pb.GetStreamStatusRequest(streamId=pb.StreamId(value=7)))
+        stub.BeginReceive(pb.BeginReceiveRequest(streamId=pb.StreamId(value=(1001 << 32) | 99),
+                                                 recvBuffAddr=pb.MemAddr(value=0x1000)))
+    h = svc.rpc_latency["GetDeviceMetadata"]
+    assert h.n == 5 and 0 < h.min <= h.max and h.quantile(0.5) >= h.min
+    st = json.loads(stub.GetStats(pb.GetStatsRequest()).json)
+    assert st["rpc_latency"]["GetDeviceMetadata"]["n"] == 5
+    assert st["rpc_latency"]["BeginReceive"]["n"] == 1
+
+
 def test_begin_send(dev):  # TestBeginSend (:65-79)
     stub, _, _ = dev
     r = stub.BeginSend(pb.BeginSendRequest(sendBuffAddr=pb.MemAddr(value=0x1000), numBytes=1024,
