@@ -331,7 +331,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                     int64_t B, int64_t K, int64_t C, torch::Tensor labels,
                                     double inv_batch, c10::optional<torch::Tensor> logits,
                                     torch::Tensor dz, c10::optional<torch::Tensor> dzT,
-                                    torch::Tensor stats) {
+                                    torch::Tensor stats, c10::optional<torch::Tensor> dzp,
+                                    c10::optional<torch::Tensor> dzpT) {
     TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && H.size(0) >= B && H.size(1) >= K, "H shape");
     TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.size(0) >= C && W.size(1) >= K, "W shape");
     check_cuda(labels, "labels"); check_f32(stats, "stats");
@@ -346,13 +347,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     uint16_t* t = nullptr; int64_t ldt = 0;
     if (dzT) { TORCH_CHECK(dzT->dim() == 2 && dzT->size(0) >= Cp && dzT->size(1) >= B, "dzT shape");
                t = bf16p(*dzT, "dzT"); ldt = dzT->stride(0); }
+    uint16_t* pp = nullptr; int64_t ldp = 0; uint16_t* ppT = nullptr; int64_t ldpT = 0;
+    if (dzp) { TORCH_CHECK(dzp->dim() == 2 && dzp->stride(1) == 1 && dzp->size(0) >= B && dzp->size(1) >= K, "dzp shape");
+               pp = bf16p(*dzp, "dzp"); ldp = dzp->stride(0); }
+    if (dzpT) { TORCH_CHECK(dzp && dzpT->dim() == 2 && dzpT->stride(1) == 1 && dzpT->size(0) >= K && dzpT->size(1) >= B,
+                            "dzpT shape (needs dzp)");
+                ppT = bf16p(*dzpT, "dzpT"); ldpT = dzpT->stride(0); }
     hip_ok(head_softmax_xent(bf16p(H, "H"), H.stride(0), bf16p(W, "W"), W.stride(0), b, (int)B, (int)K,
                              (int)C, labels.data_ptr<int32_t>(), (float)inv_batch, lg, ldl,
                              bf16p(dz, "dz"), dz.stride(0), t, ldt, (int)Cp, stats.data_ptr<float>(),
-                             cur_stream()), "head_softmax_xent");
+                             cur_stream(), pp, ldp, ppT, ldpT), "head_softmax_xent");
   }, py::arg("H"), py::arg("W"), py::arg("bias"), py::arg("B"), py::arg("K"), py::arg("C"),
      py::arg("labels"), py::arg("inv_batch"), py::arg("logits"), py::arg("dz"), py::arg("dzT"),
-     py::arg("stats"));
+     py::arg("stats"), py::arg("dzp") = py::none(), py::arg("dzpT") = py::none());
   m.def("rowsum_bf16", [bf16p](torch::Tensor X, int64_t N, int64_t cols, c10::optional<torch::Tensor> out,
                               c10::optional<torch::Tensor> bias, double lr) {
     TORCH_CHECK(X.dim() == 2 && X.size(0) >= N && X.size(1) >= cols, "X shape");

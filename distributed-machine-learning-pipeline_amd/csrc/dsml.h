@@ -200,12 +200,16 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 hipError_t softmax_xent(const float* logits, int64_t ldl, const int32_t* labels, int B, int C,
                         int Cp, float inv_batch, uint16_t* dz, int64_t ldz, uint16_t* dzT,
                         int64_t ldt, float* stats, hipStream_t s);
-// Classifier head fused with softmax-CE (C <= 16): logits = H . W^T + b per
-// row, then the softmax_xent outputs.  `logits` may be null.
+// Classifier head fused with softmax-CE (C <= 16, K <= 4096): logits = H . W^T
+// + b per row, then the softmax_xent outputs.  `logits` may be null.  With
+// `dzp`, also the next backward product: dzp = (dz . W) * (H > 0) in bf16
+// (+ the transposed copy dzpT), from operands the kernel already holds.
 hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,
                              const float* bias, int B, int K, int C, const int32_t* labels,
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
-                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s);
+                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
+                             uint16_t* dzp = nullptr, int64_t ldzp = 0, uint16_t* dzpT = nullptr,
+                             int64_t ldpt = 0);
 hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
                        float lr, hipStream_t s);
 hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,

@@ -722,9 +722,11 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
     float inv_batch, float* __restrict__ logits, int64_t ldl, uint16_t* __restrict__ dz,
-    int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats) {
+    int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats,
+    uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt) {
   __shared__ float part[kHeadMaxC][257];  // per-thread partial dot products, per class
   __shared__ float zsum[kHeadMaxC];
+  __shared__ float gz[kHeadMaxC];         // bf16-rounded dLogits of this row
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* hr = H + (int64_t)m * ldh;
   // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
@@ -766,49 +768,88 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     if (sg == 0) zsum[c] = v;
   }
   __syncthreads();
-  if (w != 0) return;
-  const int c = lane;
-  const bool cv = c < C;
-  float z = -3.402823466e38f;
-  if (cv) z = zsum[c] + (bias ? bias[c] : 0.f);
-  if (cv && logits) logits[(int64_t)m * ldl + c] = z;
-  const int y = labels[m];
-  float mx = z;
-  int am = cv ? c : 0x7fffffff;
+  if (w == 0) {
+    const int c = lane;
+    const bool cv = c < C;
+    float z = -3.402823466e38f;
+    if (cv) z = zsum[c] + (bias ? bias[c] : 0.f);
+    if (cv && logits) logits[(int64_t)m * ldl + c] = z;
+    const int y = labels[m];
+    float mx = z;
+    int am = cv ? c : 0x7fffffff;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(mx, o, 64);
-    const int oa = __shfl_xor(am, o, 64);
-    argmax_combine(mx, am, om, oa);
-  }
-  const float e = cv ? expf(z - mx) : 0.f;
-  float se = e;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(am, o, 64);
+      argmax_combine(mx, am, om, oa);
+    }
+    const float e = cv ? expf(z - mx) : 0.f;
+    float se = e;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
-  const float p = e / se;
-  const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
-  if (c < Cp) {
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    const float p = e / se;
+    const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
     const uint16_t hq = f32_to_bf16(gr);
-    dz[(int64_t)m * ldz + c] = hq;
-    if (dzT) dzT[(int64_t)c * ldt + m] = hq;
+    if (c < Cp) {
+      dz[(int64_t)m * ldz + c] = hq;
+      if (dzT) dzT[(int64_t)c * ldt + m] = hq;
+    }
+    if (c < kHeadMaxC) gz[c] = bf16_to_f32(hq);
+    if (c == y && stats) {
+      atomicAdd(stats + 0, -logf(p + 1e-10f));
+      atomicAdd(stats + 1, am == y ? 1.f : 0.f);
+      atomicAdd(stats + 2, 1.f);
+    }
   }
-  if (c == y && stats) {
-    atomicAdd(stats + 0, -logf(p + 1e-10f));
-    atomicAdd(stats + 1, am == y ? 1.f : 0.f);
-    atomicAdd(stats + 2, 1.f);
+  if (dzp == nullptr) return;
+  // ---- fused activation gradient of the layer below (the NEXT backward GEMM):
+  // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
+  // chunks this thread already holds; bf16 row store + transposed copy.
+  __syncthreads();
+  float g[kHeadMaxC];
+#pragma unroll
+  for (int c = 0; c < kHeadMaxC; ++c) g[c] = c < C ? gz[c] : 0.f;
+#pragma unroll
+  for (int j = 0; j < kHeadMaxK8; ++j) {
+    const int k = (t + 256 * j) * 8;
+    if (k >= K) continue;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < kHeadMaxC; ++c) {
+      const uint4 x = wv[j][c];
+      a[0] += g[c] * bf16lo(x.x); a[1] += g[c] * bf16hi(x.x);
+      a[2] += g[c] * bf16lo(x.y); a[3] += g[c] * bf16hi(x.y);
+      a[4] += g[c] * bf16lo(x.z); a[5] += g[c] * bf16hi(x.z);
+      a[6] += g[c] * bf16lo(x.w); a[7] += g[c] * bf16hi(x.w);
+    }
+    const float h[8] = {bf16lo(hv[j].x), bf16hi(hv[j].x), bf16lo(hv[j].y), bf16hi(hv[j].y),
+                        bf16lo(hv[j].z), bf16hi(hv[j].z), bf16lo(hv[j].w), bf16hi(hv[j].w)};
+    uint16_t q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = f32_to_bf16(h[e] > 0.f ? a[e] : 0.f);
+    *reinterpret_cast<uint4*>(dzp + (int64_t)m * ldzp + k) =
+        make_uint4(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16),
+                   q[4] | ((uint32_t)q[5] << 16), q[6] | ((uint32_t)q[7] << 16));
+    if (dzpT) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dzpT[(int64_t)(k + e) * ldpt + m] = q[e];
+    }
   }
 }
 
 hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,
                              const float* bias, int B, int K, int C, const int32_t* labels,
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
-                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s) {
+                             uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
+                             uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt) {
+  if (dzp && ((ldzp & 7) || ((uintptr_t)dzp & 15))) return hipErrorInvalidValue;
   if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
       (ldw & 7) ||
       (((uintptr_t)H | (uintptr_t)W) & 15))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_softmax_xent_k, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
-                     labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats);
+                     labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
+                     ldpt);
   return hipGetLastError();
 }
 

@@ -129,11 +129,14 @@ class WideMlpTrainer:
                            obfT=self.HT[l + 1])
             else:
                 self._gemm(f"f{l}", self.H[l], self.Wb[l], bias=b, of32=self.logits)
-        if fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row)
+        if fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
+            # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
             _, b = self.views[L - 1]
+            prev = L >= 2
             C.head_softmax_xent(self.H[L - 1], self.Wb[L - 1], b, Bt, self.pd[L - 1], d[L],
                                 self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], self.dZT[L],
-                                self.stats)
+                                self.stats, dzp=self.dZ[L - 1] if prev else None,
+                                dzpT=self.dZT[L - 1] if prev else None)
         else:
             C.softmax_xent(self.logits, self.y[r0:r0 + Bt], Bt, d[L], 1.0 / Bt, self.dZ[L],
                            self.dZT[L], self.stats)
@@ -143,7 +146,8 @@ class WideMlpTrainer:
         for l in range(L - 1, -1, -1):
             W, b = self.views[l]
             gW, gb = self.gviews[l]
-            if l > 0:  # activation gradient first: it needs the pre-update W_l^T
+            if l > 0 and not (fused_head and l == L - 1):
+                # activation gradient first: it needs the pre-update W_l^T
                 self._gemm(f"b{l}", self.dZ[l + 1], self.WbT[l], mask=self.H[l], obf=self.dZ[l],
                            obfT=self.dZT[l])
             if fused_sgd:

@@ -132,6 +132,18 @@ def test_head_softmax_xent(C_, K):
     assert stats[2].item() == B
     loss = -torch.log(p.gather(1, y.long().view(-1, 1)) + 1e-10).sum().item()
     assert abs(stats[0].item() - loss) / loss < 1e-3
+    # fused next activation gradient: dZ_prev = (bf16(dZ) . W) * (H > 0)
+    Kp = (K + 15) // 16 * 16
+    dzp = torch.zeros(B, Kp, dtype=torch.bfloat16, device=DEV)
+    dzpT = torch.zeros(Kp, B, dtype=torch.bfloat16, device=DEV)
+    C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
+                        dzT, stats, dzp=dzp, dzpT=dzpT)
+    torch.cuda.synchronize()
+    dzb = dz.cpu()[:, :C_].float()
+    want = (dzb @ W.float()) * (H.float() > 0)
+    got = dzp.cpu()[:, :K].float()
+    assert (got - want).abs().max().item() < 1e-2 * max(1.0, want.abs().max().item())
+    assert torch.equal(dzpT.cpu()[:K].t(), dzp.cpu()[:, :K])
 
 
 @pytest.mark.parametrize("gemm", ["rows64", "splitk"])
