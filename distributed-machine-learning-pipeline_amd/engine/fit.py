@@ -65,11 +65,15 @@ def build_trainer(cfg: TrainConfig, spec: MlpSpec, data: Dataset, ctx: DistConte
         if cfg.momentum or cfg.weight_decay:
             raise ValueError("the wide bf16 engine implements plain SGD")
         return WideMlpTrainer(spec, data, batch=cfg.batch, lr=cfg.lr, ctx=ctx, seed=cfg.seed,
-                              init="kaiming" if cfg.init == "auto" else cfg.init, sync=cfg.sync,
+                              init="kaiming" if cfg.init == "auto" else cfg.init,
+                              # the fused exchanges are fp32-MLP kernels; the wide engine syncs by RCCL
+                              sync="rccl" if cfg.sync in ("auto", "xact", "xgmi") else cfg.sync,
                               graph=cfg.graph_steps != 0), engine
     from .trainer import MlpTrainer
 
-    gs = cfg.graph_steps if not ctx.is_distributed else 0
+    # graphs replay the fused-exchange steps too; a step with an RCCL collective
+    # runs as the eager C++ loop whatever graph_steps says (MlpTrainer.train_steps)
+    gs = cfg.graph_steps
     return MlpTrainer(spec, data, batch=cfg.batch, lr=cfg.lr, ctx=ctx, seed=cfg.seed,
                       init="reference" if cfg.init == "auto" else cfg.init, momentum=cfg.momentum,
                       weight_decay=cfg.weight_decay, sync=cfg.sync,

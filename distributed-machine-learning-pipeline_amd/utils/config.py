@@ -43,9 +43,9 @@ class TrainConfig:
     data: str = "synthetic"               # synthetic | mnist (idx files under data_dir)
     data_dir: str = ""
     samples: int = 60032                  # synthetic samples per replica
-    sync: str = "rccl"                    # auto | xact | xgmi | rccl | ring | torch
+    sync: str = "auto"                    # auto | xact | xgmi | rccl | ring | torch
     ring_chunk_bytes: int = 1 << 20
-    graph_steps: int = 50                 # steps per hipGraph (single replica); 0 = eager
+    graph_steps: int = 50                 # steps per hipGraph (fused-exchange steps too); 0 = eager
     backend: str = "auto"                 # torch.distributed backend: auto | nccl | gloo
     device: str = "auto"                  # auto | cuda | cpu
     checkpoint: str = ""                  # path to write checkpoints to
