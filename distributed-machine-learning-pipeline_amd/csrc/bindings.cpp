@@ -446,7 +446,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     hip_ok(mlp_read_stamps(v.data()), "mlp_read_stamps");
     return v;
   });
-  m.def("mlp_set_stamping", [](bool on) { mlp_set_stamping(on); mlp_set_stamping_fast(on); });
+  m.def("mlp_set_stamping", [](bool on) {
+    mlp_set_stamping(on);
+    mlp_set_stamping_fast(on);
+    mlp_set_stamping_xact(on);
+  });
+  m.def("mlp_stamps_xact", []() {
+    std::vector<uint64_t> v(kMaxStamps);
+    hip_ok(mlp_read_stamps_xact(v.data()), "mlp_read_stamps_xact");
+    return v;
+  });
   m.def("mlp_stamps_fast", []() {
     std::vector<uint64_t> v(kMaxStamps);
     hip_ok(mlp_read_stamps_fast(v.data()), "mlp_read_stamps_fast");

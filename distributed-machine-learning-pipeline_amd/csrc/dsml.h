@@ -126,7 +126,7 @@ bool mlp_xact_supported(const MlpDesc& d);
 // waves: 4 or 8 per tile block, 0 = 8 from 4 ranks on.
 hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
                               int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
-                              int waves, hipStream_t s);
+                              const XchgTab& tab, int waves, hipStream_t s);
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
                               const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
 
@@ -140,6 +140,8 @@ hipError_t mlp_read_stamps(uint64_t* host_out);  // kMaxStamps entries
 void mlp_set_stamping(bool on);
 hipError_t mlp_read_stamps_fast(uint64_t* host_out);
 void mlp_set_stamping_fast(bool on);
+hipError_t mlp_read_stamps_xact(uint64_t* host_out);
+void mlp_set_stamping_xact(bool on);
 
 hipError_t sgd_update_f32(float* P, const float* G, int64_t n, float scale, hipStream_t s);
 hipError_t sgd_momentum_f32(float* P, const float* G, float* V, int64_t n, float lr,

@@ -22,16 +22,21 @@
 // summation order.
 //
 // One launch replaces K_C:
-//   blocks [0, S)           pushers: block s loads 16-column strip s of this
-//                           rank's H_l / dZ_l from the workspace (coalesced),
-//                           transposes it through LDS into fragment order and
-//                           writes it into every rank's receive slot for this
-//                           rank (itself included, so tile blocks read all N
-//                           images the same way) with 16 B system-scope stores
-//                           (sc0 sc1) over xGMI, drains them and raises flag
-//                           (me, s) in each rank's memory.  Pushers never wait.
-//   blocks [S, ...)         one 16(n) x 32(k) tile of some dW_l per block,
-//                           4 waves splitting the N x B/4 MFMA k-steps; they
+//   blocks [0, S x G)       pushers: block (s, g) loads 16-column strip s of
+//                           this rank's H_l / dZ_l from the workspace
+//                           (coalesced), transposes it through LDS into
+//                           fragment order and writes it into this rank's
+//                           receive slot of the ranks of destination group g
+//                           (G = 1 group with 4-wave blocks; with 8-wave blocks
+//                           G = N/2 groups of 2 ranks, one per 256-thread half,
+//                           so no CU issues more than one remote store per
+//                           thread); all groups cover every rank, itself
+//                           included, so tile blocks read all N images the same
+//                           way.  16 B system-scope stores (sc0 sc1) over xGMI,
+//                           drained, then flag (me, s) in each destination's
+//                           memory.  Pushers never wait.
+//   blocks [S x G, ...)     one 16(n) x 32(k) tile of some dW_l per block,
+//                           4 (or 8) waves splitting the N x B/4 k-steps; they
 //                           poll only LOCAL flags, and only those of the <= 3
 //                           strips they read, load the N images from local HBM
 //                           with sc0 sc1 16 B loads, reduce the 4 wave partials
@@ -79,6 +84,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xa_rsrc(const void* p) {
 // ranks, halving each wave's loads and MFMA chain; pushers split the ranks).
 constexpr int kStrip = 1024;  // floats of one 16-column strip of an image matrix
 
+// a[k] for a runtime k from a kernel-argument array, by selects (a dynamic
+// index would copy the array to scratch memory first)
+template <typename T>
+__device__ __forceinline__ T xa_pick(const T (&a)[kMaxPeers], int k) {
+  T r = a[0];
+#pragma unroll
+  for (int j = 1; j < kMaxPeers; ++j) r = k == j ? a[j] : r;
+  return r;
+}
+
+// Phase stamps (s_memrealtime, 100 MHz) of pusher block 0 ([0, 8)) and of the
+// first tile block ([8, 16)), profiling only (tools/xact_stamps.py).
+__device__ uint64_t g_xact_stamps[kMaxStamps];
+__device__ int g_xact_stamp_on;
+#define XA_STAMP(i)                                                                     \
+  do {                                                                                  \
+    if (stamp_on && threadIdx.x == 0) g_xact_stamps[(i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 __host__ __device__ inline int xa_strips(int D) { return (D + 15) >> 4; }
 
 // Image segment of layer l's matrix: which = 0 -> H_l (1 <= l < L), 1 -> dZ_l (1 <= l <= L).
@@ -117,23 +141,32 @@ template <int WV>
 __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
     const float* __restrict__ Xswz, int64_t xstride, float* __restrict__ P,
     const float* __restrict__ ws, int64_t* __restrict__ ctr, MlpDesc d, float lr, XchgArgs xa,
-    int nstrips) {
+    XchgTab tab, int nstrips) {
   constexpr int NH = WV / 4;  // rank phases: wave w serves ranks r with r % NH == w / 4
   __shared__ float red[WV][9][64];  // pushers reuse it as the 64 x 17 transpose tile
   __shared__ int flag_ok;
   const uint64_t step = xa_ctr(ctr) - 1;  // K_A advanced A to step + 1
   const uint64_t want = step + 1;
   const int N = xa.nranks, me = xa.rank;
-  const XchgTab* __restrict__ tab = xa.tab;
+  // the peer pointer table arrives by value in the kernel arguments: no
+  // dependent load before the first store or poll address is known
   const int64_t par = (int64_t)(step & 1) * xa.half;
   const int64_t payload = (int64_t)nstrips * kStrip;
   const int tid = threadIdx.x;
   const int B = d.batch;
+  // pusher blocks: (strip, destination group); each writes its strip to <= NH
+  // ranks (one per 256-thread half), so no CU issues more than NH remote stores
+  // per thread (the store issue rate, not the links, bounded one block per strip)
+  const int G = NH == 2 ? (N + 1) / 2 : 1;  // destination groups (= pusher blocks per strip)
+  const int per = (N + G - 1) / G;          // destinations per pusher block
+  const int npush = nstrips * G;
+  const int stamp_on = g_xact_stamp_on && (blockIdx.x == 0 || (int)blockIdx.x == npush);
 
-  if ((int)blockIdx.x < nstrips) {
+  if ((int)blockIdx.x < npush) {
+    XA_STAMP(0);
     // ------------------------------------------------------------- pusher --
-    // Block s: strip s of this rank's image -> every rank (itself included).
-    const int s = blockIdx.x;
+    // Block (s, grp): strip s of this rank's image -> ranks grp + G * half.
+    const int s = blockIdx.x % nstrips, grp = blockIdx.x / nstrips;
     int m, which, t;
     xa_strip_seg(d, s, m, which, t);
     const int D = d.dims[m];
@@ -155,18 +188,25 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
       for (int k = 0; k < 4; ++k) tile[row * 17 + 4 * (tid & 3) + k] = v[k];
     }
     __syncthreads();
+    XA_STAMP(1);
     const int w = t2 >> 6, ln = t2 & 63, i = ln & 15, q = ln >> 4;
     xa_f4 f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) f[j] = tile[(4 * w + 16 * j + q) * 17 + i];
     const int64_t off = (int64_t)me * payload + (int64_t)s * kStrip + t2 * 4;  // floats
-    for (int dst = half; dst < N; dst += NH)
-      __builtin_amdgcn_raw_buffer_store_b128(f, xa_rsrc(tab->buf[dst] + par), (int)(off * 4), 0,
-                                             kSys);
+    for (int h = half; h < per; h += NH) {
+      const int dst = grp + G * h;
+      if (dst < N)
+        __builtin_amdgcn_raw_buffer_store_b128(f, xa_rsrc(xa_pick(tab.buf, dst) + par),
+                                               (int)(off * 4), 0, kSys);
+    }
+    XA_STAMP(2);
     // every storing wave drains its stores, then one lane per rank raises the flag
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < N) xa_st_flag(tab->flags[tid] + me * nstrips + s, want);
+    XA_STAMP(3);
+    if (tid < per && grp + G * tid < N)
+      xa_st_flag(xa_pick(tab.flags, grp + G * tid) + me * nstrips + s, want);
     if (blockIdx.x == 0 && tid == 0) {
       // step-counter hand-off B = A (the tile blocks never read B)
       __hip_atomic_store(reinterpret_cast<uint64_t*>(ctr + 1), xa_ctr(ctr), __ATOMIC_RELAXED,
@@ -176,7 +216,8 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
   }
 
   // ------------------------------------------------------------------ tile --
-  int bid = blockIdx.x - nstrips;
+  XA_STAMP(8);
+  int bid = blockIdx.x - npush;
   int l = 0;
   for (; l < d.nlayers - 1; ++l) {
     const int nt = ((d.dims[l + 1] + 15) >> 4) * ((d.dims[l] + 31) >> 5);
@@ -227,17 +268,21 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
     }
   }
 
+  XA_STAMP(9);
   // wait for the strips this tile reads, from every rank (local flags):
   // threads [0,64) poll dZ_{l+1} strip tn, [64,128) H_l strip 2tk, [128,192) 2tk+1
   const int sdz = (int)(xa_seg_off(d, l + 1, 1) / kStrip) + tn;
   const int sh = l == 0 ? -1 : (int)(xa_seg_off(d, l, 0) / kStrip) + 2 * tk;
+  // LDS-only barriers around the poll: __syncthreads() would also wait for the
+  // input-fragment and old-weight loads above (s_waitcnt vmcnt(0)), serialising
+  // their memory round trip with the poll's instead of overlapping the two.
   if (tid == 0) flag_ok = 1;
-  __syncthreads();
+  lds_barrier();
   {
     const int part = tid >> 6, src = tid & 63;
     const int strip = part == 0 ? sdz : (sh < 0 || (part == 2 && !s1v) ? -1 : sh + part - 1);
     if (part < 3 && src < N && strip >= 0) {
-      const uint64_t* f = tab->flags[me] + src * nstrips + strip;
+      const uint64_t* f = xa_pick(tab.flags, me) + src * nstrips + strip;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (xa_ld_flag(f) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
@@ -249,11 +294,12 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
       }
     }
   }
-  __syncthreads();
+  lds_barrier();  // every poller is done; flag_ok (LDS) is final
+  XA_STAMP(10);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
 
   // The exchanged operands: one 16 B fragment load per matrix strip and lane.
-  const __amdgpu_buffer_rsrc_t rv = xa_rsrc(tab->buf[me] + par);
+  const __amdgpu_buffer_rsrc_t rv = xa_rsrc(xa_pick(tab.buf, me) + par);
   const int64_t dzo = (int64_t)sdz * kStrip + frag;
   const int64_t ao = l == 0 ? 0 : (int64_t)sh * kStrip - (int64_t)(2 * tk) * kStrip;
 #pragma unroll
@@ -281,6 +327,7 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
       }
     }
   }
+  XA_STAMP(11);
   dbacc += __shfl_xor(dbacc, 16, 64);
   dbacc += __shfl_xor(dbacc, 32, 64);
 #pragma unroll
@@ -290,6 +337,7 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
   }
   red[w][8][lane] = dbacc;
   __syncthreads();
+  XA_STAMP(12);
   if (w != 0 || !flag_ok) return;  // a timed-out peer: leave the weights alone
   float s0v[4], s1v4[4], sb = 0.f;
 #pragma unroll
@@ -313,9 +361,24 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
     }
   }
   if (tk == 0 && q == 0 && nv) P[d.b_off[l] + n] = bold - lr * sb;
+  if (stamp_on) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    XA_STAMP(13);
+  }
 }
 
 }  // namespace
+
+hipError_t mlp_read_stamps_xact(uint64_t* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_xact_stamps), sizeof(uint64_t) * kMaxStamps, 0,
+                             hipMemcpyDeviceToHost);
+}
+
+void mlp_set_stamping_xact(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xact_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
+}
 
 int mlp_xact_payload(const MlpDesc& d) { return (int)xa_seg_off(d, d.nlayers + 1, 0); }
 
@@ -328,7 +391,7 @@ bool mlp_xact_supported(const MlpDesc& d) {
 
 hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, const float* ws,
                               int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
-                              int waves, hipStream_t s) {
+                              const XchgTab& tab, int waves, hipStream_t s) {
   const int payload = mlp_xact_payload(d);
   const int nstrips = payload / kStrip;
   if (ctr == nullptr || x.tab == nullptr || x.err == nullptr || x.nranks < 1 ||
@@ -337,13 +400,15 @@ hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, cons
       xstride < (int64_t)d.nbatches * xa_strips(d.dims[0]) * kStrip ||
       (waves != 0 && waves != 4 && waves != 8))
     return hipErrorInvalidValue;
-  dim3 grid(nstrips + mlp_wgrad_tiles(d));
-  if (waves == 8 || (waves == 0 && x.nranks >= 4))
+  const bool eight = waves == 8 || (waves == 0 && x.nranks >= 4);
+  const int G = eight ? (x.nranks + 1) / 2 : 1;  // pusher blocks per strip
+  dim3 grid(nstrips * G + mlp_wgrad_tiles(d));
+  if (eight)
     hipLaunchKernelGGL(mlp_f32_wgrad_xact_k<8>, grid, dim3(512), 0, s, Xswz, xstride, P, ws, ctr,
-                       d, lr_over_n, x, nstrips);
+                       d, lr_over_n, x, tab, nstrips);
   else
     hipLaunchKernelGGL(mlp_f32_wgrad_xact_k<4>, grid, dim3(256), 0, s, Xswz, xstride, P, ws, ctr,
-                       d, lr_over_n, x, nstrips);
+                       d, lr_over_n, x, tab, nstrips);
   return hipGetLastError();
 }
 

@@ -295,7 +295,7 @@ void MlpRunner::enqueue_step(hipStream_t s) {
     if (xact_)
       DSML_HIP_CHECK(mlp_f32_wgrad_xact(xall_, xstride_, b_.P, b_.ws, b_.ctr, d_,
                                         lr_ / (float)xchg_->nranks(), xchg_->args(),
-                                        xact_waves_, s));
+                                        xchg_->table(), xact_waves_, s));
     else
       DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
                                         lr_ / (float)xchg_->nranks(), xchg_->args(), s));

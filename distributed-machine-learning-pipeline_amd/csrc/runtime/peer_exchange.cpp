@@ -64,6 +64,7 @@ std::vector<uint8_t> PeerExchange::ipc_handle() const {
 
 void PeerExchange::publish_table(const XchgTab& t, int rank, int n) {
   DSML_HIP_CHECK(hipMemcpy(dtab_, &t, sizeof(t), hipMemcpyHostToDevice));
+  tab_host_ = t;
   args_.tab = dtab_;
   args_.rank = rank;
   args_.nranks = n;

@@ -213,6 +213,9 @@ class PeerExchange {
   void allreduce(const float* in, float* out, int64_t n, hipStream_t s, int algo = 0);
   bool connected() const { return args_.tab != nullptr; }
   const XchgArgs& args() const { return args_; }
+  // Host copy of the pointer table (kernels that take it by value, as kernel
+  // arguments, skip the dependent load of the device-resident copy).
+  const XchgTab& table() const { return tab_host_; }
   int nranks() const { return args_.nranks; }
   int rank() const { return args_.rank; }
   int ntiles() const { return ntiles_; }
@@ -233,6 +236,7 @@ class PeerExchange {
   XchgTab* dtab_ = nullptr;
   uint32_t* err_ = nullptr;
   XchgArgs args_;
+  XchgTab tab_host_{};
   uint64_t seq_ = 0;
 };
 
