@@ -128,7 +128,8 @@ hipError_t mlp_f32_wgrad_xact(const float* Xswz, int64_t xstride, float* P, cons
                               int64_t* ctr, const MlpDesc& d, float lr_over_n, const XchgArgs& x,
                               const XchgTab& tab, int waves, hipStream_t s);
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
-                              const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s);
+                              const MlpDesc& d, float lr_over_n, const XchgArgs& x,
+                              const XchgTab& tab, hipStream_t s);
 
 // ---- elementwise / reduction (kernels/elementwise.hip) -----------------------
 enum DType : int32_t { kF32 = 0, kBF16 = 1, kF16 = 2, kU8 = 3, kI32 = 4 };

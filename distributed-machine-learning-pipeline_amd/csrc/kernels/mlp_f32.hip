@@ -395,11 +395,21 @@ __device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
   __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a[k] for a runtime k from a kernel-argument array, by selects (a dynamic
+// index would copy the array to scratch memory first)
+template <typename T>
+__device__ __forceinline__ T pick_peer(const T (&a)[kMaxPeers], int k) {
+  T r = a[0];
+#pragma unroll
+  for (int j = 1; j < kMaxPeers; ++j) r = k == j ? a[j] : r;
+  return r;
+}
+
 template <bool XCHG>
 __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ P, float* __restrict__ Gout,
     const float* __restrict__ ws, int64_t* __restrict__ ctr, int64_t row0, MlpDesc d, float lr,
-    int fused_sgd, XchgArgs xa) {
+    int fused_sgd, XchgArgs xa, XchgTab tab) {
   const int B = d.batch;
   int bid = blockIdx.x;
   int l = 0;
@@ -474,9 +484,10 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     const uint64_t step = ld_ctr(ctr) - 1;
     const uint64_t want = step + 1;
     const int64_t poff = (int64_t)(step & 1) * xa.half;
-    const XchgTab* __restrict__ tab = xa.tab;
+    // the peer pointer table is a kernel argument (no dependent load of the
+    // device copy before the first publish / poll address is known)
     const bool bl = tk == 0 && q == 0;
-    float* mine = tab->buf[xa.rank] + poff;
+    float* mine = pick_peer(tab.buf, xa.rank) + poff;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = tn * 16 + 4 * q + r;
@@ -489,9 +500,9 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     // every lane's payload stores are complete before the flag is raised
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
-      st_sys64(tab->flags[xa.rank] + blockIdx.x, want);
+      st_sys64(pick_peer(tab.flags, xa.rank) + blockIdx.x, want);
     if (lane < xa.nranks && lane != xa.rank) {
-      const uint64_t* f = tab->flags[lane] + blockIdx.x;
+      const uint64_t* f = pick_peer(tab.flags, lane) + blockIdx.x;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (ld_sys64(f) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
@@ -510,7 +521,7 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
 #pragma unroll
     for (int p = 0; p < kMaxPeers; ++p) {
       if (p < xa.nranks && p != xa.rank) {
-        const float* pb = tab->buf[p] + poff;
+        const float* pb = tab.buf[p] + poff;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           pv[p][2 * r] = ld_sys(pb + woff + (int64_t)rc[r] * K + k0c);
@@ -650,18 +661,19 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
                          hipStream_t s) {
   dim3 grid(mlp_wgrad_tiles(d));
   hipLaunchKernelGGL(mlp_f32_wgrad_k<false>, grid, dim3(64), 0, s, X, ldx, P, G, ws, ctr, row0, d,
-                     lr, fused_sgd, XchgArgs{});
+                     lr, fused_sgd, XchgArgs{}, XchgTab{});
   return hipGetLastError();
 }
 
 hipError_t mlp_f32_wgrad_xchg(const float* X, int64_t ldx, float* P, const float* ws, int64_t* ctr,
-                              const MlpDesc& d, float lr_over_n, const XchgArgs& x, hipStream_t s) {
+                              const MlpDesc& d, float lr_over_n, const XchgArgs& x,
+                              const XchgTab& tab, hipStream_t s) {
   if (ctr == nullptr || x.tab == nullptr || x.err == nullptr || x.nranks < 1 ||
       x.nranks > kMaxPeers || x.rank < 0 || x.rank >= x.nranks)
     return hipErrorInvalidValue;
   dim3 grid(mlp_wgrad_tiles(d));
   hipLaunchKernelGGL(mlp_f32_wgrad_k<true>, grid, dim3(64), 0, s, X, ldx, P, nullptr, ws, ctr, 0,
-                     d, lr_over_n, 1, x);
+                     d, lr_over_n, 1, x, tab);
   return hipGetLastError();
 }
 

@@ -298,7 +298,8 @@ void MlpRunner::enqueue_step(hipStream_t s) {
                                         xchg_->table(), xact_waves_, s));
     else
       DSML_HIP_CHECK(mlp_f32_wgrad_xchg(b_.X, b_.ldx, b_.P, b_.ws, b_.ctr, d_,
-                                        lr_ / (float)xchg_->nranks(), xchg_->args(), s));
+                                        lr_ / (float)xchg_->nranks(), xchg_->args(),
+                                        xchg_->table(), s));
     return;
   }
   const bool multi = comm_ != nullptr && comm_->nranks() > 1;
