@@ -60,7 +60,10 @@ def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200) -> 
             out[f"{name}_error"] = str(e)[:200]
         else:
             out[name] = timed(lambda: ar(t))
-            ar.check()
+            # a peer timeout is recorded, not raised: every rank keeps issuing the
+            # same collectives, and the timed training result is still reported
+            if ar.x.error():
+                out[f"{name}_error"] = "peer exchange timed out"
     return out
 
 

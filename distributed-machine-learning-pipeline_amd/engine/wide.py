@@ -12,8 +12,9 @@ copy) runs inside the GEMM, on the last K split of each tile to arrive.  The
 weight-gradient GEMMs carry the SGD update (fp32 master W and the bf16 W / W^T
 copies, vectorised through LDS) and the bias step (row sums of dZ^T) when there
 is one replica.  Per step, with L layers: 1 input cast, L forward GEMMs,
-softmax-CE, 2L-1 backward GEMMs (+ the all-reduce and L update kernels with
-several replicas).
+softmax-CE, 2L-1 backward GEMMs (+ with several replicas, one all-reduce and
+one update per layer, bucketed by layer on a comm stream that overlaps the
+backward of the layers below).
 """
 from __future__ import annotations
 
@@ -94,6 +95,13 @@ class WideMlpTrainer:
         self.comm = None
         if self.ctx.is_distributed and sync in ("rccl", "ring"):
             self.comm = make_native_comm(self.ctx)
+        # per-layer gradient buckets (W_l and b_l plus any padding between them) and
+        # the stream their all-reduce + SGD run on, overlapped with the backward
+        lay = self.layout
+        self._gspan = [(min(lay.w_off[l], lay.b_off[l]),
+                        max(lay.w_off[l] + d[l + 1] * d[l], lay.b_off[l] + d[l + 1]))
+                       for l in range(L)]
+        self._cs = torch.cuda.Stream(dev) if self.ctx.is_distributed else None
         for l in range(L):  # bf16 copies of the initial weights
             W, _ = self.views[l]
             self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, self.Wb[l], self.WbT[l])
@@ -158,20 +166,35 @@ class WideMlpTrainer:
             else:
                 C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, of32=gW,
                                      bgrad=gb)
+                self._sync_layer(l, scale)
         if not fused_sgd:
+            # the next step's forward reads every updated layer
+            torch.cuda.current_stream(self.device).wait_stream(self._cs)
+        self.steps_done += 1
+
+    def _sync_layer(self, l: int, scale: float) -> None:
+        """Per-layer gradient bucket: as soon as layer l's weight gradient is
+        written, its all-reduce and its SGD + bf16 refresh run on the comm stream
+        while the backward of layers < l continues on the compute stream (none of
+        them reads W_l or its bf16 copies).  Buckets are whole layers, issued in
+        the same order on every rank."""
+        C, d = self.C, self.spec.dims
+        main = torch.cuda.current_stream(self.device)
+        self._cs.wait_stream(main)
+        W, b = self.views[l]
+        gW, gb = self.gviews[l]
+        lo, hi = self._gspan[l]
+        with torch.cuda.stream(self._cs):
+            g = self.G[lo:hi]
             if self.comm is not None:
-                (self.comm.ring_allreduce_(self.G, 0, 4 << 20) if self.sync == "ring"
-                 else self.comm.allreduce_(self.G, 0))
+                (self.comm.ring_allreduce_(g, 0, 4 << 20) if self.sync == "ring"
+                 else self.comm.allreduce_(g, 0))
             else:
                 import torch.distributed as dist
 
-                dist.all_reduce(self.G)
-            for l in range(L):
-                W, b = self.views[l]
-                gW, gb = self.gviews[l]
-                C.sgd_cast(W, gW, d[l + 1], d[l], scale, self.Wb[l], self.WbT[l])
-                C.sgd_update_(b, gb, scale)
-        self.steps_done += 1
+                dist.all_reduce(g)
+            C.sgd_cast(W, gW, d[l + 1], d[l], scale, self.Wb[l], self.WbT[l])
+            C.sgd_update_(b, gb, scale)
 
     def _capture_epoch(self) -> None:
         torch.cuda.synchronize(self.device)
