@@ -10,89 +10,134 @@ random-init weights of the same architecture; fp32 compute like the reference.
 Weak scaling: each rank trains batch 64 on its own shard; global batch = 64*N.
 Every timed step is a full optimizer step: fused forward/backward HIP kernels,
 gradient sync (N>1: activation exchange or one-shot gradient exchange fused into
-the weight-gradient kernel over xGMI, or RCCL — chosen at init by a self-test +
-timing), SGD update.
+the weight-gradient kernel over xGMI, RCCL's all-reduce, or the in-house
+multi-ring all-reduce on RCCL send/recv — chosen at init by a self-test + timing
+of every candidate), SGD update.  For N>1 the JSON also carries the µs/step of
+every sync candidate and the 1 MiB device all-reduce latency of each algorithm
+(BASELINE's second metric: ring all-reduce at 1 MiB).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: launched by torch.distributed.run, one rank per GPU)
+Launch:
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+    N = 1: runs in this process.
+    N > 1 without a launcher: this process never touches the GPU; it starts
+    `torch.distributed.run` with N ranks (one per GPU) and exits with its code.
+    Fewer than N visible GPUs is an error (rc 2), never a smaller run.
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    (the driver's form): WORLD_SIZE must equal --gpus.
+  --cpu-dry-run: the same launcher and rank plumbing on CPU (gloo, torch
+    reference math); its JSON says "rehearsal": true and "device": "cpu".
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_SAMPLES_PER_S = 819.0  # BASELINE.md: 599,680 samples / 732 s
+_LAUNCHED = "HIPDSML_BENCH_CHILD"
 
 
-def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200) -> dict:
-    """Device all-reduce latency of a `nbytes` fp32 buffer across the job's GPUs
-    (the BASELINE's second metric, ring all-reduce at 1 MiB): RCCL's
-    ncclAllReduce and the one-shot and two-shot xGMI peer all-reduces.  Max
-    over ranks."""
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(a, argv) -> int:
+    """Parent of an N-rank run: count GPUs (no GPU initialisation), start one
+    rank per GPU through torch.distributed.run, return its exit code."""
+    n = a.gpus
+    if not a.cpu_dry_run:
+        import torch
+
+        vis = torch.cuda.device_count()  # does not initialise the GPU
+        need = 1 if a.rehearse_one_gpu else n
+        if vis < need:
+            print(f"bench.py: --gpus {n} needs {need} visible GPUs, found {vis}", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, **{_LAUNCHED: "1"})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200,
+                         ring_chunk: int = 1 << 20) -> dict:
+    """Device all-reduce latency (µs, max over ranks) of a `nbytes` fp32 buffer
+    across the job's GPUs: RCCL's ncclAllReduce ("rccl"), the in-house ring on
+    ncclSend/ncclRecv over every directed Hamiltonian ring ("ring") and over a
+    single ring ("ring_1"), and the one-shot / two-shot xGMI peer all-reduces.
+    A candidate that errors or times out on ANY rank is reported as
+    "<name>_error" on every rank, never as a latency."""
     import torch
 
-    from hipdsml.parallel.xchg import ExchangeUnavailable, XgmiAllReduce
+    from hipdsml.parallel.xchg import ExchangeUnavailable, XgmiAllReduce, reset_group
 
-    out = {}
+    out = {"bytes": nbytes, "ring_chunk_bytes": ring_chunk}
     t = torch.zeros(nbytes // 4, device=ctx.device)
 
-    def timed(fn):
-        for _ in range(10):
-            fn()
-        torch.cuda.synchronize()
+    def timed(name, fn, err=lambda: False):
+        ok = 1.0
+        try:
+            for _ in range(10):
+                fn()
+            torch.cuda.synchronize()
+            ok = 0.0 if err() else 1.0
+        except Exception as e:  # noqa: BLE001
+            out[f"{name}_error"] = str(e)[:200]
+            ok = 0.0
+        if ctx.all_reduce_scalars(ok, op="min")[0] < 1:  # agreed before timing
+            out.setdefault(f"{name}_error", "failed on a peer")
+            return
         ctx.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
             fn()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / iters
-        return round(1e6 * ctx.all_reduce_scalars(dt, op="max")[0], 2)
+        bad = ctx.all_reduce_scalars(1.0 if err() else 0.0, op="max")[0]
+        dt = ctx.all_reduce_scalars(dt, op="max")[0]
+        if bad:
+            out[f"{name}_error"] = "peer exchange timed out"
+        else:
+            out[name] = round(1e6 * dt, 2)
 
     if comm is not None:
-        out["rccl"] = timed(lambda: comm.allreduce_(t, 0))
+        timed("rccl", lambda: comm.allreduce_(t, 0))
+        timed("ring", lambda: comm.ring_allreduce_(t, 0, ring_chunk, 0))
+        timed("ring_1", lambda: comm.ring_allreduce_(t, 0, ring_chunk, 1))
     for name, algo in (("xgmi", "oneshot"), ("xgmi_2shot", "twoshot")):
         try:
             ar = XgmiAllReduce(ctx, t.numel(), algo=algo)
         except ExchangeUnavailable as e:
             out[f"{name}_error"] = str(e)[:200]
-        else:
-            out[name] = timed(lambda: ar(t))
-            # a peer timeout is recorded, not raised: every rank keeps issuing the
-            # same collectives, and the timed training result is still reported
-            if ar.x.error():
-                out[f"{name}_error"] = "peer exchange timed out"
+            continue
+        timed(name, lambda: ar(t), lambda: ar.x.error() != 0)
+        reset_group(ctx, ar.x)
     return out
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--model", default="784-128-64-10")
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
-    ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--sync", default="auto", choices=["auto", "xact", "xgmi", "rccl", "ring", "torch"],
-                    help="gradient sync (N>1): xact = activation exchange over xGMI (every GPU "
-                         "pushes its activations and computes the global-batch weight gradients), "
-                         "xgmi = one-shot gradient exchange fused into the weight-gradient kernel, "
-                         "rccl = ncclAllReduce; auto = the fastest of the three measured at init "
-                         "(exchanges only after passing a self-test against an all-reduce)")
-    ap.add_argument("--graph-steps", type=int, default=50,
-                    help="steps captured per hipGraph (0 = eager C++ launch loop); steps with an "
-                         "RCCL collective always run as the eager C++ loop")
-    ap.add_argument("--samples-per-rank", type=int, default=60032)
-    ap.add_argument("--no-allreduce-probe", action="store_true",
-                    help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
-    ap.add_argument("--rehearse-one-gpu", action="store_true",
-                    help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
-                         "two ranks on one GPU); --sync auto then weighs the exchanges against "
-                         "a torch.distributed all-reduce instead of RCCL")
-    a = ap.parse_args()
+def _physical_gpus(ctx) -> int:
+    """Distinct GPUs (host, device UUID) the job's ranks run on."""
+    import torch
 
+    if ctx.device.type != "cuda":
+        return 0
+    props = torch.cuda.get_device_properties(ctx.device)
+    ident = f"{socket.gethostname()}/{getattr(props, 'uuid', '')}/{ctx.device.index}"
+    if not ctx.is_distributed:
+        return 1
+    return len(set(ctx.all_gather_bytes("hipdsml/bench/gpu", ident.encode())))
+
+
+def run(a) -> int:
     import torch
 
     from hipdsml.data.mnist import synthetic_mnist
@@ -102,9 +147,12 @@ def main() -> int:
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != a.gpus:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE",
-              file=sys.stderr)
-    if a.rehearse_one_gpu:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+    rehearsal = bool(a.rehearse_one_gpu or a.cpu_dry_run)
+    if a.cpu_dry_run:
+        ctx = DistContext.from_env(device="cpu", backend="gloo")
+    elif a.rehearse_one_gpu:
         ctx = DistContext.from_env(device="cuda", backend="gloo", device_index=0)
     else:
         ctx = DistContext.from_env(device="cuda")
@@ -113,23 +161,41 @@ def main() -> int:
     tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,
                     graph_steps=a.graph_steps,
                     auto_fallback="torch" if a.rehearse_one_gpu else "rccl")
+    n = ctx.world_size
+    sync_us = None
+    if n > 1 and tr.sync_times and a.sync == "auto":
+        sync_us = tr.sync_times  # auto already timed every candidate
+    elif n > 1 and tr.backend == "hip" and not a.no_sync_sweep:
+        # every sync candidate's µs/step, measured the way training runs it
+        cands = ["xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu else ["xact", "xgmi", "torch"]
+        sync_us = tr.time_sync_modes(cands, steps=max(100, a.graph_steps * 2))
     tr.train_steps(a.warmup)
     tr.synchronize()
+    tr.prepare(a.steps)  # graph capture stays outside the timed region
+    tr.read_stats()
     ctx.barrier()
-    torch.cuda.synchronize()
+    if tr.backend == "hip":
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     tr.train_steps(a.steps)
     tr.synchronize()
-    torch.cuda.synchronize()
+    if tr.backend == "hip":
+        torch.cuda.synchronize()
     t1 = time.perf_counter()
     ctx.barrier()
     elapsed = t1 - t0
     elapsed = ctx.all_reduce_scalars(elapsed, op="max")[0] if ctx.is_distributed else elapsed
     st = tr.read_stats(global_=True)
-    n = ctx.world_size
-    ar_us = allreduce_latency_us(ctx, tr.comm) if n > 1 and not a.no_allreduce_probe else None
+    ar_us = None
+    if n > 1 and tr.backend == "hip" and not a.no_allreduce_probe:
+        ar_us = allreduce_latency_us(ctx, tr.comm, ring_chunk=a.ring_chunk)
+    phys = _physical_gpus(ctx)
     samples = a.batch * n * a.steps
     value = samples / elapsed
+    if tr.comm is not None:
+        rccl_nranks = tr.comm.nranks
+    else:
+        rccl_nranks = n if ctx.backend == "nccl" else None
     if ctx.rank == 0:
         out = {
             "metric": "MNIST MLP samples/sec",
@@ -154,6 +220,12 @@ def main() -> int:
                 "graph_steps": a.graph_steps,
                 "lr": a.lr,
             },
+            "world_size": n,
+            "rccl_nranks": rccl_nranks,
+            "physical_gpus": phys,
+            "rehearsal": rehearsal,
+            "device": ctx.device.type,
+            "sync_us_per_step": sync_us,
             "allreduce_1MiB_us": ar_us,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
@@ -161,6 +233,45 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     ctx.destroy()
     return 0
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--model", default="784-128-64-10")
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--sync", default="auto", choices=["auto", "xact", "xgmi", "rccl", "ring", "torch"],
+                    help="gradient sync (N>1): xact = activation exchange over xGMI (every GPU "
+                         "pushes its activations and computes the global-batch weight gradients), "
+                         "xgmi = one-shot gradient exchange fused into the weight-gradient kernel, "
+                         "rccl = ncclAllReduce, ring = multi-ring all-reduce on ncclSend/ncclRecv; "
+                         "auto = the fastest measured at init (exchanges only after passing a "
+                         "self-test against an all-reduce)")
+    ap.add_argument("--graph-steps", type=int, default=50,
+                    help="steps captured per hipGraph (0 = eager C++ launch loop); RCCL "
+                         "collectives are captured with the kernels")
+    ap.add_argument("--ring-chunk", type=int, default=1 << 20,
+                    help="chunk bytes of the in-house ring all-reduce")
+    ap.add_argument("--samples-per-rank", type=int, default=60032)
+    ap.add_argument("--no-allreduce-probe", action="store_true",
+                    help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
+    ap.add_argument("--no-sync-sweep", action="store_true",
+                    help="skip timing every sync candidate (N>1)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
+                         "two ranks on one GPU); the JSON says rehearsal: true")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="launcher/rank plumbing on CPU (gloo, torch math); rehearsal: true")
+    a = ap.parse_args(argv)
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not os.environ.get(_LAUNCHED):
+        return _launch(a, argv)
+    return run(a)
 
 
 if __name__ == "__main__":

@@ -105,12 +105,19 @@ struct PyMlpRunner {
   std::vector<torch::Tensor> keep;  // keep tensors alive while the runner exists
   std::unique_ptr<MlpRunner> r;
   hipStream_t stream = nullptr;
+  bool own_stream = true;
   int device = 0;
 
+  // stream_handle != 0: run on that (caller-owned) stream instead of a fresh
+  // one.  Replicas of one process that spin on each other (the xGMI exchanges)
+  // need streams on distinct hardware queues; HIP deals streams round-robin over
+  // GPU_MAX_HW_QUEUES, so such groups take streams from a pool created back to
+  // back once per process (parallel/xchg.py replica_streams) rather than
+  // whatever queue a stream created later in a long process lands on.
   PyMlpRunner(const std::vector<int64_t>& desc, torch::Tensor X, torch::Tensor labels,
               torch::Tensor P, torch::Tensor G, torch::Tensor V, torch::Tensor ws,
               torch::Tensor slab, torch::Tensor ctr, torch::Tensor stats, float lr, float momentum,
-              float weight_decay) {
+              float weight_decay, uintptr_t stream_handle) {
     d = desc_from_list(desc);
     check_f32(X, "X");
     check_f32(P, "params");
@@ -153,12 +160,17 @@ struct PyMlpRunner {
     b.stats = stats.data_ptr<float>();
     b.nparams = P.numel();
     hip_ok(hipSetDevice(device), "hipSetDevice");
-    hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (stream_handle != 0) {
+      stream = reinterpret_cast<hipStream_t>(stream_handle);
+      own_stream = false;
+    } else {
+      hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    }
     r = std::make_unique<MlpRunner>(d, b, lr, momentum, weight_decay);
   }
   ~PyMlpRunner() {
     r.reset();
-    if (stream) {
+    if (stream && own_stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
@@ -183,8 +195,8 @@ struct PyMlpRunner {
     hip_ok(hipStreamSynchronize(stream), "sync");
     r->capture(steps, capture_comm, stream);
   }
-  void replay(int times) {
-    for (int i = 0; i < times; ++i) r->replay(stream);
+  void replay(int times, int steps) {
+    for (int i = 0; i < times; ++i) r->replay(stream, steps);
   }
   void synchronize() {
     py::gil_scoped_release nogil;
@@ -488,12 +500,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<PyMlpRunner>(m, "MlpRunner")
       .def(py::init<const std::vector<int64_t>&, torch::Tensor, torch::Tensor, torch::Tensor,
                     torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
-                    torch::Tensor, float, float, float>())
+                    torch::Tensor, float, float, float, uintptr_t>(),
+           py::arg("desc"), py::arg("X"), py::arg("labels"), py::arg("P"), py::arg("G"),
+           py::arg("V"), py::arg("ws"), py::arg("slab"), py::arg("ctr"), py::arg("stats"),
+           py::arg("lr"), py::arg("momentum"), py::arg("weight_decay"), py::arg("stream") = 0)
       .def("step", &PyMlpRunner::step, py::arg("n") = 1)
       .def("fwd_bwd", &PyMlpRunner::fwd_bwd)
       .def("update", &PyMlpRunner::update)
       .def("capture", &PyMlpRunner::capture, py::arg("steps"), py::arg("capture_comm") = true)
-      .def("replay", &PyMlpRunner::replay, py::arg("times") = 1)
+      .def("replay", &PyMlpRunner::replay, py::arg("times") = 1, py::arg("steps") = 0)
+      .def("captured", [](PyMlpRunner& s, int steps) { return s.r->captured(steps); },
+           py::arg("steps") = 0)
       .def("synchronize", &PyMlpRunner::synchronize)
       .def("stream_handle", &PyMlpRunner::stream_handle)
       .def("graph_steps", [](PyMlpRunner& s) { return s.r->graph_steps(); })

@@ -54,6 +54,36 @@ __device__ __forceinline__ void full_barrier() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Spin until the peer flag *f reaches `want` (system-scope relaxed polls).
+// Gives up after `timeout` s_memrealtime ticks (100 MHz) and sets *err — and
+// also stops as soon as *err is already set: once any wait of the exchange has
+// timed out, the peer is gone, and every later wait (other blocks, later
+// calls) returning at once keeps a dead peer from costing one full timeout per
+// wait.  Returns true when the flag arrived.
+template <int kSleep>
+__device__ __forceinline__ bool poll_flag_ge(const uint64_t* f, uint64_t want, uint32_t* err,
+                                             uint64_t timeout) {
+  typedef __attribute__((address_space(1))) uint64_t g64;
+  typedef __attribute__((address_space(1))) uint32_t g32;
+  const g64* gf = (const g64*)f;
+  const g32* ge = (const g32*)err;
+  if (__hip_atomic_load(gf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want) return true;
+  if (__hip_atomic_load(ge, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t it = 0;
+  while (__hip_atomic_load(gf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    if ((++it & 255u) == 0u &&
+        __hip_atomic_load(ge, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+      return false;
+    __builtin_amdgcn_s_sleep(kSleep);
+  }
+  return true;
+}
+
 // DPP lane permutations (no LDS round trip, unlike __shfl_* = ds_bpermute).
 constexpr int kDppQuadXor1 = 0xB1;      // quad_perm:[1,0,3,2]
 constexpr int kDppQuadXor2 = 0x4E;      // quad_perm:[2,3,0,1]

@@ -388,9 +388,6 @@ __device__ __forceinline__ void st_sys(float* p, float v) {
   __hip_atomic_store((gu32*)(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
-  return __hip_atomic_load((const gu64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
   __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -501,17 +498,9 @@ __global__ __launch_bounds__(64) void mlp_f32_wgrad_k(
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       st_sys64(pick_peer(tab.flags, xa.rank) + blockIdx.x, want);
-    if (lane < xa.nranks && lane != xa.rank) {
-      const uint64_t* f = pick_peer(tab.flags, lane) + blockIdx.x;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (ld_sys64(f) < want) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
-          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
+    if (lane < xa.nranks && lane != xa.rank)
+      (void)poll_flag_ge<2>(pick_peer(tab.flags, lane) + blockIdx.x, want, xa.err,
+                            xa.timeout_ticks);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __asm__ volatile("" ::: "memory");
     // All peers' tiles in one load batch, then the ordered sum.

@@ -65,9 +65,6 @@ typedef __attribute__((address_space(1))) uint64_t xa_u64;
 typedef float xa_f4 __attribute__((ext_vector_type(4)));
 constexpr int kSys = 1 | 16;  // buffer aux: sc0 | sc1 = system scope
 
-__device__ __forceinline__ uint64_t xa_ld_flag(const uint64_t* p) {
-  return __hip_atomic_load((const xa_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void xa_st_flag(uint64_t* p, uint64_t v) {
   __hip_atomic_store((xa_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -282,16 +279,9 @@ __global__ __launch_bounds__(64 * WV) void mlp_f32_wgrad_xact_k(
     const int part = tid >> 6, src = tid & 63;
     const int strip = part == 0 ? sdz : (sh < 0 || (part == 2 && !s1v) ? -1 : sh + part - 1);
     if (part < 3 && src < N && strip >= 0) {
-      const uint64_t* f = xa_pick(tab.flags, me) + src * nstrips + strip;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (xa_ld_flag(f) < want) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
-          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          flag_ok = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
+      if (!poll_flag_ge<1>(xa_pick(tab.flags, me) + src * nstrips + strip, want, xa.err,
+                           xa.timeout_ticks))
+        flag_ok = 0;
     }
   }
   lds_barrier();  // every poller is done; flag_ok (LDS) is final

@@ -33,10 +33,6 @@ __device__ __forceinline__ void st_sys4(float* p, float4 v) {
   __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(q + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint64_t ld_flag(const uint64_t* p) {
-  return __hip_atomic_load((const __attribute__((address_space(1))) uint64_t*)p, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void st_flag(uint64_t* p, uint64_t v) {
   __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)p, v, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
@@ -69,17 +65,8 @@ __global__ __launch_bounds__(kXThreads) void xchg_allreduce_k(const float* __res
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) st_flag(tab->flags[xa.rank] + blockIdx.x, seq);
-  if (threadIdx.x < xa.nranks && threadIdx.x != xa.rank) {
-    const uint64_t* f = tab->flags[threadIdx.x] + blockIdx.x;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (ld_flag(f) < seq) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
-        __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
+  if (threadIdx.x < xa.nranks && threadIdx.x != xa.rank)
+    (void)poll_flag_ge<1>(tab->flags[threadIdx.x] + blockIdx.x, seq, xa.err, xa.timeout_ticks);
   __syncthreads();
   float4 acc[U];
 #pragma unroll
@@ -140,17 +127,9 @@ __global__ __launch_bounds__(kXThreads) void xchg_allreduce2_k(const float* __re
     return b >= n ? 0 : (n - b < cs ? n - b : cs);
   };
   auto wait_flags = [&](int base) {
-    if (threadIdx.x < N && threadIdx.x != me) {
-      const uint64_t* f = tab->flags[threadIdx.x] + base + blockIdx.x;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (ld_flag(f) < seq) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
-          __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
+    if (threadIdx.x < N && threadIdx.x != me)
+      (void)poll_flag_ge<1>(tab->flags[threadIdx.x] + base + blockIdx.x, seq, xa.err,
+                            xa.timeout_ticks);
     __syncthreads();
   };
   // ---- phase 1a: publish this block's slice of every chunk ----

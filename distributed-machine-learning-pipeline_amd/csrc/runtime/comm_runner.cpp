@@ -206,11 +206,17 @@ MlpRunner::MlpRunner(const MlpDesc& d, const MlpBuffers& b, float lr, float mome
 MlpRunner::~MlpRunner() { reset_graph(); }
 
 void MlpRunner::reset_graph() {
-  if (exec_) (void)hipGraphExecDestroy(exec_);
-  if (graph_) (void)hipGraphDestroy(graph_);
-  exec_ = nullptr;
-  graph_ = nullptr;
+  for (auto& kv : graphs_) {
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+  }
+  graphs_.clear();
   graph_steps_ = 0;
+}
+
+bool MlpRunner::captured(int steps) const {
+  if (steps == 0) return graph_steps_ != 0;
+  return graphs_.count(steps) != 0;
 }
 
 void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
@@ -324,8 +330,15 @@ void MlpRunner::enqueue_step(hipStream_t s) {
 
 void MlpRunner::capture(int steps, bool capture_comm, hipStream_t s) {
   if (steps < 1) throw std::invalid_argument("capture: steps must be >= 1");
-  reset_graph();
+  if (capture_comm != capture_comm_) reset_graph();
   capture_comm_ = capture_comm;
+  auto it = graphs_.find(steps);
+  if (it != graphs_.end()) {  // recapture (buffers or plan may have changed)
+    if (it->second.exec) (void)hipGraphExecDestroy(it->second.exec);
+    if (it->second.graph) (void)hipGraphDestroy(it->second.graph);
+    graphs_.erase(it);
+  }
+  Captured c;
   DSML_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
   try {
     for (int i = 0; i < steps; ++i) enqueue_step(s);
@@ -335,14 +348,21 @@ void MlpRunner::capture(int steps, bool capture_comm, hipStream_t s) {
     if (g) (void)hipGraphDestroy(g);
     throw;
   }
-  DSML_HIP_CHECK(hipStreamEndCapture(s, &graph_));
-  DSML_HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  DSML_HIP_CHECK(hipStreamEndCapture(s, &c.graph));
+  const hipError_t e = hipGraphInstantiate(&c.exec, c.graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(c.graph);
+    DSML_HIP_CHECK(e);
+  }
+  graphs_[steps] = c;
   graph_steps_ = steps;
 }
 
-void MlpRunner::replay(hipStream_t s) {
-  if (!exec_) throw std::runtime_error("replay: no captured graph");
-  DSML_HIP_CHECK(hipGraphLaunch(exec_, s));
+void MlpRunner::replay(hipStream_t s, int steps) {
+  if (steps == 0) steps = graph_steps_;
+  auto it = graphs_.find(steps);
+  if (it == graphs_.end()) throw std::runtime_error("replay: no captured graph of that size");
+  DSML_HIP_CHECK(hipGraphLaunch(it->second.exec, s));
 }
 
 void mlp_eval(const MlpDesc& d, const float* X, int64_t ldx, const int32_t* labels, int64_t row0,

@@ -279,11 +279,14 @@ class MlpRunner {
   // the gradient all-reduce is driven from Python.
   void enqueue_fwd_bwd(hipStream_t s);
   void enqueue_update(hipStream_t s);
-  // Capture `steps` steps into a hipGraph on stream s (comm included when
-  // capture_comm).  Replaying it runs `steps` steps.
+  // Capture `steps` steps into a hipGraph on stream s (the RCCL collective of a
+  // multi-rank step included: it is recorded as graph nodes like any kernel).
+  // Graphs are kept per step count, so a run of n = q * G + r steps replays a
+  // G-step and an r-step graph instead of falling back to eager launches.
   void capture(int steps, bool capture_comm, hipStream_t s);
-  void replay(hipStream_t s);
-  bool captured() const { return exec_ != nullptr; }
+  // Replay the graph of `steps` steps (0: the most recently captured one).
+  void replay(hipStream_t s, int steps = 0);
+  bool captured(int steps = 0) const;
   int graph_steps() const { return graph_steps_; }
   void reset_graph();
   const MlpDesc& desc() const { return d_; }
@@ -307,9 +310,12 @@ class MlpRunner {
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;
-  hipGraph_t graph_ = nullptr;
-  hipGraphExec_t exec_ = nullptr;
-  int graph_steps_ = 0;
+  struct Captured {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::map<int, Captured> graphs_;  // by step count
+  int graph_steps_ = 0;             // step count of the last capture
   bool capture_comm_ = true;
 };
 

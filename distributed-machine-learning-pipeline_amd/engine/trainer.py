@@ -69,8 +69,9 @@ class MlpTrainer:
                  momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
                  ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
                  params: Optional[torch.Tensor] = None, external_comm=None,
-                 capture_collectives: bool = False, xchg_timeout_ms: float = 10000.0,
-                 xact_waves: int = 0, auto_fallback: str = "rccl"):
+                 capture_collectives: Optional[bool] = None, xchg_timeout_ms: float = 10000.0,
+                 xact_waves: int = 0, auto_fallback: str = "rccl",
+                 stream: Optional["torch.cuda.Stream"] = None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -100,7 +101,11 @@ class MlpTrainer:
         self._stats_cpu = StepStats()
         self.comm = external_comm
         self.xchg = None
-        self.capture_collectives = capture_collectives
+        if capture_collectives is None:  # RCCL collectives recorded into the step graphs
+            import os
+
+            capture_collectives = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "1") != "0"
+        self.capture_collectives = bool(capture_collectives)
         self.xchg_timeout_ms = xchg_timeout_ms
         self.xact_waves = int(xact_waves)  # 0: 8-wave tile blocks from 4 ranks on, else 4
         # sync='auto' without RCCL (one-GPU rehearsals, where RCCL refuses two
@@ -114,6 +119,7 @@ class MlpTrainer:
         self.Xall: Optional[torch.Tensor] = None
         self._exchanges: Dict[str, object] = {}
         self.runner = None
+        self._stream = stream  # caller-owned stream for the native runner (None: its own)
         if self.device.type == "cuda":
             self._init_hip(ring_chunk_bytes)
             self.backend = "hip"
@@ -135,9 +141,11 @@ class MlpTrainer:
         self.stats = torch.zeros(4, dtype=torch.float32, device=d)
         self.runner = C.MlpRunner(self.layout.desc_list(), self.X, self.y, self.P, self.G, self.V,
                                   self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
-                                  self.weight_decay)
+                                  self.weight_decay,
+                                  stream=self._stream.cuda_stream if self._stream is not None else 0)
         self.runner.set_world_size(self.ctx.world_size)
-        self._captured = False
+        self._ring_chunk = int(ring_chunk_bytes)
+        self._collective_warm = False  # an eager collective step has run (RCCL connected)
         if not self.ctx.is_distributed:
             return
         if self.sync == "torch":
@@ -188,9 +196,14 @@ class MlpTrainer:
         return swizzle_inputs(out, self.batch)
 
     def _activate(self, mode: Optional[str]) -> None:
-        if mode is None:
+        """Point the native runner at one gradient-sync mode.  None keeps the
+        RCCL communicator as configured; 'rccl' / 'ring' select ncclAllReduce
+        or the in-house multi-ring send/recv all-reduce on it."""
+        if mode in (None, "rccl", "ring", "torch"):
             self.runner.set_exchange(None)
             self.xchg = None
+            if mode in ("rccl", "ring") and self.comm is not None:
+                self.runner.set_comm(self.comm, 1 if mode == "ring" else 0, self._ring_chunk)
         elif mode == "xgmi":
             self.xchg = self._exchanges["xgmi"]
             self.runner.set_exchange(self.xchg)
@@ -248,52 +261,53 @@ class MlpTrainer:
                 ok.append(m)
         choice = ok[0] if ok else None
         if self.sync == "auto" and ok:
-            times = {}
-            fallback = self.sync_active  # rccl / ring, or torch (rehearsals)
-            for m in ok + [None]:
-                self._activate(m)
-                times[m or fallback] = self._time_steps(20)
+            # every candidate timed the way train_steps runs it (graph replay,
+            # RCCL collectives captured too); ties go to the earlier candidate
+            fallback = ["rccl", "ring"] if self.comm is not None else [self.sync_active]
+            times = self.time_sync_modes(ok + fallback)
             choice = min(times, key=times.get)
-            choice = None if choice == fallback else choice
-            log.info("sync auto: %s", ", ".join(f"{k} {1e6 * v:.1f} us/step"
-                                                for k, v in times.items()))
-            self.sync_times = {k: round(1e6 * v, 2) for k, v in times.items()}
-        self._activate(choice)  # drops any graph captured while timing
-        self._captured = False
-        if choice is not None:
-            self.sync_active = choice
-        if choice != "xact":
+            log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
+            self.sync_times = times
+        self._set_mode(choice or self.sync_active)
+        if self.sync_active != "xact":
             self.Xall = None  # the replicated inputs are only read by xact
 
+    def _set_mode(self, mode: str) -> None:
+        self._activate(mode)
+        self.sync_active = mode
+
+    def time_sync_modes(self, modes, steps: int = 0) -> Dict[str, float]:
+        """Collective: µs/step (max over ranks) of each gradient-sync mode in
+        `modes` (xact / xgmi / rccl / ring / torch), measured as train_steps
+        runs it; the training state and the active mode are restored."""
+        cur = self.sync_active
+        steps = steps or max(100, 2 * self.graph_steps)
+        out: Dict[str, float] = {}
+        for m in modes:
+            if m in EXCHANGE_MODES and m not in self._exchanges:
+                continue
+            if m in ("rccl", "ring") and self.comm is None:
+                continue
+            self._set_mode(m)
+            out[m] = round(1e6 * self._time_steps(steps), 2)
+        self._set_mode(cur)
+        return out
+
     def _time_steps(self, n: int) -> float:
-        """Max-over-ranks wall time per step, run the way train_steps will run
-        the active mode (graph replay for the fused exchanges, the eager C++
-        loop for a step with an RCCL collective); state restored."""
+        """Max-over-ranks wall time per step of the active mode, run exactly as
+        train_steps runs it (graphs prepared and warmed first); state restored."""
         from ..parallel import xchg as X
 
         P0, ctr0, st0 = self.P.clone(), self.ctr.clone(), self.stats.clone()
-        if self.graph_steps > 0 and self.runner.exchange_active():
-            self.runner.capture(self.graph_steps, True)
-            reps = max(1, n // self.graph_steps)
-            n = reps * self.graph_steps
-
-            def run():
-                self.runner.replay(reps)
-            self.runner.replay(1)  # warm-up
-        elif self.comm is None and self.sync_active == "torch":
-            def run():
-                self._hip_step_torch_sync(n)
-            self._hip_step_torch_sync(2)
-        else:
-            def run():
-                self.runner.step(n)
-            self.runner.step(2)
+        sd0 = self.steps_done
+        self.train_steps(n)  # warm-up: RCCL connections, graph capture and upload
         self.runner.synchronize()
         self.ctx.barrier()
         t0 = time.perf_counter()
-        run()
+        self.train_steps(n)
         self.runner.synchronize()
         dt = (time.perf_counter() - t0) / n
+        self.steps_done = sd0
         dt = self.ctx.all_reduce_scalars(dt, op="max")[0]
         self.P.copy_(P0)
         self.ctr.copy_(ctr0)
@@ -316,6 +330,33 @@ class MlpTrainer:
             self.runner.update()
 
     # -------------------------------------------------------------- public --
+    def _graphs_on(self) -> bool:
+        """Whether train_steps replays hipGraphs for the active sync mode."""
+        if self.graph_steps <= 0 or self.runner is None:
+            return False
+        if not self.ctx.is_distributed:
+            return True
+        if self.sync_active == "torch":
+            return False  # torch.distributed all-reduce between native launches
+        if self.sync_active in ("rccl", "ring"):
+            return self.capture_collectives
+        return True  # fused xGMI exchanges
+
+    def _graph_sizes(self, n: int):
+        reps, rem = divmod(n, self.graph_steps)
+        return ([self.graph_steps] if reps else []) + ([rem] if rem else [])
+
+    def prepare(self, n: int) -> None:
+        """Capture (outside any timed region) the graphs train_steps(n) will
+        replay: a run of n = q*G + r steps replays a G-step and an r-step graph."""
+        if self.backend != "hip" or not self._graphs_on():
+            return
+        if self.sync_active in ("rccl", "ring") and not self._collective_warm:
+            return  # captured on first use, after an eager step (train_steps)
+        for k in self._graph_sizes(n):
+            if not self.runner.captured(k):
+                self.runner.capture(k, True)
+
     def train_steps(self, n: int) -> None:
         """Enqueue `n` optimizer steps (asynchronous on GPU)."""
         if n <= 0:
@@ -325,18 +366,25 @@ class MlpTrainer:
                 self._torch_step()
                 self.steps_done += 1
             return
-        collective_in_step = self.ctx.is_distributed and self.sync_active in ("rccl", "ring")
         if self.ctx.is_distributed and self.sync_active == "torch":
             self._hip_step_torch_sync(n)
-        elif self.graph_steps > 0 and (self.capture_collectives or not collective_in_step):
-            if not self._captured:
-                self.runner.capture(self.graph_steps, True)
-                self._captured = True
+        elif self._graphs_on():
+            self.steps_done += n
+            if self.sync_active in ("rccl", "ring") and not self._collective_warm:
+                # RCCL connects its peers on the first collective it enqueues:
+                # run that step eagerly on every rank before anything is captured
+                self.runner.step(1)
+                self._collective_warm = True
+                n -= 1
+                if n == 0:
+                    return
+            self.prepare(n)
             reps, rem = divmod(n, self.graph_steps)
             if reps:
-                self.runner.replay(reps)
+                self.runner.replay(reps, self.graph_steps)
             if rem:
-                self.runner.step(rem)
+                self.runner.replay(1, rem)
+            return
         else:
             self.runner.step(n)
         self.steps_done += n

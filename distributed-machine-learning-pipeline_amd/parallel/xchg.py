@@ -125,6 +125,30 @@ def make_exchange(ctx: DistContext, half_floats: int, ntiles: int, timeout_ms: f
     return x
 
 
+_REPLICA_STREAMS: dict = {}
+
+
+def replica_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
+    """`n` streams for in-process replicas that spin on each other, created
+    back to back on first use and reused for the life of the process.
+
+    HIP gives a new stream a fresh hardware queue until GPU_MAX_HW_QUEUES (4)
+    exist, then the least-used one: a pool created early in the process holds
+    distinct queues, while streams created later in a long process (after
+    torch, copy-engine and RPC streams) can pile onto one queue — and a kernel
+    queued behind a peer that is spinning for it never starts.  Create the pool
+    before other streams (tests/conftest.py does).  n <= 3 is safe: the
+    device's null stream holds a queue of its own."""
+    if n > 4:
+        raise ValueError("at most 4 in-process replicas (one per hardware queue)")
+    key = (device.type, device.index)
+    pool = _REPLICA_STREAMS.setdefault(key, [])
+    if len(pool) < n:
+        # create the whole pool at once so its members are consecutive
+        pool.extend(torch.cuda.Stream(device) for _ in range(4 - len(pool)))
+    return pool[:n]
+
+
 def make_local_group(layout: Optional[MlpLayout], devices: List[int], timeout_ms: float = 10000.0,
                      half_floats: int = 0, ntiles: int = 0):
     """Exchanges for N replicas living in ONE process (tests / single-process

@@ -195,6 +195,48 @@ def test_rccl_single_rank_comm():
     assert comm.aborted
 
 
+@pytest.mark.parametrize("blocking", [True, False])
+def test_rccl_collectives_captured_in_graph(blocking):
+    """RCCL calls recorded into a hipGraph (how multi-GPU steps are replayed)
+    give the same bytes as the eager calls; non-blocking comms too."""
+    C = require_native()
+    comm = C.RcclComm(C.rccl_unique_id(), 0, 1, 0, blocking)
+    x = torch.randn(4096, device=DEV)
+    eager = x.clone()
+    comm.allreduce_(eager, 0)
+    torch.cuda.synchronize()
+    buf = x.clone()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=s):
+        comm.allreduce_(buf, 0)
+        buf.mul_(2.0)
+        comm.allreduce_(buf, 0)
+    for _ in range(3):
+        buf.copy_(x)
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(buf, 2.0 * eager)
+    assert comm.async_error() == ""
+
+
+def test_trainer_graph_sizes_cover_any_step_count():
+    """train_steps(n) replays a G-step and an r-step graph for n = q*G + r
+    (no eager fallback), bit-identical to eager launches."""
+    spec = MlpSpec((784, 128, 64, 10))
+    ds = synthetic_mnist(64 * 8, seed=4)
+    a = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9)
+    b = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9, graph_steps=5)
+    for n in (3, 12, 7):
+        a.train_steps(n)
+        b.train_steps(n)
+    a.synchronize()
+    b.synchronize()
+    assert b.runner.captured(5) and b.runner.captured(3) and b.runner.captured(2)
+    assert torch.equal(a.P, b.P)
+
+
 def test_device_runtime_roundtrip():
     C = require_native()
     arena = C.DeviceArena(0, 1 << 20)

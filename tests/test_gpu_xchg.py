@@ -14,7 +14,8 @@ from hipdsml.data.mnist import synthetic_mnist
 from hipdsml.engine.trainer import MlpTrainer
 from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
 from hipdsml.parallel.dist import DistContext
-from hipdsml.parallel.xchg import make_local_act_group, make_local_group, swizzle_inputs
+from hipdsml.parallel.xchg import (make_local_act_group, make_local_group, replica_streams,
+                                   swizzle_inputs)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -36,8 +37,10 @@ def _reference(world, steps, lr, nb, seed=7):
 
 
 def _local_group(world, nb, graph_steps, timeout_ms=5000.0):
+    # replicas spin on each other: their streams must sit on distinct HW queues
+    ss = replica_streams(DEV, world)
     trs = [MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * nb, seed=300 + r), batch=64, lr=0.05,
-                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps)
+                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps, stream=ss[r])
            for r in range(world)]
     xs = make_local_group(trs[0].layout, [0] * world, timeout_ms)
     for t, x in zip(trs, xs):
@@ -76,8 +79,9 @@ def test_missing_peer_times_out_instead_of_hanging():
 
 def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0, waves=0):
     """Activation exchange between `world` replicas of one process."""
+    ss = replica_streams(DEV, world)
     trs = [MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * nb, seed=300 + r), batch=64, lr=0.05,
-                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps)
+                      seed=7, ctx=DistContext(device=DEV), graph_steps=graph_steps, stream=ss[r])
            for r in range(world)]
     rows = nb * 64
     Xall = swizzle_inputs(torch.stack([t.X[:rows] for t in trs]), 64)
@@ -170,25 +174,13 @@ def test_two_processes_ipc(world, graph_steps, sync):
     assert err < 2e-5, err
 
 
-_STREAMS = []
-
-
-def _replica_streams(n):
-    """One stream per in-process replica, created once: HIP maps streams onto
-    4 hardware queues, and two replicas whose streams landed on the same queue
-    would serialise (the later kernel queued behind its spinning peer)."""
-    while len(_STREAMS) < n:
-        _STREAMS.append(torch.cuda.Stream(DEV))
-    return _STREAMS[:n]
-
-
 @pytest.mark.parametrize("algo", [0, 1])  # one-shot, two-shot
 @pytest.mark.parametrize("world,n", [(2, 262144), (3, 1000), (2, 4), (3, 1 << 20), (3, 12)])
 def test_standalone_allreduce_in_process(world, n, algo):
     n = n // 4 * 4
     xs = make_local_group(None, [0] * world, 5000.0, half_floats=2 << 20, ntiles=256)
     g = torch.Generator().manual_seed(n)
-    streams = _replica_streams(world)
+    streams = replica_streams(DEV, world)
     for it in range(3):  # parity alternates; in-place on the last call
         host = [torch.randn(n, generator=g) for _ in range(world)]
         ins = [h.to(DEV) for h in host]
