@@ -184,6 +184,17 @@ struct PyMlpRunner {
     hip_ok(hipStreamWaitEvent(stream, e, 0), "hipStreamWaitEvent");
     hip_ok(hipEventDestroy(e), "hipEventDestroy");
   }
+  // The reverse edge: torch's current stream waits for everything enqueued on
+  // the runner's stream.  A host-side synchronize alone is not enough for a
+  // consumer on another queue: with per-XCD L2s it can still read lines it
+  // cached before the runner's kernels wrote them back (tests/test_gpu_xchg.py).
+  void join_into_torch() {
+    hipEvent_t e;
+    hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipEventRecord(e, stream), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(cur_stream(), e, 0), "hipStreamWaitEvent");
+    hip_ok(hipEventDestroy(e), "hipEventDestroy");
+  }
   void step(int n) {
     join_torch();
     for (int i = 0; i < n; ++i) r->enqueue_step(stream);
@@ -512,6 +523,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("captured", [](PyMlpRunner& s, int steps) { return s.r->captured(steps); },
            py::arg("steps") = 0)
       .def("synchronize", &PyMlpRunner::synchronize)
+      .def("join_into_torch", &PyMlpRunner::join_into_torch)
       .def("stream_handle", &PyMlpRunner::stream_handle)
       .def("graph_steps", [](PyMlpRunner& s) { return s.r->graph_steps(); })
       .def("set_lr", [](PyMlpRunner& s, float lr) { s.r->set_lr(lr); })
@@ -738,6 +750,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("roctx_push", [](const std::string& name) { return roctxRangePushA(name.c_str()); });
   m.def("roctx_pop", []() { return roctxRangePop(); });
   m.def("roctx_mark", [](const std::string& name) { roctxMarkA(name.c_str()); });
+  // A stream on a hardware queue of its own.  HIP hands ordinary new streams
+  // the least-used of its GPU_MAX_HW_QUEUES (4) queues once they all exist; a
+  // stream created with a CU mask always gets a fresh queue.  In-process
+  // replicas that spin on each other (xGMI exchange tests) need exactly that:
+  // two of them sharing a queue would serialise, the later one never starting.
+  // The mask covers every CU (no partitioning); the stream lives until
+  // stream_destroy.
+  m.def("dedicated_stream", [](int device) {
+    hip_ok(hipSetDevice(device), "hipSetDevice");
+    hipDeviceProp_t p;
+    hip_ok(hipGetDeviceProperties(&p, device), "hipGetDeviceProperties");
+    std::vector<uint32_t> mask((size_t)(p.multiProcessorCount + 31) / 32, 0xffffffffu);
+    hipStream_t st = nullptr;
+    hip_ok(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
+           "hipExtStreamCreateWithCUMask");
+    return reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("stream_destroy", [](uintptr_t h) {
+    hip_ok(hipStreamDestroy(reinterpret_cast<hipStream_t>(h)), "hipStreamDestroy");
+  });
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;

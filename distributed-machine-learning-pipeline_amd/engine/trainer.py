@@ -121,8 +121,8 @@ class MlpTrainer:
         self.runner = None
         self._stream = stream  # caller-owned stream for the native runner (None: its own)
         if self.device.type == "cuda":
-            self._init_hip(ring_chunk_bytes)
             self.backend = "hip"
+            self._init_hip(ring_chunk_bytes)
         else:
             self.backend = "torch"
 
@@ -391,6 +391,7 @@ class MlpTrainer:
 
     def synchronize(self) -> None:
         if self.runner is not None:
+            self.runner.join_into_torch()  # torch reads P / stats after the runner (event edge)
             self.runner.synchronize()
             if self.xchg is not None:
                 from ..parallel.xchg import check

@@ -128,24 +128,27 @@ def make_exchange(ctx: DistContext, half_floats: int, ntiles: int, timeout_ms: f
 _REPLICA_STREAMS: dict = {}
 
 
-def replica_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
-    """`n` streams for in-process replicas that spin on each other, created
-    back to back on first use and reused for the life of the process.
+def replica_streams(device: torch.device, n: int) -> List[torch.cuda.ExternalStream]:
+    """`n` streams for in-process replicas that spin on each other, each on a
+    hardware queue of its own (``_C.dedicated_stream``: a full CU mask makes
+    HIP create a fresh queue instead of handing out the least-used of its
+    GPU_MAX_HW_QUEUES).  Two replicas on one queue would serialise — a kernel
+    queued behind a peer that spins for it never starts.  Created once per
+    process and reused (at most 8).
 
-    HIP gives a new stream a fresh hardware queue until GPU_MAX_HW_QUEUES (4)
-    exist, then the least-used one: a pool created early in the process holds
-    distinct queues, while streams created later in a long process (after
-    torch, copy-engine and RPC streams) can pile onto one queue — and a kernel
-    queued behind a peer that is spinning for it never starts.  Create the pool
-    before other streams (tests/conftest.py does).  n <= 3 is safe: the
-    device's null stream holds a queue of its own."""
-    if n > 4:
-        raise ValueError("at most 4 in-process replicas (one per hardware queue)")
+    These are BLOCKING streams (the CU-mask constructor takes no flags): drive
+    the replicas while torch's current stream is a non-null stream, since the
+    runners join torch's current stream and an event recorded on the legacy
+    null stream waits for every blocking stream — including a spinning peer."""
+    from ..ops.native import require_native
+
+    if n > 8:
+        raise ValueError("at most 8 in-process replicas")
+    C = require_native()
     key = (device.type, device.index)
     pool = _REPLICA_STREAMS.setdefault(key, [])
-    if len(pool) < n:
-        # create the whole pool at once so its members are consecutive
-        pool.extend(torch.cuda.Stream(device) for _ in range(4 - len(pool)))
+    while len(pool) < n:
+        pool.append(torch.cuda.ExternalStream(C.dedicated_stream(device.index), device=device))
     return pool[:n]
 
 

@@ -24,16 +24,6 @@ def _gpu():
 
 def pytest_collection_modifyitems(config, items):
     if _gpu():
-        if any("gpu" in it.keywords for it in items):
-            # In-process replica groups spin on each other and need streams on
-            # distinct HW queues; HIP hands a new stream the least-used queue,
-            # so the pool is created first, before any test makes its own
-            # streams (parallel/xchg.py replica_streams).
-            import torch
-
-            from hipdsml.parallel.xchg import replica_streams
-
-            replica_streams(torch.device("cuda", 0), 4)
         return
     skip = pytest.mark.skip(reason="no GPU on this host")
     for it in items:

@@ -22,6 +22,17 @@ DEV = torch.device("cuda", 0)
 DIMS = (784, 128, 64, 10)
 
 
+@pytest.fixture(autouse=True)
+def _nonblocking_current_stream():
+    """Replica streams (parallel/xchg.py replica_streams) each own a hardware
+    queue but are BLOCKING streams (HIP's CU-mask streams take no flags): work
+    recorded on the legacy null stream waits for them.  Every runner call joins
+    torch's current stream first, so torch's current stream must not be the
+    null stream while replicas spin on each other."""
+    with torch.cuda.stream(torch.cuda.Stream(DEV)):
+        yield
+
+
 def _reference(world, steps, lr, nb, seed=7):
     lay = MlpLayout(MlpSpec(DIMS), 64, nb)
     P = init_params(lay, seed, "reference")
@@ -174,38 +185,6 @@ def test_two_processes_ipc(world, graph_steps, sync):
     assert err < 2e-5, err
 
 
-@pytest.mark.parametrize("algo", [0, 1])  # one-shot, two-shot
-@pytest.mark.parametrize("world,n", [(2, 262144), (3, 1000), (2, 4), (3, 1 << 20), (3, 12)])
-def test_standalone_allreduce_in_process(world, n, algo):
-    n = n // 4 * 4
-    xs = make_local_group(None, [0] * world, 5000.0, half_floats=2 << 20, ntiles=256)
-    g = torch.Generator().manual_seed(n)
-    streams = replica_streams(DEV, world)
-    for it in range(3):  # parity alternates; in-place on the last call
-        host = [torch.randn(n, generator=g) for _ in range(world)]
-        ins = [h.to(DEV) for h in host]
-        outs = [torch.empty_like(i) for i in ins]
-        torch.cuda.synchronize()
-        for r in range(world):
-            with torch.cuda.stream(streams[r]):
-                if it == 2:
-                    xs[r].allreduce_(ins[r], algo)
-                else:
-                    xs[r].allreduce(ins[r], outs[r], algo)
-        torch.cuda.synchronize()
-        assert [x.error() for x in xs] == [0] * world, f"iteration {it}: a peer timed out"
-        want = host[0].clone()
-        for h in host[1:]:
-            want = want + h  # the kernel's rank-ordered sum
-        for r in range(world):
-            got = (ins[r] if it == 2 else outs[r]).cpu()
-            bad = (got != want).nonzero().flatten()
-            assert bad.numel() == 0, (it, r, bad.numel(), bad[:4].tolist(), got[bad[:4]].tolist(),
-                                      want[bad[:4]].tolist())
-        for x in xs:
-            assert x.error() == 0
-
-
 def _ar_worker(rank, world, port, outdir, algo="oneshot"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -234,3 +213,50 @@ def test_standalone_allreduce_ipc(algo):
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["res"]
             for it in range(4):
                 assert torch.all(res[it] == float(1 + it + 2 + it))
+
+
+SIZES = (262144, 1000, 4, 1 << 20, 12)
+
+
+def _ar_values_worker(rank, world, port, outdir, algo):
+    """Every element of random inputs, sizes from 4 floats to 4 MiB, parity
+    alternating, in-place on the last call; one process per replica (the
+    production shape: one process per GPU, here all on cuda:0)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from hipdsml.parallel.xchg import XgmiAllReduce
+
+    ctx = DistContext.from_env(device="cuda", backend="gloo")
+    ar = XgmiAllReduce(ctx, max(SIZES), algo=algo, timeout_ms=5000.0)
+    out = {}
+    for n in SIZES:
+        g = torch.Generator().manual_seed(n)
+        for it in range(3):
+            host = [torch.randn(n, generator=g) for _ in range(world)]
+            x = host[rank].to(ctx.device)
+            ar(x)
+            out[f"{n}/{it}"] = x.cpu()
+    torch.cuda.synchronize()
+    ar.check()
+    torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot"])
+def test_standalone_allreduce_values_ipc(world, algo):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ar_values_worker, args=(world, _free_port(), d, algo), nprocs=world,
+                           start_method="spawn", join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for n in SIZES:
+        g = torch.Generator().manual_seed(n)
+        for it in range(3):
+            host = [torch.randn(n, generator=g) for _ in range(world)]
+            want = host[0].clone()
+            for h in host[1:]:
+                want = want + h  # the kernel's rank-ordered sum
+            for r in range(world):
+                got = res[r][f"{n}/{it}"]
+                bad = (got != want).nonzero().flatten()
+                assert bad.numel() == 0, (n, it, r, bad.numel(), bad[:4].tolist())
