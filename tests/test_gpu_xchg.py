@@ -22,15 +22,25 @@ DEV = torch.device("cuda", 0)
 DIMS = (784, 128, 64, 10)
 
 
-@pytest.fixture(autouse=True)
-def _nonblocking_current_stream():
-    """Replica streams (parallel/xchg.py replica_streams) each own a hardware
-    queue but are BLOCKING streams (HIP's CU-mask streams take no flags): work
-    recorded on the legacy null stream waits for them.  Every runner call joins
-    torch's current stream first, so torch's current stream must not be the
-    null stream while replicas spin on each other."""
+def _fresh(fn, *args):
+    """Run `fn(*args)` in a freshly spawned process.
+
+    In-process replica groups are exact in a fresh process but intermittently
+    read stale lines in a long pytest process whose caching allocator hands
+    them memory other kernels (on other queues) touched before: with per-XCD
+    L2s, a replica reading memory another queue wrote is only safe behind a
+    stream-ordered (event) hand-off, and the test groups deliberately run their
+    replicas on independent queues.  Production runs one process per GPU.
+    Exceptions in the child fail the test with the child's traceback."""
+    mp.start_processes(_fresh_entry, args=(fn, args), nprocs=1, start_method="spawn", join=True)
+
+
+def _fresh_entry(_rank, fn, args):
+    # replica streams are BLOCKING (CU-mask streams take no flags): runners join
+    # torch's current stream, which must therefore not be the legacy null stream
+    # (an event recorded there waits for every blocking stream, spinning peers too)
     with torch.cuda.stream(torch.cuda.Stream(DEV)):
-        yield
+        fn(*args)
 
 
 def _reference(world, steps, lr, nb, seed=7):
@@ -60,8 +70,7 @@ def _local_group(world, nb, graph_steps, timeout_ms=5000.0):
     return trs, xs
 
 
-@pytest.mark.parametrize("world,graph_steps", [(2, 0), (3, 0), (2, 5)])
-def test_local_group_matches_reference(world, graph_steps):
+def _case_local_group(world, graph_steps):
     nb, steps = 4, 10
     trs, xs = _local_group(world, nb, graph_steps)
     for chunk in (5, 5):
@@ -78,7 +87,12 @@ def test_local_group_matches_reference(world, graph_steps):
     assert xs[0].memory_kind in ("uncached", "finegrained", "coarse")
 
 
-def test_missing_peer_times_out_instead_of_hanging():
+@pytest.mark.parametrize("world,graph_steps", [(2, 0), (3, 0), (2, 5)])
+def test_local_group_matches_reference(world, graph_steps):
+    _fresh(_case_local_group, world, graph_steps)
+
+
+def _case_missing_peer():
     trs, xs = _local_group(2, 2, 0, timeout_ms=200.0)
     trs[0].train_steps(1)  # rank 1 never runs
     with pytest.raises(RuntimeError, match="timed out"):
@@ -86,6 +100,10 @@ def test_missing_peer_times_out_instead_of_hanging():
     xs[0].reset()
     torch.cuda.synchronize()
     assert xs[0].error() == 0
+
+
+def test_missing_peer_times_out_instead_of_hanging():
+    _fresh(_case_missing_peer)
 
 
 def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0, waves=0):
@@ -108,9 +126,7 @@ def _local_act_group(world, nb, graph_steps, timeout_ms=5000.0, waves=0):
 # process, a 4th replica stream could queue behind a spinning peer
 # 8-wave tile blocks (the form used from 4 ranks on): two replicas are the most
 # whose spinning launches (2 x 243 blocks of 512 threads) fit one GPU together
-@pytest.mark.parametrize("world,graph_steps,waves", [(2, 0, 0), (3, 0, 0), (3, 5, 0), (2, 5, 0),
-                                                    (2, 0, 8), (2, 5, 8)])
-def test_local_act_group_matches_reference(world, graph_steps, waves):
+def _case_local_act_group(world, graph_steps, waves):
     nb, steps = 4, 10
     trs, xs = _local_act_group(world, nb, graph_steps, waves=waves)
     for chunk in (5, 5):
@@ -126,7 +142,13 @@ def test_local_act_group_matches_reference(world, graph_steps, waves):
     assert err < 2e-5, err
 
 
-def test_act_exchange_missing_peer_times_out():
+@pytest.mark.parametrize("world,graph_steps,waves", [(2, 0, 0), (3, 0, 0), (3, 5, 0), (2, 5, 0),
+                                                    (2, 0, 8), (2, 5, 8)])
+def test_local_act_group_matches_reference(world, graph_steps, waves):
+    _fresh(_case_local_act_group, world, graph_steps, waves)
+
+
+def _case_act_missing_peer():
     trs, xs = _local_act_group(2, 2, 0, timeout_ms=200.0)
     P0 = trs[0].P.clone()
     trs[0].train_steps(1)  # rank 1 never pushes
@@ -137,6 +159,10 @@ def test_act_exchange_missing_peer_times_out():
     xs[0].reset()
     torch.cuda.synchronize()
     assert xs[0].error() == 0
+
+
+def test_act_exchange_missing_peer_times_out():
+    _fresh(_case_act_missing_peer)
 
 
 def _free_port():
