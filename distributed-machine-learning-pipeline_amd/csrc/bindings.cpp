@@ -507,6 +507,30 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              P.data_ptr<float>(), ws.data_ptr<float>(), slab.data_ptr<float>(),
              stats.data_ptr<float>(), cur_stream());
   });
+  // Forward on the fused kernels with the logits kept: returns a [batch x C]
+  // view into ws (ws must cover the full layout of `desc`).  The RunForward RPC.
+  m.def("mlp_forward_logits", [](const std::vector<int64_t>& desc, torch::Tensor X,
+                                 torch::Tensor labels, int64_t row0, torch::Tensor P,
+                                 torch::Tensor ws, torch::Tensor slab, torch::Tensor stats) {
+    const MlpDesc d = desc_from_list(desc);
+    check_f32(X, "X"); check_f32(P, "P"); check_f32(slab, "slab"); check_f32(stats, "stats");
+    check_f32(ws, "ws"); check_cuda(labels, "labels");
+    TORCH_CHECK(labels.scalar_type() == torch::kInt32, "labels must be int32");
+    TORCH_CHECK(X.dim() == 2 && X.size(1) % 4 == 0 && X.size(1) >= d.dims[0], "bad X");
+    TORCH_CHECK(row0 >= 0 && row0 + d.batch <= X.size(0) && row0 + d.batch <= labels.numel(),
+                "rows out of range");
+    TORCH_CHECK(P.numel() >= layout_param_end(d), "params too small");
+    TORCH_CHECK(ws.numel() >= layout_ws_end(d), "workspace too small for the layout");
+    TORCH_CHECK(stats.numel() >= 3, "stats must hold 3 floats");
+    const MlpLaunchCfg c = mlp_plan_first_layer(d);
+    TORCH_CHECK(slab.numel() >= (int64_t)c.nsplit * d.batch * d.dims[1], "slab too small");
+    TORCH_CHECK(d.lds_floats * 4 <= 160 * 1024, "model too wide for the fused row chain");
+    mlp_eval(d, X.data_ptr<float>(), X.size(1), labels.data_ptr<int32_t>(), row0,
+             P.data_ptr<float>(), ws.data_ptr<float>(), slab.data_ptr<float>(),
+             stats.data_ptr<float>(), cur_stream(), true);
+    const int C = d.dims[d.nlayers];
+    return ws.narrow(0, d.dz_off[d.nlayers], (int64_t)d.batch * C).view({d.batch, C});
+  });
 
   py::class_<PyMlpRunner>(m, "MlpRunner")
       .def(py::init<const std::vector<int64_t>&, torch::Tensor, torch::Tensor, torch::Tensor,

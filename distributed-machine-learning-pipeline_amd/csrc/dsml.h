@@ -59,7 +59,8 @@ hipError_t mlp_f32_first_layer(const float* X, int64_t ldx, const float* P, floa
                                const MlpLaunchCfg& c, const int32_t* labels, float* ws,
                                hipStream_t s);
 // Row-local chain: layer-1 epilogue, layers 2..L forward, softmax-xent,
-// activation gradients down to dZ_1.  train=0 => forward + stats only.
+// activation gradients down to dZ_1.  train=0 => forward + stats only;
+// train=2 => forward + stats, logits written to ws + dz_off[L] ([batch x C]).
 hipError_t mlp_f32_rowchain(const float* P, const float* slab, int nsplit, float* ws,
                             const int32_t* labels, int64_t* ctr, int64_t row0,
                             const MlpDesc& d, float* stats, int train, float inv_batch,

@@ -302,7 +302,8 @@ __global__ __launch_bounds__(256) void mlp_f32_rowchain_k(
           const float p = expf(Z[r * sL + c] - mx) * inv;
           if (c == y) loss = -logf(p + 1e-10f);
           g = (p - (c == y ? 1.f : 0.f)) * inv_batch;
-          if (train) Gg[(int64_t)m * C + c] = g;
+          if (train == 1) Gg[(int64_t)m * C + c] = g;
+          else if (train == 2) Gg[(int64_t)m * C + c] = Z[r * sL + c];  // logits out
         }
         G[r * sL + c] = g;
       }
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(256) void mlp_f32_rowchain_k(
       }
     }
   }
-  if (!train) return;
+  if (train != 1) return;
   __syncthreads();
   DSML_STAMP(3);
 

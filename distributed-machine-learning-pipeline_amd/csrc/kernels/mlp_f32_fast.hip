@@ -233,7 +233,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (cv && valid) {
       g = (p - (c == y ? 1.f : 0.f)) * inv_batch;
       if (c == y) loss = -logf(p + 1e-10f);
-      if (train) G3g[(int64_t)m * D3 + c] = g;
+      if (train == 1) G3g[(int64_t)m * D3 + c] = g;
+      else if (train == 2) G3g[(int64_t)m * D3 + c] = z;  // logits out (RunForward)
     }
     lds[Lay::DZ3 + r * Lay::S3 + c] = g;
     float correct = (c == 0 && valid && amax == y) ? 1.f : 0.f;
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       atomicAdd(stats + 2, cnt);
     }
   }
-  if (!train) return;
+  if (train != 1) return;
   lds_barrier();
   FAST_STAMP(4);
 

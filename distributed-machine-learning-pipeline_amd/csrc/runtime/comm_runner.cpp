@@ -366,11 +366,11 @@ void MlpRunner::replay(hipStream_t s, int steps) {
 }
 
 void mlp_eval(const MlpDesc& d, const float* X, int64_t ldx, const int32_t* labels, int64_t row0,
-              const float* P, float* ws, float* slab, float* stats, hipStream_t s) {
+              const float* P, float* ws, float* slab, float* stats, hipStream_t s, bool logits) {
   const MlpLaunchCfg c = mlp_plan_first_layer(d);
   DSML_HIP_CHECK(mlp_f32_first_layer(X, ldx, P, slab, nullptr, row0, d, c, labels, ws, s));
-  DSML_HIP_CHECK(
-      mlp_f32_rowchain(P, slab, c.nsplit, ws, labels, nullptr, row0, d, stats, 0, 1.0f, s));
+  DSML_HIP_CHECK(mlp_f32_rowchain(P, slab, c.nsplit, ws, labels, nullptr, row0, d, stats,
+                                  logits ? 2 : 0, 1.0f, s));
 }
 
 }  // namespace dsml

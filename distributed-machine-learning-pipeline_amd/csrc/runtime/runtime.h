@@ -320,7 +320,9 @@ class MlpRunner {
 };
 
 // Forward-only evaluation over `rows` resident rows (one launch pair).
+// logits != 0: also writes the logits to ws + dz_off[L] (ws sized for d).
 void mlp_eval(const MlpDesc& d, const float* X, int64_t ldx, const int32_t* labels,
-              int64_t row0, const float* P, float* ws, float* slab, float* stats, hipStream_t s);
+              int64_t row0, const float* P, float* ws, float* slab, float* stats, hipStream_t s,
+              bool logits = false);
 
 }  // namespace dsml

@@ -80,6 +80,25 @@ def build_trainer(cfg: TrainConfig, spec: MlpSpec, data: Dataset, ctx: DistConte
                       ring_chunk_bytes=cfg.ring_chunk_bytes, graph_steps=gs), engine
 
 
+def _fault_hook(ctx: DistContext, step: int) -> None:
+    """Fault injection for failure-detection tests (BASELINE config 5):
+    HIPDSML_FAULT="rank:step:mode" makes `rank` die (mode exit) or stall
+    forever (mode hang) once it has run `step` steps."""
+    spec = os.environ.get("HIPDSML_FAULT", "")
+    if not spec:
+        return
+    r, s, mode = spec.split(":")
+    if int(r) != ctx.rank or step < int(s):
+        return
+    print(f"[fault injection] rank {ctx.rank}: {mode} at step {step}", flush=True)
+    if mode == "exit":
+        os._exit(13)
+    if mode == "hang":
+        while True:
+            time.sleep(3600)
+    raise ValueError(f"unknown fault mode {mode!r}")
+
+
 def run(cfg: TrainConfig, out=print) -> Dict[str, Any]:
     if cfg.trace:
         trace.enable(True)
@@ -127,6 +146,7 @@ def _run(cfg: TrainConfig, ctx: DistContext, out) -> Dict[str, Any]:
             nxt = min(nxt, (s // every_ckpt + 1) * every_ckpt)
         with trace.trace_range(f"train_steps[{s}:{nxt}]"):
             tr.train_steps(nxt - s)
+        _fault_hook(ctx, tr.steps_done)
         at_epoch = tr.steps_done % per_epoch == 0
         at_log = tr.steps_done % chunk == 0 or at_epoch or tr.steps_done == total
         if at_log:

@@ -390,15 +390,18 @@ class MlpTrainer:
         self.steps_done += n
 
     def synchronize(self) -> None:
-        if self.runner is not None:
-            self.runner.join_into_torch()  # torch reads P / stats after the runner (event edge)
-            self.runner.synchronize()
-            if self.xchg is not None:
-                from ..parallel.xchg import check
+        """Wait for every enqueued step; raises if a peer timed out / faulted
+        (the wait runs under the job's watchdog, parallel/watchdog.py)."""
+        with self.ctx.guard("synchronize"):
+            if self.runner is not None:
+                self.runner.join_into_torch()  # torch reads P / stats after the runner (event edge)
+                self.runner.synchronize()
+                if self.xchg is not None:
+                    from ..parallel.xchg import check
 
-                check(self.xchg)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+                    check(self.xchg)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         if self.backend == "torch":
@@ -442,6 +445,38 @@ class MlpTrainer:
         return {"loss": loss / max(n, 1), "accuracy": 100.0 * correct / max(n, 1), "n": n}
 
     # ------------------------------------------------- per-batch RPC helpers --
+    @torch.no_grad()
+    def forward_logits(self, X: torch.Tensor, y: Optional[torch.Tensor] = None):
+        """Logits of rows X at the current params, plus (loss_sum, correct)
+        when labels are given — the RunForward RPC.  GPU: the fused HIP
+        forward kernels (K_A + the row chain in logits mode); CPU: torch."""
+        rows = X.shape[0]
+        if self.backend == "torch":
+            logits, _ = forward_ref(self.layout, self.P, X.to(self.P.device, torch.float32))
+            if y is None:
+                return logits, 0.0, 0
+            p = torch.softmax(logits, 1)
+            yl = y.to(logits.device).long()
+            loss = (-torch.log(p.gather(1, yl.view(-1, 1)).squeeze(1) + 1e-10)).sum().item()
+            return logits, loss, int((logits.argmax(1) == yl).sum().item())
+        from ..ops.native import require_native
+
+        C = require_native()
+        lay = MlpLayout(self.spec, rows, 1)
+        Xd = _pad_cols(X.to(self.device, torch.float32))
+        yd = (y.to(self.device, torch.int32) if y is not None
+              else torch.zeros(rows, dtype=torch.int32, device=self.device)).contiguous()
+        ws = torch.zeros(lay.ws_floats, dtype=torch.float32, device=self.device)
+        slab = torch.empty(lay.slab_floats(), dtype=torch.float32, device=self.device)
+        stats = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.synchronize()
+        logits = C.mlp_forward_logits(lay.desc_list(), Xd, yd, 0, self.P, ws, slab, stats).clone()
+        torch.cuda.synchronize(self.device)
+        if y is None:
+            return logits, 0.0, 0
+        loss, correct, _ = stats[:3].tolist()
+        return logits, loss, int(correct)
+
     def batch_gradients(self, X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         """Flat gradient (param layout) of one batch at the current params —
         the RunBackward RPC.  GPU: the fused HIP kernels on a one-batch plan."""
@@ -490,7 +525,8 @@ class MlpTrainer:
         if self.ctx.is_distributed:
             import torch.distributed as dist
 
-            dist.all_reduce(g)
+            with self.ctx.guard("gradient all_reduce"):
+                dist.all_reduce(g)
         if self.momentum or self.weight_decay:
             gg = g / world + self.weight_decay * self.P
             self.V.mul_(self.momentum).add_(gg)

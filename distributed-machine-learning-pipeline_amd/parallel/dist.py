@@ -9,6 +9,7 @@ native RCCL communicator (``hipdsml._C.RcclComm``) is bootstrapped by sharing an
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 from dataclasses import dataclass
@@ -16,6 +17,8 @@ from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+from .watchdog import Watchdog, timeout_from_env
 
 
 @dataclass
@@ -26,6 +29,7 @@ class DistContext:
     backend: str = "none"
     device: torch.device = torch.device("cpu")
     initialized_here: bool = False
+    watchdog: Optional[Watchdog] = None
 
     @property
     def is_distributed(self) -> bool:
@@ -33,7 +37,13 @@ class DistContext:
 
     @classmethod
     def from_env(cls, device: str = "auto", backend: Optional[str] = None,
-                 timeout_s: float = 600.0, device_index: Optional[int] = None) -> "DistContext":
+                 timeout_s: Optional[float] = None, device_index: Optional[int] = None,
+                 watchdog_s: Optional[float] = None) -> "DistContext":
+        """Process group from the torchrun environment.  N > 1 also starts the
+        data-plane watchdog (parallel/watchdog.py; HIPDSML_WATCHDOG_S, default
+        300 s, 0 disables); HIPDSML_PG_TIMEOUT_S sets the process-group timeout."""
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("HIPDSML_PG_TIMEOUT_S", "600"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -59,7 +69,17 @@ class DistContext:
                 dist.init_process_group(**kw)
                 ctx.initialized_here = True
             ctx.backend = dist.get_backend()
+            wd = timeout_from_env() if watchdog_s is None else watchdog_s
+            if wd > 0:
+                grace = float(os.environ.get("HIPDSML_WATCHDOG_GRACE_S", "10"))
+                ctx.watchdog = Watchdog(wd, grace=grace, name=f"[rank {rank}]")
         return ctx
+
+    def guard(self, what: str):
+        """Blocking section under the watchdog (no-op without one)."""
+        if self.watchdog is None:
+            return contextlib.nullcontext()
+        return self.watchdog.guard(what)
 
     # -- collectives on small host/device tensors (outside timed regions) ----
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
@@ -67,7 +87,10 @@ class DistContext:
             return t
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                "min": dist.ReduceOp.MIN, "prod": dist.ReduceOp.PRODUCT}[op]
-        dist.all_reduce(t, op=rop)
+        with self.guard("all_reduce"):
+            dist.all_reduce(t, op=rop)
+            if t.is_cuda:
+                torch.cuda.synchronize(t.device)
         return t
 
     def all_reduce_scalars(self, *vals: float, op: str = "sum") -> list:
@@ -78,10 +101,12 @@ class DistContext:
 
     def barrier(self) -> None:
         if self.is_distributed:
-            if self.device.type == "cuda" and self.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
-            else:
-                dist.barrier()
+            with self.guard("barrier"):
+                if self.device.type == "cuda" and self.backend == "nccl":
+                    dist.barrier(device_ids=[self.device.index])
+                    torch.cuda.synchronize(self.device)
+                else:
+                    dist.barrier()
 
     def share_bytes(self, key: str, value: Optional[bytes]) -> bytes:
         """Rank 0 publishes `value` under `key` in the TCP store; every rank reads it."""
@@ -92,7 +117,8 @@ class DistContext:
         if self.rank == 0:
             assert value is not None
             store.set(key, value)
-        return bytes(store.get(key))
+        with self.guard(f"store.get {key}"):
+            return bytes(store.get(key))
 
     def all_gather_bytes(self, key: str, value: bytes) -> list:
         """Every rank publishes `value`; returns all ranks' values in rank order."""
@@ -100,19 +126,27 @@ class DistContext:
             return [value]
         store = dist.distributed_c10d._get_default_store()
         store.set(f"{key}/{self.rank}", value)
-        return [bytes(store.get(f"{key}/{r}")) for r in range(self.world_size)]
+        with self.guard(f"store.get {key}"):
+            return [bytes(store.get(f"{key}/{r}")) for r in range(self.world_size)]
 
     def destroy(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
         if self.initialized_here and dist.is_initialized():
-            dist.destroy_process_group()
+            if self.watchdog is None or self.watchdog.fault is None:
+                dist.destroy_process_group()  # a faulted group may not shut down cleanly
             self.initialized_here = False
 
 
 _uid_counter = 0
 
 
-def make_native_comm(ctx: DistContext, blocking: bool = True):
-    """Bootstrap a native RCCL communicator over the process group's store."""
+def make_native_comm(ctx: DistContext, blocking: bool = False):
+    """Bootstrap a native RCCL communicator over the process group's store.
+
+    Non-blocking by default (``ncclConfig_t.blocking = 0``): no RCCL host call
+    can wait unboundedly on a dead peer, and the context's watchdog polls the
+    communicator's async error and aborts it on a fault (parallel/watchdog.py)."""
     from ..ops.native import require_native
 
     global _uid_counter
@@ -121,4 +155,8 @@ def make_native_comm(ctx: DistContext, blocking: bool = True):
     key = f"hipdsml/rccl_uid/{_uid_counter}"
     uid = C.rccl_unique_id() if ctx.rank == 0 else None
     uid = ctx.share_bytes(key, uid)
-    return C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.device.index, blocking)
+    with ctx.guard("ncclCommInitRank"):
+        comm = C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.device.index, blocking)
+    if ctx.watchdog is not None:
+        ctx.watchdog.watch_comm(comm)
+    return comm

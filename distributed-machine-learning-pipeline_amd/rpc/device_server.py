@@ -230,7 +230,10 @@ class GPUDeviceServicer:
 
             C = require_native()
             try:
-                comm = C.RcclComm(request.uniqueId, request.rank, request.nranks, self.dev.gpu, True)
+                # non-blocking: no RCCL host call waits unboundedly on a dead
+                # peer; the coordinator's Abort fan-out (ncclCommAbort) makes
+                # in-flight RCCL kernels return
+                comm = C.RcclComm(request.uniqueId, request.rank, request.nranks, self.dev.gpu, False)
             except Exception as e:  # init failure (peer died during bootstrap)
                 context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
             self.comms[cid] = comm
@@ -392,6 +395,11 @@ class GPUDeviceServicer:
                 torch.cuda.synchronize(self.dev.gpu)
         except Exception as e:
             context.abort(grpc.StatusCode.INTERNAL, f"all-reduce failed: {e}")
+        if comm.aborted:  # an Abort landed mid-collective: the kernels returned early
+            context.abort(grpc.StatusCode.ABORTED, "communicator aborted during the all-reduce")
+        err = comm.async_error()
+        if err not in ("", "in-progress"):
+            context.abort(grpc.StatusCode.INTERNAL, f"RCCL error: {err}")
         us = (time.perf_counter() - t0) * 1e6 / reps
         self.counters["allreduces"] += reps
         return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
@@ -499,8 +507,6 @@ class GPUDeviceServicer:
         return pb.EvaluateResponse(success=True, accuracy=ev["accuracy"], loss=ev["loss"], count=ev["n"])
 
     def RunForward(self, request, context):
-        from ..models.mlp import forward_ref, loss_and_dlogits_ref
-
         tr = self._need_trainer(context)
         rows = request.numRows or tr.batch
         d0 = tr.spec.dims[0]
@@ -512,10 +518,11 @@ class GPUDeviceServicer:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         X = X.clone()
         y = y.clone() if y is not None else None
-        logits, _ = forward_ref(tr.layout, tr.P, X)
+        # GPU: the fused HIP forward kernels (K_A + row chain, logits kept);
+        # host devices: the fp32 torch reference
+        logits, loss_sum, corr = tr.forward_logits(X, y)
         loss = correct = 0.0
         if y is not None:
-            loss_sum, _, corr = loss_and_dlogits_ref(logits, y)
             loss, correct = float(loss_sum) / rows, int(corr)
         if request.outputAddr:
             self.dev.write(request.outputAddr, logits.detach().float().cpu().numpy().tobytes(),

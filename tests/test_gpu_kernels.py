@@ -221,6 +221,21 @@ def test_rccl_collectives_captured_in_graph(blocking):
     assert comm.async_error() == ""
 
 
+def test_rccl_abort_with_collective_enqueued():
+    """ncclCommAbort while a collective is still queued behind other work:
+    nothing hangs, the comm reports aborted and refuses further calls."""
+    C = require_native()
+    comm = C.RcclComm(C.rccl_unique_id(), 0, 1, 0, False)
+    t = torch.ones(1 << 20, device=DEV)
+    torch.cuda._sleep(20_000_000)  # GPU busy ahead of the collective
+    comm.allreduce_(t, 0)
+    comm.abort()
+    torch.cuda.synchronize()
+    assert comm.aborted and comm.async_error() == "aborted"
+    with pytest.raises(RuntimeError, match="aborted"):
+        comm.allreduce_(t, 0)
+
+
 def test_trainer_graph_sizes_cover_any_step_count():
     """train_steps(n) replays a G-step and an r-step graph for n = q*G + r
     (no eager fallback), bit-identical to eager launches."""

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from hipdsml.data.mnist import synthetic_mnist
-from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
+from hipdsml.models.mlp import MlpLayout, MlpSpec, forward_ref, grads_ref, init_params
 from hipdsml.rpc.proto import DT_BFLOAT16, DT_FLOAT32, pb
 
 from cluster_util import cluster, d2h, h2d
@@ -61,9 +61,14 @@ def test_hip_device_forward_backward_apply():
         svc.dev.write(0x100000, ds.X.numpy().tobytes())
         svc.dev.write(0x200000, ds.y.numpy().astype(np.int32).tobytes())
         f = stub.RunForward(pb.RunForwardRequest(deviceId=1, inputAddr=0x100000, numRows=64,
-                                                 labelsAddr=0x200000))
+                                                 labelsAddr=0x200000, outputAddr=0x300000))
         g, loss_sum, corr = grads_ref(lay, P0, ds.X, ds.y)
         assert abs(f.loss - float(loss_sum) / 64) < 1e-4 and f.correct == int(corr)
+        # logits come from the fused HIP forward kernels: fp32 torch reference to 1e-5
+        want, _ = forward_ref(lay, P0, ds.X)
+        got_l = torch.frombuffer(bytearray(svc.dev.read(0x300000, 64 * 10 * 4)),
+                                 dtype=torch.float32).view(64, 10)
+        assert (got_l - want).abs().max().item() < 1e-5
         b = stub.RunBackward(pb.RunBackwardRequest(deviceId=1, gradientAddr=0x1000))
         assert b.numBytes == lay.nparams * 4
         got = torch.frombuffer(bytearray(svc.dev.read(0x1000, b.numBytes)), dtype=torch.float32)
