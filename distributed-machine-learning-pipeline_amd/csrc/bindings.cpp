@@ -197,7 +197,7 @@ struct PyMlpRunner {
   }
   void step(int n) {
     join_torch();
-    for (int i = 0; i < n; ++i) r->enqueue_step(stream);
+    r->enqueue_steps(n, stream);
   }
   void fwd_bwd() { join_torch(); r->enqueue_fwd_bwd(stream); }
   void update() { join_torch(); r->enqueue_update(stream); }
@@ -484,6 +484,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     hip_ok(mlp_read_stamps_fast(v.data()), "mlp_read_stamps_fast");
     return v;
   });
+  m.def("mlp_persist_supported", [](const std::vector<int64_t>& desc) {
+    return mlp_persist_supported(desc_from_list(desc));
+  });
+  m.def("mlp_persist_xbuf_granules", []() { return mlp_persist_xbuf_granules(); });
   m.def("mlp_plan", [](const std::vector<int64_t>& desc) {
     const MlpDesc d = desc_from_list(desc);
     const MlpLaunchCfg c = mlp_plan_first_layer(d);
@@ -566,6 +570,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         s.r->set_act_exchange(x, Xall.data_ptr<float>(), xstride, waves);
       }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"), py::arg("waves") = 0,
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("set_persist", [](PyMlpRunner& s, c10::optional<torch::Tensor> xbuf,
+                             c10::optional<torch::Tensor> err, double timeout_ms) {
+        if (!xbuf) { s.r->set_persist(nullptr, nullptr, 0.0); return; }
+        check_cuda(*xbuf, "xbuf");
+        TORCH_CHECK(xbuf->scalar_type() == torch::kInt64 &&
+                    xbuf->numel() >= mlp_persist_xbuf_granules(), "xbuf: int64[",
+                    mlp_persist_xbuf_granules(), "]");
+        TORCH_CHECK(err && err->is_cuda() && err->scalar_type() == torch::kInt32 && err->numel() >= 1,
+                    "err: int32[1] on the GPU");
+        s.keep.push_back(*xbuf);
+        s.keep.push_back(*err);
+        s.r->set_persist(reinterpret_cast<uint64_t*>(xbuf->data_ptr<int64_t>()),
+                         reinterpret_cast<uint32_t*>(err->data_ptr<int32_t>()), timeout_ms);
+      }, py::arg("xbuf").none(true), py::arg("err") = py::none(), py::arg("timeout_ms") = 2000.0)
+      .def("persist_active", [](PyMlpRunner& s) { return s.r->persist_active(); })
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
       .def("exchange_mode", [](PyMlpRunner& s) { return s.r->exchange_mode(); })
       .def("plan", [](PyMlpRunner& s) {

@@ -83,6 +83,18 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
                          int64_t* ctr, int64_t row0, const MlpDesc& d, float lr, int fused_sgd,
                          hipStream_t s);
 
+// ---- persistent fused step (kernels/mlp_persist.hip) -------------------------
+// One launch runs `steps` SGD steps of the 784-128-64-10 MLP at batch 64 with
+// the weights resident on chip (36 workgroups: 32 layer-1 tiles + 4 row
+// chains, tagged-granule hand-offs).  `xb` holds mlp_persist_xbuf_granules()
+// uint64 granules, zeroed whenever the step counter is rewound; `err` is set
+// when a hand-off timed out (the launch then ends early).
+bool mlp_persist_supported(const MlpDesc& d);
+int64_t mlp_persist_xbuf_granules();
+hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
+                             int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
+                             float* stats, uint32_t* err, uint64_t timeout_ticks, hipStream_t s);
+
 // ---- peer exchange: gradient all-reduce fused into K_C over xGMI -------------
 // Every replica's K_C publishes each weight-gradient tile into its own
 // exchange buffer (IPC-shared with the peers, uncached), raises a per-tile

@@ -1,0 +1,678 @@
+// Persistent fused training kernel for the flagship MLP 784-128-64-10 (fp32,
+// batch 64 per replica): ONE launch runs S consecutive SGD steps with every
+// weight resident on chip, replacing the three launches per step of
+// mlp_f32.hip (K_A split-K layer 1, K_B row chain, K_C weight gradients).
+//
+// Reference hot loop replaced: client.go:596-647 (forwardPass :112-141,
+// backwardPass :143-202, updateWeights :254-267), 937 x 10 times on the CPU.
+//
+// Why: at B = 64 a step is ~29 MFLOP, i.e. well under a microsecond of MFMA
+// work spread over tens of CUs; the three-launch step costs ~18-21 us, almost
+// all of it kernel boundaries, per-launch weight reloads and dependent memory
+// round trips.  Here a step is two on-chip hand-offs between resident roles.
+//
+// Roles (36 workgroups x 256 threads, one per CU; residency is trivially met):
+//
+//  * 32 layer-1 blocks (gn, gk), gn < 8, gk < 4, own W1[16 gn .. +16][196 gk
+//    .. +196] (and b1[16 gn ..] when gk == 0) in LDS for the whole launch.
+//    Per step: Z1 partial [64 x 16] = X[:, k slice] . W1 tile^T (MFMA
+//    16x16x4 f32), published as tagged granules; then, once the chain blocks
+//    have published dZ1, dW1 tile = dZ1[:, n slice]^T . X[:, k slice] and the
+//    SGD update in LDS.  The next step's X slice is prefetched into registers
+//    while the block waits.
+//  * 4 chain blocks c own batch rows 16c .. 16c+15 and a full copy of W2, b2,
+//    W3, b3 in LDS.  Per step: H1 = relu(sum of the 4 k-partials), layer 2 and
+//    3 forward, softmax + cross-entropy (eps 1e-10, client.go:151), dZ3 =
+//    (p - y)/B, dZ2 = dZ3 W3 * (H2 > 0), dZ1 = dZ2 W2 * (H1 > 0) published to
+//    the layer-1 blocks (the critical path ends here).  Off the critical path
+//    the chains exchange their rows of H1, H2, dZ2, dZ3, and every chain
+//    computes the full-batch dW2, db2, dW3, db3 in the same order, so the four
+//    copies of W2 / W3 stay bit-identical without a broadcast.
+//
+// Hand-offs are data-tagged 8-byte granules {fp32 value, step tag} written by
+// single write-through (sc1) stores and read with sc1 loads until every tag
+// matches: no flags, no fences, no barriers across workgroups (MI355X
+// microarch: an 8-B granule is never torn; sc1 loads/stores keep the hand-off
+// coherent across XCDs).  Tags are the global step number + 1, so buffers
+// need zeroing only when the step counter is rewound (host side).
+//
+// Every wait is bounded (timeout -> error word, checked by the host after the
+// launch) and gives up at once when another block already timed out, so a
+// fault ends the launch instead of hanging the GPU.
+#include "common.h"
+#include "../dsml.h"
+
+namespace dsml {
+
+namespace {
+
+constexpr int kD0 = 784, kD1 = 128, kD2 = 64, kD3 = 10, kB = 64;
+constexpr int kGN = 8, kGK = 4, kKC = kD0 / kGK;  // 196 k per layer-1 block
+constexpr int kNL1 = kGN * kGK;                   // 32 layer-1 blocks
+constexpr int kNCH = 4;                           // chain blocks (16 rows each)
+constexpr int kThreads = 256;
+static_assert(kKC % 4 == 0, "k slice must hold whole MFMA k-steps");
+
+// ---- LDS layouts (floats) ----------------------------------------------------
+constexpr int kXS = kKC + 16;              // X / W1 tile row stride (2-way conflicts at most)
+struct L1Lay {
+  static constexpr int X0 = 0;                       // X tile, buffer 0 [64][kXS]
+  static constexpr int X1 = X0 + kB * kXS;           // buffer 1
+  static constexpr int W = X1 + kB * kXS;            // W1 tile [16][kXS]
+  static constexpr int DZ = W + 16 * kXS;            // dZ1 tile [64][17]
+  static constexpr int B1 = DZ + kB * 17;            // b1 slice [16]
+  static constexpr int TOTAL = B1 + 16;
+};
+constexpr int kS1 = kD1 + 4, kS2 = kD2 + 4, kS3 = 16 + 4;
+struct ChLay {
+  static constexpr int W2 = 0;                       // [64][kS1]
+  static constexpr int W3 = W2 + kD2 * kS1;          // [16][kS2] rows >= 10 zero
+  static constexpr int B2 = W3 + 16 * kS2;           // [64]
+  static constexpr int B3 = B2 + kD2;                // [16]
+  static constexpr int H1 = B3 + 16;                 // all rows [64][kS1]
+  static constexpr int H2 = H1 + kB * kS1;           // [64][kS2]
+  static constexpr int DZ2 = H2 + kB * kS2;          // [64][kS2]
+  static constexpr int DZ3 = DZ2 + kB * kS2;         // [64][kS3] cols >= 10 zero
+  static constexpr int RED = DZ3 + kB * kS3;         // [4][16][16] layer-3 partials
+  static constexpr int TOTAL = RED + 4 * 256;
+};
+constexpr int kLdsFloats = L1Lay::TOTAL > ChLay::TOTAL ? L1Lay::TOTAL : ChLay::TOTAL;
+static_assert(kLdsFloats * 4 <= 160 * 1024, "LDS budget");
+
+// ---- exchange buffer layout (8-byte granules) -----------------------------------
+// PART[32][64][16]   layer-1 partials (b1 added by gk == 0 blocks)
+// DZ1 [64][128]      activation gradient of layer 1
+// CX  [2][4][kCXG]   chain exchange (parity by step): H1 rows [16][128],
+//                    H2 rows [16][64], dZ2 rows [16][64], dZ3 rows [16][16]
+constexpr int kPartG = kNL1 * kB * 16;
+constexpr int kDz1G = kB * kD1;
+constexpr int kCXG = 16 * kD1 + 16 * kD2 + 16 * kD2 + 16 * 16;  // 4352
+constexpr int64_t kOffPart = 0, kOffDz1 = kOffPart + kPartG, kOffCx = kOffDz1 + kDz1G;
+constexpr int64_t kTotalG = kOffCx + 2 * kNCH * kCXG;
+
+constexpr int kSc1 = 16;  // buffer aux: sc1 (write-through store / L1-bypassing load)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint2 gran(float v, uint32_t tag) {
+  return make_uint2(__float_as_uint(v), tag);
+}
+// One granule, one 8-byte write-through store.
+__device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t r, int64_t g, float v, uint32_t tag) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const uint2 x = gran(v, tag);
+  u2 w = {x.x, x.y};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)(g * 8), 0, kSc1);
+}
+// Two adjacent granules (16 B, 16-B aligned), one load.
+__device__ __forceinline__ uint4 ld_gran2(__amdgpu_buffer_rsrc_t r, int64_t g) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(g * 8), 0, kSc1);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+struct Poll {
+  uint32_t* err;
+  uint64_t timeout;
+  uint64_t t0;
+  uint32_t spins;
+  __device__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); spins = 0; }
+  // true: keep waiting; false: give up (timeout, or another block gave up)
+  __device__ bool again() {
+    if ((++spins & 31u) == 0u &&
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    return true;
+  }
+};
+
+__device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+struct PersistArgs {
+  const float* X;
+  int64_t ldx;
+  const int32_t* labels;
+  float* P;
+  int64_t w_off[3], b_off[3];
+  int64_t* ctr;
+  int32_t nbatches;
+  int32_t steps;
+  float lr;
+  float inv_batch;
+  uint64_t* xb;  // exchange granules (kTotalG)
+  float* stats;
+  uint32_t* err;
+  uint64_t timeout_ticks;
+};
+
+// -----------------------------------------------------------------------------
+// Layer-1 block
+// -----------------------------------------------------------------------------
+__device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int lb) {
+  const int gn = lb % kGN, gk = lb / kGN;
+  const int n0 = gn * 16, k0 = gk * kKC;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  float* Wl = lds + L1Lay::W;
+  float* Dz = lds + L1Lay::DZ;
+  float* B1 = lds + L1Lay::B1;
+
+  // ---- prologue: W1 tile, b1 slice, X of the first step ----
+  const float* W1g = a.P + a.w_off[0];
+  for (int e = tid; e < 16 * (kKC / 4); e += kThreads) {
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    *reinterpret_cast<float4*>(Wl + r * kXS + 4 * c4) =
+        *reinterpret_cast<const float4*>(W1g + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4);
+  }
+  if (tid < 16) B1[tid] = gk == 0 ? a.P[a.b_off[0] + n0 + tid] : 0.f;
+  constexpr int kXF4 = kB * (kKC / 4);                 // float4 of one X tile (3136)
+  constexpr int kXPer = (kXF4 + kThreads - 1) / kThreads;  // 13
+  float4 xr[kXPer];
+  auto load_x = [&](uint64_t s) {
+    const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * kB;
+#pragma unroll
+    for (int j = 0; j < kXPer; ++j) {
+      const int e = tid + j * kThreads;
+      const int ec = e < kXF4 ? e : kXF4 - 1;
+      const int r = ec / (kKC / 4), c4 = ec - r * (kKC / 4);
+      xr[j] = *reinterpret_cast<const float4*>(a.X + (r0 + r) * a.ldx + k0 + 4 * c4);
+    }
+  };
+  auto store_x = [&](int buf) {
+    float* Xl = lds + (buf ? L1Lay::X1 : L1Lay::X0);
+#pragma unroll
+    for (int j = 0; j < kXPer; ++j) {
+      const int e = tid + j * kThreads;
+      if (e < kXF4) {
+        const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+        *reinterpret_cast<float4*>(Xl + r * kXS + 4 * c4) = xr[j];
+      }
+    }
+  };
+  load_x(s0);
+  store_x(0);
+  if (a.steps > 1) load_x(s0 + 1);
+  __syncthreads();
+
+  bool ok = true;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);
+    const int buf = it & 1;
+    const float* Xl = lds + (buf ? L1Lay::X1 : L1Lay::X0);
+
+    // ---- forward partial: wave w -> rows 16w..16w+15, all 16 n of the tile ----
+    {
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const float* xa = Xl + (16 * w + i) * kXS + q;
+      const float* wa = Wl + i * kXS + q;
+#pragma unroll 7
+      for (int ks = 0; ks < kKC / 4; ks += 2) {
+        acc0 = mfma_f32_16x16x4(xa[4 * ks], wa[4 * ks], acc0);
+        if (ks + 1 < kKC / 4) acc1 = mfma_f32_16x16x4(xa[4 * ks + 4], wa[4 * ks + 4], acc1);
+      }
+      const float bn = B1[i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * w + 4 * q + r;
+        st_gran(rb, kOffPart + ((int64_t)lb * kB + m) * 16 + i, acc0[r] + acc1[r] + bn, tag);
+      }
+    }
+    // next step's X: registers -> the other LDS buffer (its last reader, the
+    // previous step's backward, finished before the barrier that ended it)
+    if (it + 1 < a.steps) store_x(buf ^ 1);
+    if (it + 2 < a.steps) load_x(s + 2);
+
+    // ---- wait for dZ1[:, n0 .. n0+15] of this step (4 chain blocks) ----
+    {
+      const int m = tid >> 2, qq = tid & 3;
+      const int64_t g = kOffDz1 + (int64_t)m * kD1 + n0 + 4 * qq;
+      uint4 v0, v1;
+      poll.start();
+      for (;;) {
+        v0 = ld_gran2(rb, g);
+        v1 = ld_gran2(rb, g + 2);
+        if (v0.y == tag && v0.w == tag && v1.y == tag && v1.w == tag) break;
+        if (!poll.again()) { ok = false; break; }
+      }
+      Dz[m * 17 + 4 * qq + 0] = __uint_as_float(v0.x);
+      Dz[m * 17 + 4 * qq + 1] = __uint_as_float(v0.z);
+      Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
+      Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
+    }
+    if (lb == 0 && it + 1 == a.steps && tid == 0) {
+      // every block has started (all chains published this step's dZ1, which
+      // needed every layer-1 block's partial): hand the step counter on
+      const uint64_t e = s0 + (uint64_t)a.steps;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr + 1), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (!ok) break;
+
+    // ---- backward: dW1 tile [16 n][196 k] = dZ1^T . X, SGD in LDS ----
+    // wave w: k tiles kt = w, w + 4, w + 8, w + 12 (13 tiles of 16, the last 4 wide)
+    f32x4 g[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kt = w + 4 * t;
+      if (kt * 16 < kKC) {
+        const int kc = kt * 16 + i;
+        const int kcc = kc < kKC ? kc : kKC - 1;
+#pragma unroll
+        for (int ms = 0; ms < kB / 4; ++ms) {
+          const int m = 4 * ms + q;
+          g[t] = mfma_f32_16x16x4(Dz[m * 17 + i], Xl[m * kXS + kcc], g[t]);
+        }
+      }
+    }
+    float db = 0.f;
+    if (gk == 0 && tid < 16) {
+#pragma unroll 8
+      for (int m = 0; m < kB; ++m) db += Dz[m * 17 + tid];
+    }
+    // every wave read this step's W1 tile in the forward, before the barrier above
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kt = w + 4 * t;
+      const int kc = kt * 16 + i;
+      if (kt * 16 < kKC && kc < kKC) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Wl[(4 * q + r) * kXS + kc] -= a.lr * g[t][r];
+      }
+    }
+    if (gk == 0 && tid < 16) B1[tid] -= a.lr * db;
+    __syncthreads();
+  }
+
+  // ---- epilogue: the resident weights back to HBM ----
+  float* W1w = a.P + a.w_off[0];
+  for (int e = tid; e < 16 * (kKC / 4); e += kThreads) {
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    *reinterpret_cast<float4*>(W1w + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4) =
+        *reinterpret_cast<const float4*>(Wl + r * kXS + 4 * c4);
+  }
+  if (gk == 0 && tid < 16) a.P[a.b_off[0] + n0 + tid] = B1[tid];
+}
+
+// -----------------------------------------------------------------------------
+// Chain block
+// -----------------------------------------------------------------------------
+__device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int rb0 = 16 * c;  // first batch row of this chain
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  float* W2 = lds + ChLay::W2;
+  float* W3 = lds + ChLay::W3;
+  float* B2 = lds + ChLay::B2;
+  float* B3 = lds + ChLay::B3;
+  float* H1 = lds + ChLay::H1;
+  float* H2 = lds + ChLay::H2;
+  float* DZ2 = lds + ChLay::DZ2;
+  float* DZ3 = lds + ChLay::DZ3;
+  float* RED = lds + ChLay::RED;
+
+  // ---- prologue: W2, W3 (rows padded to 16 with zeros), b2, b3 ----
+  for (int e = tid; e < kD2 * (kD1 / 4); e += kThreads) {
+    const int r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
+    *reinterpret_cast<float4*>(W2 + r * kS1 + 4 * c4) =
+        *reinterpret_cast<const float4*>(a.P + a.w_off[1] + (int64_t)r * kD1 + 4 * c4);
+  }
+  for (int e = tid; e < 16 * kD2; e += kThreads) {
+    const int r = e / kD2, col = e - r * kD2;
+    W3[r * kS2 + col] = r < kD3 ? a.P[a.w_off[2] + (int64_t)r * kD2 + col] : 0.f;
+  }
+  if (tid < kD2) B2[tid] = a.P[a.b_off[1] + tid];
+  if (tid < 16) B3[tid] = tid < kD3 ? a.P[a.b_off[2] + tid] : 0.f;
+  for (int e = tid; e < kB * kS3; e += kThreads) DZ3[e] = 0.f;
+  float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
+  __syncthreads();
+
+  bool ok = true;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);
+    const int par = (int)(s & 1);
+    const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * kB;
+
+    // ---- H1 rows = relu(sum of the 4 k-partials): thread -> (row, 8 columns) ----
+    {
+      const int r = tid >> 4, nc = tid & 15;
+      const int gn = nc >> 1, half = nc & 1;
+      uint4 v[kGK][4];
+      poll.start();
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int gk = 0; gk < kGK; ++gk) {
+          const int64_t g = kOffPart + ((int64_t)(gn + kGN * gk) * kB + rb0 + r) * 16 + half * 8;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) v[gk][p] = ld_gran2(rb, g + 2 * p);
+        }
+#pragma unroll
+        for (int gk = 0; gk < kGK; ++gk)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) all = all && v[gk][p].y == tag && v[gk][p].w == tag;
+        if (all) break;
+        if (!poll.again()) { ok = false; break; }
+      }
+      float hv[8];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float e0 = 0.f, e1 = 0.f;
+#pragma unroll
+        for (int gk = 0; gk < kGK; ++gk) {
+          e0 += __uint_as_float(v[gk][p].x);
+          e1 += __uint_as_float(v[gk][p].z);
+        }
+        hv[2 * p] = fmaxf(e0, 0.f);
+        hv[2 * p + 1] = fmaxf(e1, 0.f);
+      }
+      float* dst = H1 + (rb0 + r) * kS1 + nc * 8;
+      *reinterpret_cast<float4*>(dst) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+    }
+    int y = -1;
+    const int srow = w * 4 + (lane >> 4);  // softmax: 16 lanes per row, 4 rows per wave
+    y = a.labels[r0 + rb0 + srow];
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (!ok) break;
+
+    // ---- layer 2: H2 = relu(H1 W2^T + b2), wave w -> 16 output columns ----
+    {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      const float* ha = H1 + (rb0 + i) * kS1 + q;
+      const float* wb = W2 + (16 * w + i) * kS1 + q;
+#pragma unroll
+      for (int ks = 0; ks < kD1 / 4; ks += 2) {
+        a0 = mfma_f32_16x16x4(ha[4 * ks], wb[4 * ks], a0);
+        a1 = mfma_f32_16x16x4(ha[4 * ks + 4], wb[4 * ks + 4], a1);
+      }
+      const int n = 16 * w + i;
+      const float bn = B2[n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H2[(rb0 + 4 * q + r) * kS2 + n] = fmaxf(a0[r] + a1[r] + bn, 0.f);
+    }
+    __syncthreads();
+    // ---- layer 3 partial logits: K = 64 split over the 4 waves ----
+    {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* ha = H2 + (rb0 + i) * kS2 + q;
+      const float* wb = W3 + i * kS2 + q;
+#pragma unroll
+      for (int ks = 4 * w; ks < 4 * w + 4; ++ks) acc = mfma_f32_16x16x4(ha[4 * ks], wb[4 * ks], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) RED[w * 256 + (4 * q + r) * 16 + i] = acc[r];
+    }
+    __syncthreads();
+    // ---- softmax + CE + dLogits ----
+    {
+      const int col = lane & 15;
+      const bool cv = col < kD3;
+      float z = -3.402823466e38f;
+      if (cv) {
+        z = B3[col];
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) z += RED[ww * 256 + srow * 16 + col];
+      }
+      float mx = z;
+      int amax = cv ? col : 0x7fffffff;
+      row16_argmax(mx, amax);
+      const float e = cv ? expf(z - mx) : 0.f;
+      const float se = row16_sum(e);
+      const float p = e / se;
+      float g = 0.f;
+      if (cv) {
+        g = (p - (col == y ? 1.f : 0.f)) * a.inv_batch;
+        if (col == y) loss_acc += -logf(p + 1e-10f);
+      }
+      DZ3[(rb0 + srow) * kS3 + col] = g;
+      if (col == 0) {
+        corr_acc += amax == y ? 1.f : 0.f;
+        cnt_acc += 1.f;
+      }
+    }
+    __syncthreads();
+    // ---- dZ2 = (dZ3 W3) * (H2 > 0), wave w -> 16 columns ----
+    {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int h = 16 * w + i;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        acc = mfma_f32_16x16x4(DZ3[(rb0 + i) * kS3 + 4 * ks + q], W3[(4 * ks + q) * kS2 + h], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rb0 + 4 * q + r;
+        DZ2[m * kS2 + h] = H2[m * kS2 + h] > 0.f ? acc[r] : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- dZ1 = (dZ2 W2) * (H1 > 0), published to the layer-1 blocks ----
+#pragma unroll
+    for (int t = w; t < kD1 / 16; t += 4) {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      const int n = 16 * t + i;
+#pragma unroll
+      for (int ks = 0; ks < kD2 / 4; ks += 2) {
+        a0 = mfma_f32_16x16x4(DZ2[(rb0 + i) * kS2 + 4 * ks + q], W2[(4 * ks + q) * kS1 + n], a0);
+        a1 = mfma_f32_16x16x4(DZ2[(rb0 + i) * kS2 + 4 * ks + 4 + q], W2[(4 * ks + 4 + q) * kS1 + n], a1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rb0 + 4 * q + r;
+        const float v = H1[m * kS1 + n] > 0.f ? a0[r] + a1[r] : 0.f;
+        st_gran(rb, kOffDz1 + (int64_t)m * kD1 + n, v, tag);
+      }
+    }
+
+    // ---- off the critical path: exchange rows, full-batch dW2 / dW3 ----
+    {
+      const int64_t mine = kOffCx + ((int64_t)par * kNCH + c) * kCXG;
+      // payload granule e -> (segment, row, col): H1 [16][128] | H2 [16][64] | dZ2 | dZ3 [16][16]
+      for (int e = tid * 2; e < kCXG; e += 2 * kThreads) {
+        float v0, v1;
+        if (e < 2048) {
+          const int r = e >> 7, cc = e & 127;
+          v0 = H1[(rb0 + r) * kS1 + cc]; v1 = H1[(rb0 + r) * kS1 + cc + 1];
+        } else if (e < 3072) {
+          const int x = e - 2048, r = x >> 6, cc = x & 63;
+          v0 = H2[(rb0 + r) * kS2 + cc]; v1 = H2[(rb0 + r) * kS2 + cc + 1];
+        } else if (e < 4096) {
+          const int x = e - 3072, r = x >> 6, cc = x & 63;
+          v0 = DZ2[(rb0 + r) * kS2 + cc]; v1 = DZ2[(rb0 + r) * kS2 + cc + 1];
+        } else {
+          const int x = e - 4096, r = x >> 4, cc = x & 15;
+          v0 = DZ3[(rb0 + r) * kS3 + cc]; v1 = DZ3[(rb0 + r) * kS3 + cc + 1];
+        }
+        st_gran(rb, mine + e, v0, tag);
+        st_gran(rb, mine + e + 1, v1, tag);
+      }
+      // the three peers' payloads: every pair of this thread in one load batch,
+      // re-polled as a batch until all tags match
+      constexpr int kPer = (kCXG / 2 + kThreads - 1) / kThreads;  // 9 pairs per peer
+      uint4 v[kNCH - 1][kPer];
+      poll.start();
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int cs = 0; cs < kNCH - 1; ++cs) {
+          const int src = (c + 1 + cs) % kNCH;
+          const int64_t base = kOffCx + ((int64_t)par * kNCH + src) * kCXG;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
+            const int e = 2 * (tid + j * kThreads);
+            v[cs][j] = e < kCXG ? ld_gran2(rb, base + e) : make_uint4(0u, tag, 0u, tag);
+          }
+        }
+#pragma unroll
+        for (int cs = 0; cs < kNCH - 1; ++cs)
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) all = all && v[cs][j].y == tag && v[cs][j].w == tag;
+        if (all) break;
+        if (!poll.again()) { ok = false; break; }
+      }
+#pragma unroll
+      for (int cs = 0; cs < kNCH - 1; ++cs) {
+        const int sr0 = 16 * ((c + 1 + cs) % kNCH);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const int e = 2 * (tid + j * kThreads);
+          if (e >= kCXG) continue;
+          const float v0 = __uint_as_float(v[cs][j].x), v1 = __uint_as_float(v[cs][j].z);
+          if (e < 2048) {
+            const int r = e >> 7, cc = e & 127;
+            H1[(sr0 + r) * kS1 + cc] = v0; H1[(sr0 + r) * kS1 + cc + 1] = v1;
+          } else if (e < 3072) {
+            const int x = e - 2048, r = x >> 6, cc = x & 63;
+            H2[(sr0 + r) * kS2 + cc] = v0; H2[(sr0 + r) * kS2 + cc + 1] = v1;
+          } else if (e < 4096) {
+            const int x = e - 3072, r = x >> 6, cc = x & 63;
+            DZ2[(sr0 + r) * kS2 + cc] = v0; DZ2[(sr0 + r) * kS2 + cc + 1] = v1;
+          } else {
+            const int x = e - 4096, r = x >> 4, cc = x & 15;
+            DZ3[(sr0 + r) * kS3 + cc] = v0; DZ3[(sr0 + r) * kS3 + cc + 1] = v1;
+          }
+        }
+      }
+    }
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (!ok) break;
+    // dW2 [64 h][128 n] = dZ2^T H1 over the 64 batch rows; wave w: h tile w, 8 n tiles
+    {
+      f32x4 g[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int ms = 0; ms < kB / 4; ++ms) {
+        const int m = 4 * ms + q;
+        const float av = DZ2[m * kS2 + 16 * w + i];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) g[t] = mfma_f32_16x16x4(av, H1[m * kS1 + 16 * t + i], g[t]);
+      }
+      // dW3 [16 o][64 h] = dZ3^T H2 (o >= 10 rows are zero): wave w -> h tile w
+      f32x4 g3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int ms = 0; ms < kB / 4; ++ms) {
+        const int m = 4 * ms + q;
+        g3 = mfma_f32_16x16x4(DZ3[m * kS3 + i], H2[m * kS2 + 16 * w + i], g3);
+      }
+      // biases: db2[h] (thread h < 64), db3[o] (threads 64..79)
+      float db = 0.f;
+      if (tid < kD2) {
+#pragma unroll 8
+        for (int m = 0; m < kB; ++m) db += DZ2[m * kS2 + tid];
+      } else if (tid < kD2 + kD3) {
+#pragma unroll 8
+        for (int m = 0; m < kB; ++m) db += DZ3[m * kS3 + tid - kD2];
+      }
+      // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i] -= a.lr * g[t][r];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 4 * q + r;
+        if (o < kD3) W3[o * kS2 + 16 * w + i] -= a.lr * g3[r];
+      }
+      if (tid < kD2) B2[tid] -= a.lr * db;
+      else if (tid < kD2 + kD3) B3[tid - kD2] -= a.lr * db;
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: stats; chain 0 writes W2, b2, W3, b3 back ----
+  const float l = wave_sum(loss_acc), cr = wave_sum(corr_acc), cn = wave_sum(cnt_acc);
+  if (lane == 0 && a.stats != nullptr && cn > 0.f) {
+    atomicAdd(a.stats + 0, l);
+    atomicAdd(a.stats + 1, cr);
+    atomicAdd(a.stats + 2, cn);
+  }
+  if (c == 0) {
+    for (int e = tid; e < kD2 * (kD1 / 4); e += kThreads) {
+      const int r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
+      *reinterpret_cast<float4*>(a.P + a.w_off[1] + (int64_t)r * kD1 + 4 * c4) =
+          *reinterpret_cast<const float4*>(W2 + r * kS1 + 4 * c4);
+    }
+    for (int e = tid; e < kD3 * kD2; e += kThreads) {
+      const int r = e / kD2, col = e - r * kD2;
+      a.P[a.w_off[2] + (int64_t)r * kD2 + col] = W3[r * kS2 + col];
+    }
+    if (tid < kD2) a.P[a.b_off[1] + tid] = B2[tid];
+    if (tid < kD3) a.P[a.b_off[2] + tid] = B3[tid];
+  }
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void mlp_persist_k(PersistArgs a) {
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  if ((int)blockIdx.x < kNL1)
+    pk_layer1(a, lds, blockIdx.x);
+  else
+    pk_chain(a, lds, blockIdx.x - kNL1);
+}
+
+bool mlp_persist_supported(const MlpDesc& d) {
+  return d.nlayers == 3 && d.batch == kB && d.dims[0] == kD0 && d.dims[1] == kD1 &&
+         d.dims[2] == kD2 && d.dims[3] == kD3;
+}
+
+int64_t mlp_persist_xbuf_granules() { return kTotalG; }
+
+hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
+                             int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
+                             float* stats, uint32_t* err, uint64_t timeout_ticks, hipStream_t s) {
+  if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
+      (ldx % 4) != 0)
+    return hipErrorInvalidValue;
+  PersistArgs a{};
+  a.X = X;
+  a.ldx = ldx;
+  a.labels = labels;
+  a.P = P;
+  for (int l = 0; l < 3; ++l) {
+    a.w_off[l] = d.w_off[l];
+    a.b_off[l] = d.b_off[l];
+  }
+  a.ctr = ctr;
+  a.nbatches = d.nbatches;
+  a.steps = steps;
+  a.lr = lr;
+  a.inv_batch = 1.0f / (float)kB;
+  a.xb = xb;
+  a.stats = stats;
+  a.err = err;
+  a.timeout_ticks = timeout_ticks;
+  const size_t lds = (size_t)kLdsFloats * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_persist_k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(mlp_persist_k, dim3(kNL1 + kNCH), dim3(kThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dsml

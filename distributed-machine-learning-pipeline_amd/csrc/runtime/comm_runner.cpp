@@ -293,7 +293,40 @@ void MlpRunner::enqueue_update(hipStream_t s) {
     DSML_HIP_CHECK(sgd_update_f32(b_.P, b_.G, b_.nparams, lr_ * gscale, s));
 }
 
+void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms) {
+  if (xbuf == nullptr) {
+    pk_xb_ = nullptr;
+    pk_err_ = nullptr;
+    reset_graph();
+    return;
+  }
+  if (!mlp_persist_supported(d_))
+    throw std::invalid_argument("set_persist: the persistent step covers 784-128-64-10 at batch 64");
+  if (mom_ != 0.f || wd_ != 0.f) throw std::invalid_argument("set_persist: plain SGD only");
+  if (comm_ != nullptr || xchg_ != nullptr || world_ != 1)
+    throw std::invalid_argument("set_persist: single replica only");
+  if (err == nullptr) throw std::invalid_argument("set_persist: needs an error word");
+  pk_xb_ = xbuf;
+  pk_err_ = err;
+  pk_timeout_ = (uint64_t)(timeout_ms * 1e5);  // s_memrealtime: 100 MHz
+  reset_graph();
+}
+
+void MlpRunner::enqueue_steps(int n, hipStream_t s) {
+  if (n <= 0) return;
+  if (pk_xb_ != nullptr) {
+    DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
+                                     b_.stats, pk_err_, pk_timeout_, s));
+    return;
+  }
+  for (int i = 0; i < n; ++i) enqueue_step(s);
+}
+
 void MlpRunner::enqueue_step(hipStream_t s) {
+  if (pk_xb_ != nullptr) {
+    enqueue_steps(1, s);
+    return;
+  }
   if (xchg_ != nullptr) {
     DSML_HIP_CHECK(mlp_f32_first_layer(b_.X, b_.ldx, b_.P, b_.slab, b_.ctr, 0, d_, cfg_, b_.labels, b_.ws, s));
     DSML_HIP_CHECK(mlp_f32_rowchain(b_.P, b_.slab, cfg_.nsplit, b_.ws, b_.labels, b_.ctr, 0, d_,
@@ -341,7 +374,7 @@ void MlpRunner::capture(int steps, bool capture_comm, hipStream_t s) {
   Captured c;
   DSML_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
   try {
-    for (int i = 0; i < steps; ++i) enqueue_step(s);
+    enqueue_steps(steps, s);
   } catch (...) {
     hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(s, &g);

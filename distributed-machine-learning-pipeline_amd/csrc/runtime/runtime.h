@@ -271,6 +271,12 @@ class MlpRunner {
   // Xall holds every rank's input shard in MFMA fragment order (rank r at
   // Xall + r * xstride).  Replaces set_exchange's mode while set.
   void set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride, int waves = 0);
+  // Persistent fused step (kernels/mlp_persist.hip): every enqueue of n steps
+  // is ONE launch.  Single replica, plain SGD, the flagship shape only.
+  void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms);
+  bool persist_active() const { return pk_xb_ != nullptr; }
+  // Enqueue n full steps (one launch in persistent mode).
+  void enqueue_steps(int n, hipStream_t s);
   bool exchange_active() const { return xchg_ != nullptr; }
   int exchange_mode() const { return xchg_ == nullptr ? 0 : (xact_ ? 2 : 1); }
   // Enqueue one full step on stream s (no host sync).
@@ -307,6 +313,9 @@ class MlpRunner {
   const float* xall_ = nullptr;
   int64_t xstride_ = 0;
   int xact_waves_ = 0;
+  uint64_t* pk_xb_ = nullptr;
+  uint32_t* pk_err_ = nullptr;
+  uint64_t pk_timeout_ = 0;
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;

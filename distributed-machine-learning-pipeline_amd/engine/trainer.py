@@ -71,7 +71,7 @@ class MlpTrainer:
                  params: Optional[torch.Tensor] = None, external_comm=None,
                  capture_collectives: Optional[bool] = None, xchg_timeout_ms: float = 10000.0,
                  xact_waves: int = 0, auto_fallback: str = "rccl",
-                 stream: Optional["torch.cuda.Stream"] = None):
+                 stream: Optional["torch.cuda.Stream"] = None, persist: Optional[bool] = None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -120,6 +120,15 @@ class MlpTrainer:
         self._exchanges: Dict[str, object] = {}
         self.runner = None
         self._stream = stream  # caller-owned stream for the native runner (None: its own)
+        # persistent fused step (kernels/mlp_persist.hip): None = when supported
+        # (single replica, plain SGD, 784-128-64-10 @ 64); HIPDSML_PERSIST=0 disables
+        if persist is None:
+            import os
+
+            persist = os.environ.get("HIPDSML_PERSIST", "1") != "0"
+        self._want_persist = bool(persist)
+        self.pk_buf: Optional[torch.Tensor] = None
+        self.pk_err: Optional[torch.Tensor] = None
         if self.device.type == "cuda":
             self.backend = "hip"
             self._init_hip(ring_chunk_bytes)
@@ -147,6 +156,12 @@ class MlpTrainer:
         self._ring_chunk = int(ring_chunk_bytes)
         self._collective_warm = False  # an eager collective step has run (RCCL connected)
         if not self.ctx.is_distributed:
+            plain = not (self.momentum or self.weight_decay)
+            if self._want_persist and plain and C.mlp_persist_supported(self.layout.desc_list()):
+                self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64, device=d)
+                self.pk_err = torch.zeros(1, dtype=torch.int32, device=d)
+                self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0)
+                self.sync_active = "none"
             return
         if self.sync == "torch":
             self.sync_active = "torch"
@@ -312,6 +327,7 @@ class MlpTrainer:
         self.P.copy_(P0)
         self.ctr.copy_(ctr0)
         self.stats.copy_(st0)
+        self._rewound()
         # the counters went back: rewind every exchange's flags (collective)
         for x in getattr(self, "_exchanges", {}).values():
             X.reset_group(self.ctx, x)
@@ -330,9 +346,20 @@ class MlpTrainer:
             self.runner.update()
 
     # -------------------------------------------------------------- public --
+    @property
+    def persistent(self) -> bool:
+        """Steps run as one persistent launch per train_steps call."""
+        return self.runner is not None and self.pk_buf is not None
+
+    def _rewound(self) -> None:
+        """The step counter went back: stale hand-off tags could match again."""
+        if self.pk_buf is not None:
+            self.pk_buf.zero_()
+            self.pk_err.zero_()
+
     def _graphs_on(self) -> bool:
         """Whether train_steps replays hipGraphs for the active sync mode."""
-        if self.graph_steps <= 0 or self.runner is None:
+        if self.graph_steps <= 0 or self.runner is None or self.persistent:
             return False
         if not self.ctx.is_distributed:
             return True
@@ -400,6 +427,9 @@ class MlpTrainer:
                     from ..parallel.xchg import check
 
                     check(self.xchg)
+                if self.pk_err is not None and int(self.pk_err.item()) != 0:
+                    raise RuntimeError("persistent step: an on-chip hand-off timed out "
+                                       "(launch ended early; parameters are not valid)")
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
 
@@ -552,6 +582,7 @@ class MlpTrainer:
         if self.backend == "hip":
             # A = B = s at the start of step s (dsml.h step-counter protocol)
             self.ctr.fill_(self.steps_done)
+            self._rewound()
             torch.cuda.synchronize(self.device)
             if self.xchg is not None:  # flags may be ahead of the restored step
                 from ..parallel.xchg import reset_group

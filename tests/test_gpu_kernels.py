@@ -241,8 +241,8 @@ def test_trainer_graph_sizes_cover_any_step_count():
     (no eager fallback), bit-identical to eager launches."""
     spec = MlpSpec((784, 128, 64, 10))
     ds = synthetic_mnist(64 * 8, seed=4)
-    a = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9)
-    b = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9, graph_steps=5)
+    a = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9, persist=False)
+    b = MlpTrainer(spec, ds, batch=64, lr=0.01, ctx=_ctx(), seed=9, graph_steps=5, persist=False)
     for n in (3, 12, 7):
         a.train_steps(n)
         b.train_steps(n)

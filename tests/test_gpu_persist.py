@@ -1,0 +1,93 @@
+"""Persistent fused step (kernels/mlp_persist.hip): S SGD steps of the
+flagship MLP 784-128-64-10 per launch, weights resident on chip, tagged-granule
+hand-offs between 32 layer-1 blocks and 4 row-chain blocks.  Checked against
+the fp32 torch reference (models/mlp.py grads_ref) and the three-launch path."""
+import pytest
+import torch
+
+from hipdsml.data.mnist import synthetic_mnist
+from hipdsml.engine.trainer import MlpTrainer
+from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
+from hipdsml.parallel.dist import DistContext
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+SPEC = MlpSpec((784, 128, 64, 10))
+
+
+def _tr(ds, persist, lr=0.05, seed=3):
+    return MlpTrainer(SPEC, ds, batch=64, lr=lr, ctx=DistContext(device=DEV), seed=seed,
+                      persist=persist)
+
+
+def _ref(ds, steps, lr=0.05, seed=3):
+    nb = len(ds) // 64
+    lay = MlpLayout(SPEC, 64, nb)
+    P = init_params(lay, seed, "reference")
+    loss = 0.0
+    for s in range(steps):
+        b = s % nb
+        g, ls, _ = grads_ref(lay, P, ds.X[b * 64:(b + 1) * 64], ds.y[b * 64:(b + 1) * 64])
+        loss += float(ls)
+        P = P - lr * g
+    return P, loss
+
+
+def test_persistent_step_is_active_for_the_flagship():
+    t = _tr(synthetic_mnist(64 * 4, seed=1), None)
+    assert t.persistent and t.runner.persist_active()
+    assert not _tr(synthetic_mnist(64 * 4, seed=1), False).persistent
+
+
+@pytest.mark.parametrize("steps", [1, 2, 9])
+def test_persistent_matches_fp32_reference(steps):
+    ds = synthetic_mnist(64 * 4, seed=11)
+    t = _tr(ds, True)
+    t.train_steps(steps)
+    t.synchronize()
+    want, loss = _ref(ds, steps)
+    err = (t.P.cpu() - want).abs().max().item()
+    assert err < 2e-5, err
+    st = t.read_stats()
+    assert st.count == 64 * steps
+    assert abs(st.loss_sum - loss) < 1e-3 * max(1.0, loss)
+    assert int(t.ctr[0].item()) == steps and int(t.ctr[1].item()) == steps
+
+
+def test_persistent_launch_split_is_bit_exact_and_matches_three_launch_path():
+    ds = synthetic_mnist(64 * 5, seed=12)
+    a, b, c = _tr(ds, True), _tr(ds, True), _tr(ds, False)
+    a.train_steps(23)
+    for n in (7, 1, 15):  # epoch wrap-around inside and across launches
+        b.train_steps(n)
+    c.train_steps(23)
+    for t in (a, b, c):
+        t.synchronize()
+    assert torch.equal(a.P, b.P)
+    assert (a.P - c.P).abs().max().item() < 5e-5
+
+
+def test_persistent_resume_rewinds_tags(tmp_path):
+    ds = synthetic_mnist(64 * 4, seed=13)
+    a = _tr(ds, True)
+    a.train_steps(6)
+    sd = a.state_dict()
+    a.train_steps(5)
+    a.synchronize()
+    b = _tr(ds, True)
+    b.train_steps(9)  # ahead of the checkpoint: its buffers hold later tags
+    b.load_state_dict(sd)
+    b.train_steps(5)
+    b.synchronize()
+    assert torch.equal(a.P, b.P)
+
+
+def test_persistent_long_run_converges():
+    ds = synthetic_mnist(64 * 50, seed=14)
+    t = _tr(ds, True, lr=0.05)
+    t.train_steps(50)
+    first = t.read_stats()
+    t.train_steps(500)
+    last = t.read_stats()
+    assert last.avg_loss < first.avg_loss
+    assert torch.isfinite(t.P).all()
