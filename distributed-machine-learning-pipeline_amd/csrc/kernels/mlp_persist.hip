@@ -54,11 +54,14 @@ constexpr int kThreads = 256;
 static_assert(kKC % 4 == 0, "k slice must hold whole MFMA k-steps");
 
 // ---- LDS layouts (floats) ----------------------------------------------------
-constexpr int kXS = kKC + 16;              // X / W1 tile row stride (2-way conflicts at most)
+constexpr int kXS = kKC + 16;              // W1 tile row stride (2-way conflicts at most)
+// X tiles are [64][196] unpadded: LDS-DMA (global_load_lds) writes each wave
+// instruction's 1 KiB lane-linearly, so the image must be contiguous; the
+// 196-float stride costs at most 2-way bank conflicts on the MFMA operand reads.
 struct L1Lay {
-  static constexpr int X0 = 0;                       // X tile, buffer 0 [64][kXS]
-  static constexpr int X1 = X0 + kB * kXS;           // buffer 1
-  static constexpr int W = X1 + kB * kXS;            // W1 tile [16][kXS]
+  static constexpr int X0 = 0;                       // X tile, buffer 0 [64][196]
+  static constexpr int X1 = X0 + kB * kKC;           // buffer 1
+  static constexpr int W = X1 + kB * kKC;            // W1 tile [16][kXS]
   static constexpr int DZ = W + 16 * kXS;            // dZ1 tile [64][17]
   static constexpr int B1 = DZ + kB * 17;            // b1 slice [16]
   static constexpr int TOTAL = B1 + 16;
@@ -118,9 +121,9 @@ struct Poll {
   uint64_t timeout;
   uint64_t t0;
   uint32_t spins;
-  __device__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); spins = 0; }
+  __device__ __forceinline__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); spins = 0; }
   // true: keep waiting; false: give up (timeout, or another block gave up)
-  __device__ bool again() {
+  __device__ __forceinline__ bool again() {
     if ((++spins & 31u) == 0u &&
         __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
       return false;
@@ -160,6 +163,26 @@ struct PersistArgs {
 // -----------------------------------------------------------------------------
 // Layer-1 block
 // -----------------------------------------------------------------------------
+constexpr int kXF4 = kB * (kKC / 4);  // float4 of one X tile (3136 = 49 KiB-chunks of 64)
+static_assert(kXF4 % 64 == 0, "X tile must be whole 1 KiB LDS-DMA chunks");
+typedef __attribute__((address_space(1))) void* pk_gptr;
+typedef __attribute__((address_space(3))) void* pk_lptr;
+
+// X tile of step s -> LDS buffer by LDS-DMA (16 B per lane, no registers):
+// wave w issues chunks w, w+4, ...; completion is waited by the next
+// __syncthreads (its vmcnt(0)).
+__device__ __forceinline__ void pk_glds_x(const PersistArgs& a, float* lds, int buf, uint64_t s,
+                                          int lane, int w, int k0) {
+  const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * kB;
+  float* xl = lds + (buf ? L1Lay::X1 : L1Lay::X0);
+  for (int ch = w; ch < kXF4 / 64; ch += 4) {
+    const int e = ch * 64 + lane;
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    __builtin_amdgcn_global_load_lds((pk_gptr)(a.X + (r0 + r) * a.ldx + k0 + 4 * c4),
+                                     (pk_lptr)(xl + ch * 256), 16, 0, 0);
+  }
+}
+
 __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int lb) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
@@ -182,31 +205,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   if (tid < 16) B1[tid] = gk == 0 ? a.P[a.b_off[0] + n0 + tid] : 0.f;
   constexpr int kXF4 = kB * (kKC / 4);                 // float4 of one X tile (3136)
   constexpr int kXPer = (kXF4 + kThreads - 1) / kThreads;  // 13
-  float4 xr[kXPer];
-  auto load_x = [&](uint64_t s) {
-    const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * kB;
-#pragma unroll
-    for (int j = 0; j < kXPer; ++j) {
-      const int e = tid + j * kThreads;
-      const int ec = e < kXF4 ? e : kXF4 - 1;
-      const int r = ec / (kKC / 4), c4 = ec - r * (kKC / 4);
-      xr[j] = *reinterpret_cast<const float4*>(a.X + (r0 + r) * a.ldx + k0 + 4 * c4);
-    }
-  };
-  auto store_x = [&](int buf) {
-    float* Xl = lds + (buf ? L1Lay::X1 : L1Lay::X0);
-#pragma unroll
-    for (int j = 0; j < kXPer; ++j) {
-      const int e = tid + j * kThreads;
-      if (e < kXF4) {
-        const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
-        *reinterpret_cast<float4*>(Xl + r * kXS + 4 * c4) = xr[j];
-      }
-    }
-  };
-  load_x(s0);
-  store_x(0);
-  if (a.steps > 1) load_x(s0 + 1);
+  pk_glds_x(a, lds, 0, s0, lane, w, k0);
   __syncthreads();
 
   bool ok = true;
@@ -219,7 +218,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
     // ---- forward partial: wave w -> rows 16w..16w+15, all 16 n of the tile ----
     {
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const float* xa = Xl + (16 * w + i) * kXS + q;
+      const float* xa = Xl + (16 * w + i) * kKC + q;
       const float* wa = Wl + i * kXS + q;
 #pragma unroll 7
       for (int ks = 0; ks < kKC / 4; ks += 2) {
@@ -233,10 +232,9 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
         st_gran(rb, kOffPart + ((int64_t)lb * kB + m) * 16 + i, acc0[r] + acc1[r] + bn, tag);
       }
     }
-    // next step's X: registers -> the other LDS buffer (its last reader, the
-    // previous step's backward, finished before the barrier that ended it)
-    if (it + 1 < a.steps) store_x(buf ^ 1);
-    if (it + 2 < a.steps) load_x(s + 2);
+    // next step's X into the other buffer (its last reader, the previous
+    // step's backward, finished before the barrier that ended that step)
+    if (it + 1 < a.steps) pk_glds_x(a, lds, buf ^ 1, s + 1, lane, w, k0);
 
     // ---- wait for dZ1[:, n0 .. n0+15] of this step (4 chain blocks) ----
     {
@@ -278,7 +276,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 #pragma unroll
         for (int ms = 0; ms < kB / 4; ++ms) {
           const int m = 4 * ms + q;
-          g[t] = mfma_f32_16x16x4(Dz[m * 17 + i], Xl[m * kXS + kcc], g[t]);
+          g[t] = mfma_f32_16x16x4(Dz[m * 17 + i], Xl[m * kKC + kcc], g[t]);
         }
       }
     }
