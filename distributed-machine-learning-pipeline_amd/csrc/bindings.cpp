@@ -488,6 +488,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return mlp_persist_supported(desc_from_list(desc));
   });
   m.def("mlp_persist_xbuf_granules", []() { return mlp_persist_xbuf_granules(); });
+  m.def("mlp_persist_stamps", []() {
+    std::vector<uint64_t> v(3 * 8 * 8);
+    hip_ok(mlp_persist_read_stamps(v.data()), "mlp_persist_read_stamps");
+    return v;
+  });
+  m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
   m.def("mlp_plan", [](const std::vector<int64_t>& desc) {
     const MlpDesc d = desc_from_list(desc);
     const MlpLaunchCfg c = mlp_plan_first_layer(d);

@@ -90,6 +90,8 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
 // uint64 granules, zeroed whenever the step counter is rewound; `err` is set
 // when a hand-off timed out (the launch then ends early).
 bool mlp_persist_supported(const MlpDesc& d);
+hipError_t mlp_persist_read_stamps(uint64_t* host_out);  // [3][8][8] (role, step, phase)
+void mlp_persist_set_stamping(bool on);
 int64_t mlp_persist_xbuf_granules();
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,

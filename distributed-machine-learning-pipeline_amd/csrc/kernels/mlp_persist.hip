@@ -85,15 +85,21 @@ static_assert(kLdsFloats * 4 <= 160 * 1024, "LDS budget");
 // ---- exchange buffer layout (8-byte granules) -----------------------------------
 // PART[32][64][16]   layer-1 partials (b1 added by gk == 0 blocks)
 // DZ1 [64][128]      activation gradient of layer 1
-// CX  [2][4][kCXG]   chain exchange (parity by step): H1 rows [16][128],
-//                    H2 rows [16][64], dZ2 rows [16][64], dZ3 rows [16][16]
+// CX  [2][4][kCXG]   chain exchange (parity by step), PLAIN fp32 (no tags):
+//                    H1 rows [16][128], H2 rows [16][64], dZ2 rows [16][64],
+//                    dZ3 rows [16][16]; published by one flag per chain and
+//                    step (CXF), i.e. the flag form of the hand-off: half the
+//                    bytes of granules and one bulk read once the flag is seen.
 constexpr int kPartG = kNL1 * kB * 16;
 constexpr int kDz1G = kB * kD1;
 constexpr int kCXG = 16 * kD1 + 16 * kD2 + 16 * kD2 + 16 * 16;  // 4352
 constexpr int64_t kOffPart = 0, kOffDz1 = kOffPart + kPartG, kOffCx = kOffDz1 + kDz1G;
-constexpr int64_t kTotalG = kOffCx + 2 * kNCH * kCXG;
+constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCXG / 2;  // CX holds floats: 2 per granule
+constexpr int64_t kTotalG = kOffCxf + 2 * kNCH;
+static_assert(kCXG % 4 == 0, "exchange rows travel as 16-B vectors");
 
 constexpr int kSc1 = 16;  // buffer aux: sc1 (write-through store / L1-bypassing load)
+typedef uint32_t nu4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff,
@@ -142,6 +148,18 @@ __device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
 }
 
 }  // namespace
+
+// Phase stamps (s_memrealtime, 100 MHz) of layer-1 block 0 and chain block 0
+// (and layer-2 gradient block 0) for steps 8..15 of a launch, profiling only
+// (tools/pk_stamps.py): [role][step - 8][phase], role 0 = layer-1, 1 = chain,
+// 2 = layer-2 gradients.
+__device__ uint64_t g_pk_stamps[3][8][8];
+__device__ int g_pk_stamp_on;
+#define PK_STAMP(role, ph)                                                            \
+  do {                                                                                \
+    if (stamp_on && threadIdx.x == 0 && it >= 8 && it < 16)                            \
+      g_pk_stamps[(role)][it - 8][(ph)] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
 
 struct PersistArgs {
   const float* X;
@@ -209,7 +227,9 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   __syncthreads();
 
   bool ok = true;
+  const int stamp_on = g_pk_stamp_on && lb == 0;
   for (int it = 0; it < a.steps && ok; ++it) {
+    PK_STAMP(0, 0);
     const uint64_t s = s0 + (uint64_t)it;
     const uint32_t tag = (uint32_t)(s + 1);
     const int buf = it & 1;
@@ -217,13 +237,24 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 
     // ---- forward partial: wave w -> rows 16w..16w+15, all 16 n of the tile ----
     {
+      // 49 k-steps in batches of 7: a batch's 14 LDS operands are read ahead
+      // of its MFMAs (two accumulators hide the MFMA dependency latency)
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       const float* xa = Xl + (16 * w + i) * kKC + q;
       const float* wa = Wl + i * kXS + q;
-#pragma unroll 7
-      for (int ks = 0; ks < kKC / 4; ks += 2) {
-        acc0 = mfma_f32_16x16x4(xa[4 * ks], wa[4 * ks], acc0);
-        if (ks + 1 < kKC / 4) acc1 = mfma_f32_16x16x4(xa[4 * ks + 4], wa[4 * ks + 4], acc1);
+#pragma unroll
+      for (int kb = 0; kb < kKC / 4; kb += 7) {
+        float xv[7], wv[7];
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+          xv[u] = xa[4 * (kb + u)];
+          wv[u] = wa[4 * (kb + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+          if (u & 1) acc1 = mfma_f32_16x16x4(xv[u], wv[u], acc1);
+          else acc0 = mfma_f32_16x16x4(xv[u], wv[u], acc0);
+        }
       }
       const float bn = B1[i];
 #pragma unroll
@@ -232,6 +263,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
         st_gran(rb, kOffPart + ((int64_t)lb * kB + m) * 16 + i, acc0[r] + acc1[r] + bn, tag);
       }
     }
+    PK_STAMP(0, 1);
     // next step's X into the other buffer (its last reader, the previous
     // step's backward, finished before the barrier that ended that step)
     if (it + 1 < a.steps) pk_glds_x(a, lds, buf ^ 1, s + 1, lane, w, k0);
@@ -262,10 +294,16 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
     }
     ok = __syncthreads_and(ok ? 1 : 0) != 0;
     if (!ok) break;
+    PK_STAMP(0, 2);
 
     // ---- backward: dW1 tile [16 n][196 k] = dZ1^T . X, SGD in LDS ----
     // wave w: k tiles kt = w, w + 4, w + 8, w + 12 (13 tiles of 16, the last 4 wide)
     f32x4 g[4];
+    // The last k tile (kt = 12, wave 0) is 4 columns wide; its column k = 196
+    // multiplies dZ1 by ones instead, so the MFMA also yields db1 = colsum(dZ1).
+    float dv[kB / 4];  // A operand (dZ1 column i of rows 4ms + q), shared by the tiles
+#pragma unroll
+    for (int ms = 0; ms < kB / 4; ++ms) dv[ms] = Dz[(4 * ms + q) * 17 + i];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -273,17 +311,14 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
       if (kt * 16 < kKC) {
         const int kc = kt * 16 + i;
         const int kcc = kc < kKC ? kc : kKC - 1;
+        const float pad = kc == kKC ? 1.f : 0.f;
+        float xv[kB / 4];
 #pragma unroll
-        for (int ms = 0; ms < kB / 4; ++ms) {
-          const int m = 4 * ms + q;
-          g[t] = mfma_f32_16x16x4(Dz[m * 17 + i], Xl[m * kKC + kcc], g[t]);
-        }
+        for (int ms = 0; ms < kB / 4; ++ms) xv[ms] = Xl[(4 * ms + q) * kKC + kcc];
+#pragma unroll
+        for (int ms = 0; ms < kB / 4; ++ms)
+          g[t] = mfma_f32_16x16x4(dv[ms], kc < kKC ? xv[ms] : pad, g[t]);
       }
-    }
-    float db = 0.f;
-    if (gk == 0 && tid < 16) {
-#pragma unroll 8
-      for (int m = 0; m < kB; ++m) db += Dz[m * 17 + tid];
     }
     // every wave read this step's W1 tile in the forward, before the barrier above
 #pragma unroll
@@ -295,8 +330,12 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
         for (int r = 0; r < 4; ++r) Wl[(4 * q + r) * kXS + kc] -= a.lr * g[t][r];
       }
     }
-    if (gk == 0 && tid < 16) B1[tid] -= a.lr * db;
+    if (gk == 0 && w == 0 && i == kKC - 192) {  // wave 0, tile 12, column k = 196: db1
+#pragma unroll
+      for (int r = 0; r < 4; ++r) B1[4 * q + r] -= a.lr * g[3][r];
+    }
     __syncthreads();
+    PK_STAMP(0, 3);
   }
 
   // ---- epilogue: the resident weights back to HBM ----
@@ -346,7 +385,9 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   __syncthreads();
 
   bool ok = true;
+  const int stamp_on = g_pk_stamp_on && c == 0;
   for (int it = 0; it < a.steps && ok; ++it) {
+    PK_STAMP(1, 0);
     const uint64_t s = s0 + (uint64_t)it;
     const uint32_t tag = (uint32_t)(s + 1);
     const int par = (int)(s & 1);
@@ -394,6 +435,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     y = a.labels[r0 + rb0 + srow];
     ok = __syncthreads_and(ok ? 1 : 0) != 0;
     if (!ok) break;
+    PK_STAMP(1, 1);
 
     // ---- layer 2: H2 = relu(H1 W2^T + b2), wave w -> 16 output columns ----
     {
@@ -450,6 +492,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       }
     }
     __syncthreads();
+    PK_STAMP(1, 2);
     // ---- dZ2 = (dZ3 W3) * (H2 > 0), wave w -> 16 columns ----
     {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -482,105 +525,114 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       }
     }
 
+    PK_STAMP(1, 3);
     // ---- off the critical path: exchange rows, full-batch dW2 / dW3 ----
     {
-      const int64_t mine = kOffCx + ((int64_t)par * kNCH + c) * kCXG;
-      // payload granule e -> (segment, row, col): H1 [16][128] | H2 [16][64] | dZ2 | dZ3 [16][16]
-      for (int e = tid * 2; e < kCXG; e += 2 * kThreads) {
-        float v0, v1;
-        if (e < 2048) {
-          const int r = e >> 7, cc = e & 127;
-          v0 = H1[(rb0 + r) * kS1 + cc]; v1 = H1[(rb0 + r) * kS1 + cc + 1];
-        } else if (e < 3072) {
-          const int x = e - 2048, r = x >> 6, cc = x & 63;
-          v0 = H2[(rb0 + r) * kS2 + cc]; v1 = H2[(rb0 + r) * kS2 + cc + 1];
-        } else if (e < 4096) {
-          const int x = e - 3072, r = x >> 6, cc = x & 63;
-          v0 = DZ2[(rb0 + r) * kS2 + cc]; v1 = DZ2[(rb0 + r) * kS2 + cc + 1];
-        } else {
-          const int x = e - 4096, r = x >> 4, cc = x & 15;
-          v0 = DZ3[(rb0 + r) * kS3 + cc]; v1 = DZ3[(rb0 + r) * kS3 + cc + 1];
-        }
-        st_gran(rb, mine + e, v0, tag);
-        st_gran(rb, mine + e + 1, v1, tag);
+      // own rows -> CX[par][c] as 16-B write-through vectors; every storing
+      // wave drains its stores, then one lane raises the chain's flag
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const int mine = (int)((kOffCx * 2 + ((int64_t)par * kNCH + c) * kCXG) * 4);  // bytes
+      for (int e = tid * 4; e < kCXG; e += 4 * kThreads) {
+        const float* src;
+        if (e < 2048) src = H1 + (rb0 + (e >> 7)) * kS1 + (e & 127);
+        else if (e < 3072) src = H2 + (rb0 + ((e - 2048) >> 6)) * kS2 + ((e - 2048) & 63);
+        else if (e < 4096) src = DZ2 + (rb0 + ((e - 3072) >> 6)) * kS2 + ((e - 3072) & 63);
+        else src = DZ3 + (rb0 + ((e - 4096) >> 4)) * kS3 + ((e - 4096) & 15);
+        const f4v v = {src[0], src[1], src[2], src[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4v, v), rb, mine + e * 4, 0, kSc1);
       }
-      // the three peers' payloads: every pair of this thread in one load batch,
-      // re-polled as a batch until all tags match
-      constexpr int kPer = (kCXG / 2 + kThreads - 1) / kThreads;  // 9 pairs per peer
-      uint4 v[kNCH - 1][kPer];
-      poll.start();
-      for (;;) {
-        bool all = true;
-#pragma unroll
-        for (int cs = 0; cs < kNCH - 1; ++cs) {
-          const int src = (c + 1 + cs) % kNCH;
-          const int64_t base = kOffCx + ((int64_t)par * kNCH + src) * kCXG;
-#pragma unroll
-          for (int j = 0; j < kPer; ++j) {
-            const int e = 2 * (tid + j * kThreads);
-            v[cs][j] = e < kCXG ? ld_gran2(rb, base + e) : make_uint4(0u, tag, 0u, tag);
-          }
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) st_gran(rb, kOffCxf + (int64_t)par * kNCH + c, __uint_as_float(tag), tag);
+      // the peers' flags (one lane each), then their rows in one bulk read
+      if (tid < kNCH - 1) {
+        const int src = (c + 1 + tid) % kNCH;
+        poll.start();
+        for (;;) {
+          const uint4 f = ld_gran2(rb, (kOffCxf + (int64_t)par * kNCH + src) & ~(int64_t)1);
+          const uint32_t ft = ((kOffCxf + par * kNCH + src) & 1) ? f.w : f.y;
+          if (ft == tag) break;
+          if (!poll.again()) { ok = false; break; }
         }
-#pragma unroll
-        for (int cs = 0; cs < kNCH - 1; ++cs)
-#pragma unroll
-          for (int j = 0; j < kPer; ++j) all = all && v[cs][j].y == tag && v[cs][j].w == tag;
-        if (all) break;
-        if (!poll.again()) { ok = false; break; }
       }
-#pragma unroll
-      for (int cs = 0; cs < kNCH - 1; ++cs) {
-        const int sr0 = 16 * ((c + 1 + cs) % kNCH);
+      ok = __syncthreads_and(ok ? 1 : 0) != 0;
+      if (ok) {
+        constexpr int kV = kCXG / 4;                          // 1088 vectors per peer
+        constexpr int kPer = ((kNCH - 1) * kV + kThreads - 1) / kThreads;  // 13
+        nu4v v[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-          const int e = 2 * (tid + j * kThreads);
-          if (e >= kCXG) continue;
-          const float v0 = __uint_as_float(v[cs][j].x), v1 = __uint_as_float(v[cs][j].z);
-          if (e < 2048) {
-            const int r = e >> 7, cc = e & 127;
-            H1[(sr0 + r) * kS1 + cc] = v0; H1[(sr0 + r) * kS1 + cc + 1] = v1;
-          } else if (e < 3072) {
-            const int x = e - 2048, r = x >> 6, cc = x & 63;
-            H2[(sr0 + r) * kS2 + cc] = v0; H2[(sr0 + r) * kS2 + cc + 1] = v1;
-          } else if (e < 4096) {
-            const int x = e - 3072, r = x >> 6, cc = x & 63;
-            DZ2[(sr0 + r) * kS2 + cc] = v0; DZ2[(sr0 + r) * kS2 + cc + 1] = v1;
-          } else {
-            const int x = e - 4096, r = x >> 4, cc = x & 15;
-            DZ3[(sr0 + r) * kS3 + cc] = v0; DZ3[(sr0 + r) * kS3 + cc + 1] = v1;
-          }
+          const int x = tid + j * kThreads;
+          const int xc = x < (kNCH - 1) * kV ? x : 0;
+          const int cs = xc / kV, e = (xc - cs * kV) * 4;
+          const int src = (c + 1 + cs) % kNCH;
+          const int off = (int)((kOffCx * 2 + ((int64_t)par * kNCH + src) * kCXG + e) * 4);
+          v[j] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, kSc1);
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const int x = tid + j * kThreads;
+          if (x >= (kNCH - 1) * kV) continue;
+          const int cs = x / kV, e = (x - cs * kV) * 4;
+          const int sr0 = 16 * ((c + 1 + cs) % kNCH);
+          float* dst;
+          if (e < 2048) dst = H1 + (sr0 + (e >> 7)) * kS1 + (e & 127);
+          else if (e < 3072) dst = H2 + (sr0 + ((e - 2048) >> 6)) * kS2 + ((e - 2048) & 63);
+          else if (e < 4096) dst = DZ2 + (sr0 + ((e - 3072) >> 6)) * kS2 + ((e - 3072) & 63);
+          else dst = DZ3 + (sr0 + ((e - 4096) >> 4)) * kS3 + ((e - 4096) & 15);
+          const f4v f = __builtin_bit_cast(f4v, v[j]);
+          dst[0] = f[0]; dst[1] = f[1]; dst[2] = f[2]; dst[3] = f[3];
         }
       }
     }
     ok = __syncthreads_and(ok ? 1 : 0) != 0;
     if (!ok) break;
-    // dW2 [64 h][128 n] = dZ2^T H1 over the 64 batch rows; wave w: h tile w, 8 n tiles
+    PK_STAMP(1, 4);
+    // dW2 [64 h][128 n] = dZ2^T H1 over the 64 batch rows; wave w: h tile w, 8 n
+    // tiles.  Operands are read from LDS in batches ahead of their MFMAs (one
+    // read per MFMA, issued just before it, would serialise on LDS latency).
     {
       f32x4 g[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int ms = 0; ms < kB / 4; ++ms) {
-        const int m = 4 * ms + q;
-        const float av = DZ2[m * kS2 + 16 * w + i];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) g[t] = mfma_f32_16x16x4(av, H1[m * kS1 + 16 * t + i], g[t]);
+      for (int mb = 0; mb < kB / 4; mb += 4) {
+        float av[4], bv[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = 4 * (mb + u) + q;
+          av[u] = DZ2[m * kS2 + 16 * w + i];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) bv[u][t] = H1[m * kS1 + 16 * t + i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) g[t] = mfma_f32_16x16x4(av[u], bv[u][t], g[t]);
       }
       // dW3 [16 o][64 h] = dZ3^T H2 (o >= 10 rows are zero): wave w -> h tile w
       f32x4 g3 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int ms = 0; ms < kB / 4; ++ms) {
-        const int m = 4 * ms + q;
-        g3 = mfma_f32_16x16x4(DZ3[m * kS3 + i], H2[m * kS2 + 16 * w + i], g3);
+      {
+        float a3[16], b3[16];
+#pragma unroll
+        for (int ms = 0; ms < kB / 4; ++ms) {
+          const int m = 4 * ms + q;
+          a3[ms] = DZ3[m * kS3 + i];
+          b3[ms] = H2[m * kS2 + 16 * w + i];
+        }
+#pragma unroll
+        for (int ms = 0; ms < kB / 4; ++ms) g3 = mfma_f32_16x16x4(a3[ms], b3[ms], g3);
       }
-      // biases: db2[h] (thread h < 64), db3[o] (threads 64..79)
+      // biases: db2[h] (thread h < 64), db3[o] (threads 64..79): 4 partial
+      // sums of 16 rows in flight, then combined in a fixed order
       float db = 0.f;
-      if (tid < kD2) {
-#pragma unroll 8
-        for (int m = 0; m < kB; ++m) db += DZ2[m * kS2 + tid];
-      } else if (tid < kD2 + kD3) {
-#pragma unroll 8
-        for (int m = 0; m < kB; ++m) db += DZ3[m * kS3 + tid - kD2];
+      if (tid < kD2 + kD3) {
+        const float* src = tid < kD2 ? DZ2 + tid : DZ3 + (tid - kD2);
+        const int st = tid < kD2 ? kS2 : kS3;
+        float p4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < kB; ++m) p4[m & 3] += src[m * st];
+        db = (p4[0] + p4[1]) + (p4[2] + p4[3]);
       }
       // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above)
 #pragma unroll
@@ -596,6 +648,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       else if (tid < kD2 + kD3) B3[tid - kD2] -= a.lr * db;
     }
     __syncthreads();
+    PK_STAMP(1, 5);
   }
 
   // ---- epilogue: stats; chain 0 writes W2, b2, W3, b3 back ----
@@ -628,6 +681,16 @@ void mlp_persist_k(PersistArgs a) {
     pk_layer1(a, lds, blockIdx.x);
   else
     pk_chain(a, lds, blockIdx.x - kNL1);
+}
+
+hipError_t mlp_persist_read_stamps(uint64_t* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pk_stamps), sizeof(uint64_t) * 3 * 8 * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+void mlp_persist_set_stamping(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
 }
 
 bool mlp_persist_supported(const MlpDesc& d) {

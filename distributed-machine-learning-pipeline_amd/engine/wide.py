@@ -88,13 +88,19 @@ class WideMlpTrainer:
         self.tctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
         self.steps_done = 0
         # One hipGraph per epoch (every batch offset baked in): replaying it
-        # removes the ~25 host launches per step.  Single replica only (the
-        # RCCL collective stays outside graphs).
-        self.graph_enabled = graph and not self.ctx.is_distributed
-        self._graph = None
+        # removes the ~25 host launches per step.  With several replicas the
+        # per-layer RCCL all-reduces and updates on the comm stream are
+        # captured too (fork/join of the comm stream inside the capture); only
+        # the torch.distributed fallback (sync='torch', e.g. gloo) stays eager.
+        import os
+
         self.comm = None
         if self.ctx.is_distributed and sync in ("rccl", "ring"):
             self.comm = make_native_comm(self.ctx)
+        capture_comm = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "1") != "0"
+        self.graph_enabled = graph and (not self.ctx.is_distributed or
+                                        (self.comm is not None and capture_comm))
+        self._graph = None
         # per-layer gradient buckets (W_l and b_l plus any padding between them) and
         # the stream their all-reduce + SGD run on, overlapped with the backward
         lay = self.layout
@@ -196,7 +202,22 @@ class WideMlpTrainer:
             C.sgd_cast(W, gW, d[l + 1], d[l], scale, self.Wb[l], self.WbT[l])
             C.sgd_update_(b, gb, scale)
 
+    def _warm_comm(self) -> None:
+        """Every bucket's collective once, eagerly, before any capture: RCCL
+        sets up its channels / peer connections on the first call of a shape,
+        and that host-side setup must not happen inside a stream capture.  G
+        is scratch (rewritten by every step's weight-gradient GEMMs)."""
+        if self.comm is None:
+            return
+        with torch.cuda.stream(self._cs):
+            for lo, hi in self._gspan:
+                g = self.G[lo:hi]
+                (self.comm.ring_allreduce_(g, 0, 4 << 20) if self.sync == "ring"
+                 else self.comm.allreduce_(g, 0))
+        torch.cuda.synchronize(self.device)
+
     def _capture_epoch(self) -> None:
+        self._warm_comm()
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
         stream.wait_stream(torch.cuda.current_stream(self.device))
