@@ -623,16 +623,20 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 #pragma unroll
         for (int ms = 0; ms < kB / 4; ++ms) g3 = mfma_f32_16x16x4(a3[ms], b3[ms], g3);
       }
-      // biases: db2[h] (thread h < 64), db3[o] (threads 64..79): 4 partial
-      // sums of 16 rows in flight, then combined in a fixed order
-      float db = 0.f;
-      if (tid < kD2 + kD3) {
-        const float* src = tid < kD2 ? DZ2 + tid : DZ3 + (tid - kD2);
-        const int st = tid < kD2 ? kS2 : kS3;
-        float p4[4] = {0.f, 0.f, 0.f, 0.f};
+      // biases through the MFMA pipe: dZ2^T . ones (wave w: h tile w) and
+      // dZ3^T . ones (wave 0) — 16 MFMAs each instead of a 64-deep serial sum
+      f32x4 gb2 = {0.f, 0.f, 0.f, 0.f}, gb3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int m = 0; m < kB; ++m) p4[m & 3] += src[m * st];
-        db = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      for (int ms = 0; ms < kB / 4; ++ms) {
+        const int m = 4 * ms + q;
+        gb2 = mfma_f32_16x16x4(DZ2[m * kS2 + 16 * w + i], 1.f, gb2);
+      }
+      if (w == 0) {
+#pragma unroll
+        for (int ms = 0; ms < kB / 4; ++ms) {
+          const int m = 4 * ms + q;
+          gb3 = mfma_f32_16x16x4(DZ3[m * kS3 + i], 1.f, gb3);
+        }
       }
       // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above)
 #pragma unroll
@@ -644,8 +648,15 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         const int o = 4 * q + r;
         if (o < kD3) W3[o * kS2 + 16 * w + i] -= a.lr * g3[r];
       }
-      if (tid < kD2) B2[tid] -= a.lr * db;
-      else if (tid < kD2 + kD3) B3[tid - kD2] -= a.lr * db;
+      if (i == 0) {  // every column of the ones-product holds the sum
+#pragma unroll
+        for (int r = 0; r < 4; ++r) B2[16 * w + 4 * q + r] -= a.lr * gb2[r];
+        if (w == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (4 * q + r < kD3) B3[4 * q + r] -= a.lr * gb3[r];
+        }
+      }
     }
     __syncthreads();
     PK_STAMP(1, 5);
