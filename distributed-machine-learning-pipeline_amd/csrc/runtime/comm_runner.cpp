@@ -220,6 +220,7 @@ bool MlpRunner::captured(int steps) const {
 }
 
 void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
+  if (c != nullptr && c->nranks() > 1) pk_xb_ = nullptr;  // the persistent step is single-replica
   comm_ = c;
   algo_ = algo;
   chunk_bytes_ = chunk_bytes;
@@ -234,6 +235,7 @@ void MlpRunner::set_exchange(PeerExchange* x) {
     if (x->ntiles() != mlp_wgrad_tiles(d_) || x->half() < b_.nparams)
       throw std::invalid_argument("set_exchange: exchange buffers sized for another model");
   }
+  if (x != nullptr) pk_xb_ = nullptr;  // the persistent step is single-replica
   xchg_ = x;
   xact_ = false;
   reset_graph();
@@ -256,6 +258,7 @@ void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xst
     throw std::invalid_argument("set_act_exchange: exchange buffers sized for another model");
   if (Xall == nullptr || xstride < (int64_t)d_.nbatches * 64 * d_.dims[0])
     throw std::invalid_argument("set_act_exchange: replicated input shards too small");
+  pk_xb_ = nullptr;  // the persistent step is single-replica
   xchg_ = x;
   xact_ = true;
   if (waves != 0 && waves != 4 && waves != 8)

@@ -349,7 +349,7 @@ class MlpTrainer:
     @property
     def persistent(self) -> bool:
         """Steps run as one persistent launch per train_steps call."""
-        return self.runner is not None and self.pk_buf is not None
+        return self.runner is not None and self.pk_buf is not None and self.runner.persist_active()
 
     def _rewound(self) -> None:
         """The step counter went back: stale hand-off tags could match again."""
