@@ -106,6 +106,7 @@ struct PyMlpRunner {
   std::unique_ptr<MlpRunner> r;
   hipStream_t stream = nullptr;
   bool own_stream = true;
+  bool follow = false;  // run on torch's current stream at each call
   int device = 0;
 
   // stream_handle != 0: run on that (caller-owned) stream instead of a fresh
@@ -114,10 +115,14 @@ struct PyMlpRunner {
   // GPU_MAX_HW_QUEUES, so such groups take streams from a pool created back to
   // back once per process (parallel/xchg.py replica_streams) rather than
   // whatever queue a stream created later in a long process lands on.
+  // follow_torch: every call runs on torch's CURRENT stream (PyTorch's own
+  // convention), so work the caller enqueued before is ordered ahead of the
+  // steps by the stream itself -- no cross-queue event edge per call.  The
+  // runner's own stream is then used only to capture graphs.
   PyMlpRunner(const std::vector<int64_t>& desc, torch::Tensor X, torch::Tensor labels,
               torch::Tensor P, torch::Tensor G, torch::Tensor V, torch::Tensor ws,
               torch::Tensor slab, torch::Tensor ctr, torch::Tensor stats, float lr, float momentum,
-              float weight_decay, uintptr_t stream_handle) {
+              float weight_decay, uintptr_t stream_handle, bool follow_torch) {
     d = desc_from_list(desc);
     check_f32(X, "X");
     check_f32(P, "params");
@@ -165,55 +170,71 @@ struct PyMlpRunner {
       own_stream = false;
     } else {
       hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+      follow = follow_torch;
     }
     r = std::make_unique<MlpRunner>(d, b, lr, momentum, weight_decay);
   }
   ~PyMlpRunner() {
+    if (follow) (void)hipStreamSynchronize(cur_stream());
     r.reset();
-    if (stream && own_stream) {
-      (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
-    }
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (stream && own_stream) (void)hipStreamDestroy(stream);
   }
   // All runner work goes on the runner's own stream; join with torch's stream
   // first so tensors initialised by torch are visible.
+  // Reused events for the two stream edges (no create/destroy per call).
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipEvent_t edge_event(hipEvent_t& e) {
+    if (e == nullptr)
+      hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return e;
+  }
+  hipStream_t run_stream() const { return follow ? cur_stream() : stream; }
   void join_torch() {
-    hipEvent_t e;
-    hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    if (follow) return;
+    hipEvent_t e = edge_event(ev_in);
     hip_ok(hipEventRecord(e, cur_stream()), "hipEventRecord");
     hip_ok(hipStreamWaitEvent(stream, e, 0), "hipStreamWaitEvent");
-    hip_ok(hipEventDestroy(e), "hipEventDestroy");
   }
   // The reverse edge: torch's current stream waits for everything enqueued on
   // the runner's stream.  A host-side synchronize alone is not enough for a
   // consumer on another queue: with per-XCD L2s it can still read lines it
   // cached before the runner's kernels wrote them back (tests/test_gpu_xchg.py).
   void join_into_torch() {
-    hipEvent_t e;
-    hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    if (follow) return;
+    hipEvent_t e = edge_event(ev_out);
     hip_ok(hipEventRecord(e, stream), "hipEventRecord");
     hip_ok(hipStreamWaitEvent(cur_stream(), e, 0), "hipStreamWaitEvent");
-    hip_ok(hipEventDestroy(e), "hipEventDestroy");
   }
-  void step(int n) {
-    join_torch();
-    r->enqueue_steps(n, stream);
+  // join = false: the caller knows torch enqueued nothing the steps read since
+  // the last join (saves the cross-queue barrier packet).
+  void step(int n, bool join) {
+    if (join) join_torch();
+    r->enqueue_steps(n, run_stream());
   }
-  void fwd_bwd() { join_torch(); r->enqueue_fwd_bwd(stream); }
-  void update() { join_torch(); r->enqueue_update(stream); }
+  void fwd_bwd() { join_torch(); r->enqueue_fwd_bwd(run_stream()); }
+  void update() { join_torch(); r->enqueue_update(run_stream()); }
+  // Graphs are captured on the runner's own stream (never the legacy null
+  // stream) after it has caught up with torch's current stream.
   void capture(int steps, bool capture_comm) {
-    join_torch();
+    hipEvent_t e = edge_event(ev_in);
+    hip_ok(hipEventRecord(e, cur_stream()), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(stream, e, 0), "hipStreamWaitEvent");
     hip_ok(hipStreamSynchronize(stream), "sync");
     r->capture(steps, capture_comm, stream);
   }
   void replay(int times, int steps) {
-    for (int i = 0; i < times; ++i) r->replay(stream, steps);
+    hipStream_t s = run_stream();
+    for (int i = 0; i < times; ++i) r->replay(s, steps);
   }
   void synchronize() {
+    hipStream_t s = run_stream();
     py::gil_scoped_release nogil;
-    hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
   }
-  uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(stream); }
+  uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(run_stream()); }
 };
 
 struct PyComm {
@@ -545,11 +566,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<PyMlpRunner>(m, "MlpRunner")
       .def(py::init<const std::vector<int64_t>&, torch::Tensor, torch::Tensor, torch::Tensor,
                     torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
-                    torch::Tensor, float, float, float, uintptr_t>(),
+                    torch::Tensor, float, float, float, uintptr_t, bool>(),
            py::arg("desc"), py::arg("X"), py::arg("labels"), py::arg("P"), py::arg("G"),
            py::arg("V"), py::arg("ws"), py::arg("slab"), py::arg("ctr"), py::arg("stats"),
-           py::arg("lr"), py::arg("momentum"), py::arg("weight_decay"), py::arg("stream") = 0)
-      .def("step", &PyMlpRunner::step, py::arg("n") = 1)
+           py::arg("lr"), py::arg("momentum"), py::arg("weight_decay"), py::arg("stream") = 0,
+           py::arg("follow_torch") = false)
+      .def_property_readonly("follows_torch", [](PyMlpRunner& s) { return s.follow; })
+      .def("step", &PyMlpRunner::step, py::arg("n") = 1, py::arg("join") = true)
       .def("fwd_bwd", &PyMlpRunner::fwd_bwd)
       .def("update", &PyMlpRunner::update)
       .def("capture", &PyMlpRunner::capture, py::arg("steps"), py::arg("capture_comm") = true)
@@ -591,6 +614,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                          reinterpret_cast<uint32_t*>(err->data_ptr<int32_t>()), timeout_ms);
       }, py::arg("xbuf").none(true), py::arg("err") = py::none(), py::arg("timeout_ms") = 2000.0)
       .def("persist_active", [](PyMlpRunner& s) { return s.r->persist_active(); })
+      .def("persist_failed", [](PyMlpRunner& s) { return s.r->persist_failed(); },
+           "a persistent launch gave up on a hand-off (valid after a sync; no device copy)")
+      .def("clear_persist_error", [](PyMlpRunner& s) { s.r->clear_persist_error(); })
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
       .def("exchange_mode", [](PyMlpRunner& s) { return s.r->exchange_mode(); })
       .def("plan", [](PyMlpRunner& s) {

@@ -95,7 +95,8 @@ void mlp_persist_set_stamping(bool on);
 int64_t mlp_persist_xbuf_granules();
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
-                             float* stats, uint32_t* err, uint64_t timeout_ticks, hipStream_t s);
+                             float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
+                             hipStream_t s);
 
 // ---- peer exchange: gradient all-reduce fused into K_C over xGMI -------------
 // Every replica's K_C publishes each weight-gradient tile into its own

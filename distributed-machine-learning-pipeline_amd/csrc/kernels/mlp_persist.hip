@@ -155,6 +155,13 @@ __device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
 // 2 = layer-2 gradients.
 __device__ uint64_t g_pk_stamps[3][8][8];
 __device__ int g_pk_stamp_on;
+// Role 2, row 0 holds launch-level stamps: [0] layer-1 block 0 entry, [1] its
+// prologue done, [2] its exit; [3] chain 0 entry, [4] prologue done, [5] exit.
+#define PK_EDGE(ph)                                                                   \
+  do {                                                                                \
+    if (g_pk_stamp_on && threadIdx.x == 0)                                            \
+      g_pk_stamps[2][0][(ph)] = __builtin_amdgcn_s_memrealtime();                     \
+  } while (0)
 #define PK_STAMP(role, ph)                                                            \
   do {                                                                                \
     if (stamp_on && threadIdx.x == 0 && it >= 8 && it < 16)                            \
@@ -175,8 +182,16 @@ struct PersistArgs {
   uint64_t* xb;  // exchange granules (kTotalG)
   float* stats;
   uint32_t* err;
+  uint32_t* herr;  // host-mapped mirror of err (nullable): read without a copy
   uint64_t timeout_ticks;
 };
+
+// A block that gave up leaves a mark in host memory on its way out, so the
+// host learns the launch failed without a device->host copy.
+__device__ __forceinline__ void pk_report(const PersistArgs& a, bool ok) {
+  if (!ok && threadIdx.x == 0 && a.herr != nullptr)
+    __hip_atomic_store(a.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // -----------------------------------------------------------------------------
 // Layer-1 block
@@ -213,6 +228,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   float* Dz = lds + L1Lay::DZ;
   float* B1 = lds + L1Lay::B1;
 
+  if (lb == 0) PK_EDGE(0);
   // ---- prologue: W1 tile, b1 slice, X of the first step ----
   const float* W1g = a.P + a.w_off[0];
   for (int e = tid; e < 16 * (kKC / 4); e += kThreads) {
@@ -225,6 +241,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   constexpr int kXPer = (kXF4 + kThreads - 1) / kThreads;  // 13
   pk_glds_x(a, lds, 0, s0, lane, w, k0);
   __syncthreads();
+  if (lb == 0) PK_EDGE(1);
 
   bool ok = true;
   const int stamp_on = g_pk_stamp_on && lb == 0;
@@ -346,6 +363,8 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
         *reinterpret_cast<const float4*>(Wl + r * kXS + 4 * c4);
   }
   if (gk == 0 && tid < 16) a.P[a.b_off[0] + n0 + tid] = B1[tid];
+  pk_report(a, ok);
+  if (lb == 0) PK_EDGE(2);
 }
 
 // -----------------------------------------------------------------------------
@@ -368,6 +387,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   float* DZ3 = lds + ChLay::DZ3;
   float* RED = lds + ChLay::RED;
 
+  if (c == 0) PK_EDGE(3);
   // ---- prologue: W2, W3 (rows padded to 16 with zeros), b2, b3 ----
   for (int e = tid; e < kD2 * (kD1 / 4); e += kThreads) {
     const int r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
@@ -383,6 +403,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   for (int e = tid; e < kB * kS3; e += kThreads) DZ3[e] = 0.f;
   float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
   __syncthreads();
+  if (c == 0) PK_EDGE(4);
 
   bool ok = true;
   const int stamp_on = g_pk_stamp_on && c == 0;
@@ -682,6 +703,8 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     if (tid < kD2) a.P[a.b_off[1] + tid] = B2[tid];
     if (tid < kD3) a.P[a.b_off[2] + tid] = B3[tid];
   }
+  pk_report(a, ok);
+  if (c == 0) PK_EDGE(5);
 }
 
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -713,7 +736,8 @@ int64_t mlp_persist_xbuf_granules() { return kTotalG; }
 
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
-                             float* stats, uint32_t* err, uint64_t timeout_ticks, hipStream_t s) {
+                             float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
+                             hipStream_t s) {
   if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
       (ldx % 4) != 0)
     return hipErrorInvalidValue;
@@ -734,6 +758,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   a.xb = xb;
   a.stats = stats;
   a.err = err;
+  a.herr = herr;
   a.timeout_ticks = timeout_ticks;
   const size_t lds = (size_t)kLdsFloats * sizeof(float);
   static bool attr = false;

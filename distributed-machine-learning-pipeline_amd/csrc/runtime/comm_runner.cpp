@@ -203,7 +203,18 @@ MlpRunner::MlpRunner(const MlpDesc& d, const MlpBuffers& b, float lr, float mome
     throw std::invalid_argument("momentum/weight decay need a velocity buffer");
 }
 
-MlpRunner::~MlpRunner() { reset_graph(); }
+MlpRunner::~MlpRunner() {
+  reset_graph();
+  if (pk_herr_ != nullptr) (void)hipHostFree(pk_herr_);
+}
+
+bool MlpRunner::persist_failed() const {
+  return pk_herr_ != nullptr && __atomic_load_n(pk_herr_, __ATOMIC_ACQUIRE) != 0u;
+}
+
+void MlpRunner::clear_persist_error() {
+  if (pk_herr_ != nullptr) __atomic_store_n(pk_herr_, 0u, __ATOMIC_RELEASE);
+}
 
 void MlpRunner::reset_graph() {
   for (auto& kv : graphs_) {
@@ -309,6 +320,12 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms) {
   if (comm_ != nullptr || xchg_ != nullptr || world_ != 1)
     throw std::invalid_argument("set_persist: single replica only");
   if (err == nullptr) throw std::invalid_argument("set_persist: needs an error word");
+  if (pk_herr_ == nullptr) {
+    void* h = nullptr;
+    DSML_HIP_CHECK(hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    pk_herr_ = static_cast<uint32_t*>(h);
+    *pk_herr_ = 0u;
+  }
   pk_xb_ = xbuf;
   pk_err_ = err;
   pk_timeout_ = (uint64_t)(timeout_ms * 1e5);  // s_memrealtime: 100 MHz
@@ -319,7 +336,7 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
   if (n <= 0) return;
   if (pk_xb_ != nullptr) {
     DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
-                                     b_.stats, pk_err_, pk_timeout_, s));
+                                     b_.stats, pk_err_, pk_herr_, pk_timeout_, s));
     return;
   }
   for (int i = 0; i < n; ++i) enqueue_step(s);

@@ -275,6 +275,10 @@ class MlpRunner {
   // is ONE launch.  Single replica, plain SGD, the flagship shape only.
   void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms);
   bool persist_active() const { return pk_xb_ != nullptr; }
+  // Whether a persistent launch gave up on a hand-off (read from host-mapped
+  // memory the kernel marks on the way out: valid after a stream sync, no copy).
+  bool persist_failed() const;
+  void clear_persist_error();
   // Enqueue n full steps (one launch in persistent mode).
   void enqueue_steps(int n, hipStream_t s);
   bool exchange_active() const { return xchg_ != nullptr; }
@@ -315,6 +319,7 @@ class MlpRunner {
   int xact_waves_ = 0;
   uint64_t* pk_xb_ = nullptr;
   uint32_t* pk_err_ = nullptr;
+  uint32_t* pk_herr_ = nullptr;  // hipHostMalloc'd, device-visible
   uint64_t pk_timeout_ = 0;
   int algo_ = 0;
   int world_ = 1;

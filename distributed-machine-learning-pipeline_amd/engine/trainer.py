@@ -119,7 +119,9 @@ class MlpTrainer:
         self.Xall: Optional[torch.Tensor] = None
         self._exchanges: Dict[str, object] = {}
         self.runner = None
-        self._stream = stream  # caller-owned stream for the native runner (None: its own)
+        # caller-owned stream for the native runner; None: the runner follows
+        # torch's current stream at every call (no cross-stream edges per step)
+        self._stream = stream
         # persistent fused step (kernels/mlp_persist.hip): None = when supported
         # (single replica, plain SGD, 784-128-64-10 @ 64); HIPDSML_PERSIST=0 disables
         if persist is None:
@@ -151,7 +153,8 @@ class MlpTrainer:
         self.runner = C.MlpRunner(self.layout.desc_list(), self.X, self.y, self.P, self.G, self.V,
                                   self.ws, self.slab, self.ctr, self.stats, self.lr, self.momentum,
                                   self.weight_decay,
-                                  stream=self._stream.cuda_stream if self._stream is not None else 0)
+                                  stream=self._stream.cuda_stream if self._stream is not None else 0,
+                                  follow_torch=self._stream is None)
         self.runner.set_world_size(self.ctx.world_size)
         self._ring_chunk = int(ring_chunk_bytes)
         self._collective_warm = False  # an eager collective step has run (RCCL connected)
@@ -338,7 +341,10 @@ class MlpTrainer:
     def _hip_step_torch_sync(self, n: int) -> None:
         import torch.distributed as dist
 
-        stream = torch.cuda.ExternalStream(self.runner.stream_handle(), device=self.device)
+        if self.runner.follows_torch:
+            stream = torch.cuda.current_stream(self.device)
+        else:
+            stream = torch.cuda.ExternalStream(self.runner.stream_handle(), device=self.device)
         for _ in range(n):
             self.runner.fwd_bwd()
             with torch.cuda.stream(stream):
@@ -356,6 +362,7 @@ class MlpTrainer:
         if self.pk_buf is not None:
             self.pk_buf.zero_()
             self.pk_err.zero_()
+            self.runner.clear_persist_error()
 
     def _graphs_on(self) -> bool:
         """Whether train_steps replays hipGraphs for the active sync mode."""
@@ -427,10 +434,10 @@ class MlpTrainer:
                     from ..parallel.xchg import check
 
                     check(self.xchg)
-                if self.pk_err is not None and int(self.pk_err.item()) != 0:
+                if self.pk_buf is not None and self.runner.persist_failed():
                     raise RuntimeError("persistent step: an on-chip hand-off timed out "
                                        "(launch ended early; parameters are not valid)")
-            if self.device.type == "cuda":
+            elif self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:

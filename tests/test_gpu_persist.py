@@ -91,3 +91,23 @@ def test_persistent_long_run_converges():
     last = t.read_stats()
     assert last.avg_loss < first.avg_loss
     assert torch.isfinite(t.P).all()
+
+
+def test_persistent_handoff_timeout_is_reported_and_recoverable():
+    """A hand-off wait past its bound ends the launch on every block (err word)
+    and the host sees it through the host-mapped mirror, without a copy."""
+    ds = synthetic_mnist(64 * 4, seed=15)
+    t = _tr(ds, True)
+    t.runner.set_persist(t.pk_buf, t.pk_err, 1e-4)  # 10 ticks: the first wait gives up
+    t.train_steps(5)
+    with pytest.raises(RuntimeError, match="hand-off timed out"):
+        t.synchronize()
+    assert t.runner.persist_failed() and int(t.pk_err.item()) != 0
+    # rearm with a sane bound: the job can restart from a checkpoint
+    t.runner.set_persist(t.pk_buf, t.pk_err, 2000.0)
+    t._rewound()
+    t.ctr.zero_()
+    torch.cuda.synchronize()  # the runner's stream does not wait on torch's
+    t.train_steps(3)
+    t.synchronize()
+    assert not t.runner.persist_failed()
