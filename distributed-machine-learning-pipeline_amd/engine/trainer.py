@@ -304,6 +304,8 @@ class MlpTrainer:
         for m in modes:
             if m in EXCHANGE_MODES and m not in self._exchanges:
                 continue
+            if m == "xact" and self.Xall is None:
+                continue  # its replicated inputs were released when another mode won
             if m in ("rccl", "ring") and self.comm is None:
                 continue
             self._set_mode(m)
