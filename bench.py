@@ -47,21 +47,22 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _launch(a, argv) -> int:
+def _launch(a, argv, script: str = "") -> int:
     """Parent of an N-rank run: count GPUs (no GPU initialisation), start one
-    rank per GPU through torch.distributed.run, return its exit code."""
+    rank per GPU (of `script`, default this file) through
+    torch.distributed.run, return its exit code."""
     n = a.gpus
-    if not a.cpu_dry_run:
+    if not getattr(a, "cpu_dry_run", False):
         import torch
 
         vis = torch.cuda.device_count()  # does not initialise the GPU
-        need = 1 if a.rehearse_one_gpu else n
+        need = 1 if getattr(a, "rehearse_one_gpu", False) else n
         if vis < need:
             print(f"bench.py: --gpus {n} needs {need} visible GPUs, found {vis}", file=sys.stderr)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.abspath(__file__)] + list(argv)
+           os.path.abspath(script or __file__)] + list(argv)
     env = dict(os.environ, **{_LAUNCHED: "1"})
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")

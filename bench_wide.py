@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """BASELINE config 4: wide MLP 784-4096-4096-10, bf16 MFMA GEMMs, data-parallel.
-Same launch contract as bench.py (torchrun for N>1); prints one JSON line."""
+Same launch contract as bench.py: `--gpus N` > 1 without a launcher starts N
+ranks itself (bench._launch: the parent never touches the GPU, fewer visible
+GPUs is rc 2); prints one JSON line."""
 import argparse
 import json
 import os
@@ -19,7 +21,15 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--sync", default="rccl", choices=["rccl", "ring", "torch"])
     a = ap.parse_args()
-    import torch
+    import bench
+
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not os.environ.get(bench._LAUNCHED):
+        return bench._launch(a, sys.argv[1:], script=__file__)
+    if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        print(f"bench_wide.py: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}",
+              file=sys.stderr)
+        return 2
+    import torch  # noqa: F401
 
     from hipdsml.data.mnist import synthetic_mnist
     from hipdsml.engine.wide import WideMlpTrainer

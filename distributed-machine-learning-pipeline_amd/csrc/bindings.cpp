@@ -470,6 +470,86 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
      py::arg("sgdW") = py::none(), py::arg("lr") = 0.0, py::arg("splits") = 1,
      py::arg("ws") = py::none(), py::arg("ctr") = py::none(), py::arg("bgrad") = py::none(),
      py::arg("bsgd") = py::none());
+  m.def("gemm_skinny", [bf16p](torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, int64_t K, bool nn,
+                              double alpha, c10::optional<torch::Tensor> bias, bool relu,
+                              c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
+                              c10::optional<torch::Tensor> obf, c10::optional<torch::Tensor> obfT,
+                              int64_t splits, c10::optional<torch::Tensor> ws,
+                              c10::optional<torch::Tensor> ctr) {
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A, B 2-D rows");
+    TORCH_CHECK(A.size(0) >= M && A.size(1) >= K, "A too small");
+    TORCH_CHECK(nn ? (B.size(0) >= K && B.size(1) >= N) : (B.size(0) >= N && B.size(1) >= K), "B too small");
+    auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
+    };
+    GemmEpi e{};
+    e.alpha = (float)alpha;
+    e.relu = relu ? 1 : 0;
+    if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= N, "bias"); e.bias = bias->data_ptr<float>(); }
+    if (mask) { chk2(*mask, M, N, "mask"); e.mask = bf16p(*mask, "mask"); e.ldm = mask->stride(0); }
+    if (of32) { chk2(*of32, M, N, "of32"); TORCH_CHECK(of32->scalar_type() == torch::kFloat32, "of32 f32");
+                e.of32 = of32->data_ptr<float>(); e.ldo = of32->stride(0); }
+    if (obf) { chk2(*obf, M, N, "obf"); e.obf = bf16p(*obf, "obf"); e.ldb = obf->stride(0); }
+    if (obfT) { chk2(*obfT, N, M, "obfT"); e.obfT = bf16p(*obfT, "obfT"); e.ldt = obfT->stride(0); }
+    const int S = gemm_skinny_splits((int)M, (int)N, (int)K, (int)splits);
+    float* cp = nullptr;
+    int* tc = nullptr;
+    if (S > 1) {
+      TORCH_CHECK(ws && ctr, "split-K skinny GEMM needs ws (slabs) and ctr (tile counters)");
+      check_f32(*ws, "ws");
+      const int64_t tiles = ((N + 63) / 64) * ((M + 63) / 64);
+      TORCH_CHECK(ws->numel() >= (int64_t)S * tiles * 4096, "ws too small: need ", (int64_t)S * tiles * 4096);
+      check_cuda(*ctr, "ctr");
+      TORCH_CHECK(ctr->scalar_type() == torch::kInt32 && ctr->numel() >= tiles, "ctr: int32, one per 64x64 tile");
+      cp = ws->data_ptr<float>();
+      tc = ctr->data_ptr<int32_t>();
+    }
+    hip_ok(gemm_skinny(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), (int)M, (int)N, (int)K, nn,
+                       (int)splits, cp, tc, e, cur_stream()), "gemm_skinny");
+    return S;
+  }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("nn") = false,
+     py::arg("alpha") = 1.0, py::arg("bias") = py::none(), py::arg("relu") = false,
+     py::arg("mask") = py::none(), py::arg("of32") = py::none(), py::arg("obf") = py::none(),
+     py::arg("obfT") = py::none(), py::arg("splits") = 0, py::arg("ws") = py::none(),
+     py::arg("ctr") = py::none());
+  m.def("wgrad_sgd", [bf16p](torch::Tensor Z, torch::Tensor X, int64_t M, int64_t N, int64_t K, double alpha,
+                            double lr, c10::optional<torch::Tensor> W, c10::optional<torch::Tensor> Wb,
+                            c10::optional<torch::Tensor> G, c10::optional<torch::Tensor> bias,
+                            c10::optional<torch::Tensor> bgrad) {
+    TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
+    TORCH_CHECK(Z.size(0) >= M && X.size(0) >= M && Z.size(1) >= ((N + 7) / 8) * 8 &&
+                X.size(1) >= ((K + 7) / 8) * 8, "Z / X too small (rows padded to 8 columns)");
+    auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
+    };
+    float* w = nullptr; int64_t ldw = 0;
+    uint16_t* wb = nullptr; int64_t ldwb = 0;
+    float* g = nullptr; int64_t ldg = 0;
+    if (W) { chk2(*W, N, K, "W"); TORCH_CHECK(W->scalar_type() == torch::kFloat32, "W f32"); w = W->data_ptr<float>(); ldw = W->stride(0); }
+    if (Wb) { chk2(*Wb, N, K, "Wb"); wb = bf16p(*Wb, "Wb"); ldwb = Wb->stride(0); }
+    if (G) { chk2(*G, N, K, "G"); TORCH_CHECK(G->scalar_type() == torch::kFloat32, "G f32"); g = G->data_ptr<float>(); ldg = G->stride(0); }
+    float* b = nullptr; float* bg = nullptr;
+    if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= N, "bias"); b = bias->data_ptr<float>(); }
+    if (bgrad) { check_f32(*bgrad, "bgrad"); TORCH_CHECK(bgrad->numel() >= N, "bgrad"); bg = bgrad->data_ptr<float>(); }
+    hip_ok(wgrad_sgd(bf16p(Z, "Z"), Z.stride(0), bf16p(X, "X"), X.stride(0), (int)M, (int)N, (int)K, (float)alpha,
+                     (float)lr, w, ldw, wb, ldwb, g, ldg, b, bg, cur_stream()), "wgrad_sgd");
+  }, py::arg("Z"), py::arg("X"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("alpha") = 1.0,
+     py::arg("lr") = 0.0, py::arg("W") = py::none(), py::arg("Wb") = py::none(), py::arg("G") = py::none(),
+     py::arg("bias") = py::none(), py::arg("bgrad") = py::none());
+  m.def("head_stamps", []() {
+    std::vector<uint64_t> v(64 * 6);
+    hip_ok(head_read_stamps(v.data()), "head_read_stamps");
+    return v;
+  });
+  m.def("head_set_stamping", &head_set_stamping);
+  m.def("gemm_skinny_stamps", []() {
+    std::vector<uint64_t> v(1024 * 5);
+    hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");
+    return v;
+  });
+  m.def("gemm_skinny_set_stamping", &gemm_skinny_set_stamping);
+  m.def("gemm_skinny_splits", &gemm_skinny_splits, py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("splits") = 0);
   m.def("sgd_cast", [bf16p](torch::Tensor W, c10::optional<torch::Tensor> G, int64_t N, int64_t K, double lr,
                            torch::Tensor Wb, c10::optional<torch::Tensor> WbT) {
     check_f32(W, "W");

@@ -229,6 +229,27 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp = nullptr, int64_t ldzp = 0, uint16_t* dzpT = nullptr,
                              int64_t ldpt = 0);
+// Skinny GEMMs (kernels/gemm_skinny.hip): C[M x N] = A[M x K] . B^T for
+// B [N x K] (nn = false) or A . B for B [K x N] (nn = true: W read in its
+// stored layout through transposing LDS reads), 64 x 64 tiles, K split S ways
+// (splits <= 0: auto, >= 256 workgroups) with the last-arriving slice reducing
+// and applying `epi` (no sgdW / bgrad / bsgd).  slabs: S * tiles * 4096 fp32,
+// tile_ctr: one zeroed int per 64 x 64 tile (left zero).  K, N multiples of 8.
+int gemm_skinny_splits(int M, int N, int K, int splits);
+hipError_t gemm_skinny_read_stamps(uint64_t* host_out);  // [1024][5], profiling only
+void gemm_skinny_set_stamping(bool on);
+hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N,
+                       int K, bool nn, int splits, float* slabs, int* tile_ctr, const GemmEpi& epi,
+                       hipStream_t s);
+// Weight gradient from row-major activations (kernels/wgrad_sgd.hip):
+// G = alpha * Z^T X (Z [M x N], X [M x K] bf16, rows padded to 8 columns), then
+// W -= lr * G (+ bf16 copy Wb) when W is given, else G written out; bias -= lr
+// * alpha * colsum(Z) and/or bgrad = alpha * colsum(Z).  K % 4 == 0.
+hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t ldx, int M, int N,
+                     int K, float alpha, float lr, float* W, int64_t ldw, uint16_t* Wb, int64_t ldwb,
+                     float* G, int64_t ldg, float* bias, float* bgrad, hipStream_t s);
+hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
+void head_set_stamping(bool on);
 hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
                        float lr, hipStream_t s);
 hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,

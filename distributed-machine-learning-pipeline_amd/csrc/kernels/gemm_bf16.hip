@@ -716,6 +716,12 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 // Fused classifier head: logits[m][c] = H[m] . W[c] + b[c] for C <= 16
 // classes, then softmax-CE as softmax_xent_k — one 256-thread block per row.
 // Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
+__device__ uint64_t g_head_stamps[64][6];
+__device__ int g_head_stamp_on;
+#define HEAD_STAMP(k)                                                               \
+  do {                                                                              \
+    if (g_head_stamp_on && t == 0 && m < 64) g_head_stamps[m][(k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 constexpr int kHeadMaxC = 16;
 constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
 __global__ __launch_bounds__(256) void head_softmax_xent_k(
@@ -729,6 +735,10 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   __shared__ float gz[kHeadMaxC];         // bf16-rounded dLogits of this row
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* hr = H + (int64_t)m * ldh;
+  // the softmax's own operands go out with the first loads (not after the reduction)
+  HEAD_STAMP(0);
+  const int y = labels[m];
+  const float bc = (bias && lane < C) ? bias[lane] : 0.f;
   // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
   uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][kHeadMaxC];
 #pragma unroll
@@ -755,10 +765,11 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
                 h[4] * bf16lo(x.z) + h[5] * bf16hi(x.z) + h[6] * bf16lo(x.w) + h[7] * bf16hi(x.w);
     }
   }
+  HEAD_STAMP(1);
   // block reduction per class: LDS transpose, then one 16-lane DPP row per class
 #pragma unroll
   for (int c = 0; c < kHeadMaxC; ++c) part[c][t] = acc[c];
-  __syncthreads();
+  lds_barrier();  // LDS only: no wait for this block's global stores
   {
     const int c = t >> 4, sg = t & 15;  // class c = row of 16 lanes; 16 partials per lane
     float v = 0.f;
@@ -767,14 +778,14 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     v = row16_sum(v);
     if (sg == 0) zsum[c] = v;
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: no wait for this block's global stores
+  HEAD_STAMP(2);
   if (w == 0) {
     const int c = lane;
     const bool cv = c < C;
     float z = -3.402823466e38f;
-    if (cv) z = zsum[c] + (bias ? bias[c] : 0.f);
+    if (cv) z = zsum[c] + bc;
     if (cv && logits) logits[(int64_t)m * ldl + c] = z;
-    const int y = labels[m];
     float mx = z;
     int am = cv ? c : 0x7fffffff;
 #pragma unroll
@@ -801,11 +812,12 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
       atomicAdd(stats + 2, 1.f);
     }
   }
+  HEAD_STAMP(3);
   if (dzp == nullptr) return;
   // ---- fused activation gradient of the layer below (the NEXT backward GEMM):
   // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
   // chunks this thread already holds; bf16 row store + transposed copy.
-  __syncthreads();
+  lds_barrier();  // LDS only: no wait for this block's global stores
   float g[kHeadMaxC];
 #pragma unroll
   for (int c = 0; c < kHeadMaxC; ++c) g[c] = c < C ? gz[c] : 0.f;
@@ -835,6 +847,17 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
       for (int e = 0; e < 8; ++e) dzpT[(int64_t)(k + e) * ldpt + m] = q[e];
     }
   }
+  HEAD_STAMP(4);
+}
+
+hipError_t head_read_stamps(uint64_t* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_head_stamps), sizeof(uint64_t) * 64 * 6, 0,
+                             hipMemcpyDeviceToHost);
+}
+void head_set_stamping(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
 }
 
 hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,

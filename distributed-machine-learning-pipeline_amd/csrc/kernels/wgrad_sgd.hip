@@ -1,0 +1,211 @@
+// Weight gradient + SGD of the wide-MLP step, straight from the row-major
+// activations (BASELINE config 4):
+//
+//   G[n][k] = alpha * sum_m Z[m][n] X[m][k]        (Z = dZ_{l+1}, X = H_l; m = batch)
+//   W[n][k] -= lr * G   (fp32 master, float4 RMW)  ;  Wb[n][k] = bf16(W)   (next GEMMs' copy)
+//   b[n]    -= lr * alpha * sum_m Z[m][n]          (or G / db written out for an all-reduce)
+//
+// The reduction runs over the batch rows, which are the STRIDED dimension of
+// both stored activations: the 64 x 64 tiles of Z and X are staged row-major
+// by LDS-DMA and turned into MFMA operands by ds_read_b64_tr_b16 (gfx950's
+// transposing LDS read; cdna_hip_programming.md T10) — so no producer has to
+// write transposed activation copies (dZ^T, H^T) any more.
+//
+// The kernel is bound by the fp32 master read-modify-write (+ the bf16 copy):
+// every workgroup issues its W-tile loads FIRST, so that HBM round trip
+// overlaps the operand staging and the MFMAs instead of following them.
+// Reference hot loop replaced: the per-sample weight update of client.go:112-202.
+#include "common.h"
+#include "../dsml.h"
+
+namespace dsml {
+namespace {
+
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef short wg_i16x4 __attribute__((ext_vector_type(4)));
+typedef float wg_f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t wg_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) void* wg_gptr;
+typedef __attribute__((address_space(3))) void* wg_lptr;
+typedef __attribute__((address_space(3))) wg_i16x4* wg_lv4;
+
+constexpr int kWgImg = 64 * 128;  // one 64-row x 64-column bf16 image, 128-B rows
+constexpr int kWgPitch = 68;      // floats per row of the fp32 epilogue tile
+
+__device__ __forceinline__ int wg_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+
+struct WgArgs {
+  const uint16_t* Z;  // [M x >= N] bf16, ldz
+  int64_t ldz;
+  const uint16_t* X;  // [M x >= K] bf16, ldx
+  int64_t ldx;
+  int M, N, K;
+  float alpha, lr;
+  float* W;  // [N x K] fp32, ldw (SGD target) — or null with G
+  int64_t ldw;
+  uint16_t* Wb;  // bf16 copy of the updated W (nullable), ldwb
+  int64_t ldwb;
+  float* G;  // alpha * gradient out (nullable; used when W is null), ldg
+  int64_t ldg;
+  float* bias;   // b -= lr * db (nullable)
+  float* bgrad;  // db out (nullable)
+};
+
+// Operand fragment of the 16 x 16 x 32 MFMA: lane (i, g) gets image column
+// c0 + i at rows m0 + 8g .. +7 (two transposing reads of 4 rows each).
+__device__ __forceinline__ uint4 wg_frag(const char* img, int m0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (c0 >> 3) + (p >> 1);
+  const int r0 = m0 + 8 * g + q, r1 = r0 + 4;
+  const wg_i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (wg_lv4)(img + r0 * 128 + 16 * (chunk ^ wg_swz(r0)) + 8 * (p & 1)));
+  const wg_i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (wg_lv4)(img + r1 * 128 + 16 * (chunk ^ wg_swz(r1)) + 8 * (p & 1)));
+  const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+  return make_uint4(l2.x, l2.y, h2.x, h2.y);
+}
+
+__global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
+  // two operand images (16 KiB), later the fp32 epilogue tile (17 KiB)
+  __shared__ __attribute__((aligned(16))) char lds[64 * kWgPitch * 4];
+  static_assert(64 * kWgPitch * 4 >= 2 * kWgImg, "LDS carve");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  char* imz = lds;
+  char* imx = lds + kWgImg;
+
+  // ---- 1. the W tile's loads go out first (rows rl + 16j, columns cl..cl+3) ----
+  const int rl = tid >> 4, cl = 4 * (tid & 15);
+  const int kc = k0 + cl;
+  const bool kv = kc < a.K;  // K % 4 == 0: a 4-column group is whole or absent
+  float4 wold[4];
+  if (a.W) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nr = min(n0 + rl + 16 * j, a.N - 1);
+      wold[j] = kv ? *reinterpret_cast<const float4*>(a.W + (int64_t)nr * a.ldw + kc)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = {0.f, 0.f, 0.f, 0.f};
+  float dbias = 0.f;
+  const int wn = (w >> 1) * 32, wk = (w & 1) * 32;
+
+  for (int mb = 0; mb < a.M; mb += 64) {
+    // ---- 2. Z[mb.., n0..] and X[mb.., k0..] row-major images, 2 LDS-DMA pieces per wave each ----
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int piece = 2 * w + pc;  // 8 rows x 128 B
+      const int r = 8 * piece + (lane >> 3), p = lane & 7;
+      const int m = min(mb + r, a.M - 1);
+      const int zc = min(n0 + 8 * (p ^ wg_swz(r)), (int)((a.N + 7) & ~7) - 8);
+      const int xc = min(k0 + 8 * (p ^ wg_swz(r)), (int)((a.K + 7) & ~7) - 8);
+      __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + zc),
+                                       (wg_lptr)(imz + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + xc),
+                                       (wg_lptr)(imx + piece * 1024), 16, 0, 0);
+    }
+    full_barrier();  // every piece landed (vmcnt(0) also retires the W loads: issued earlier)
+
+    // ---- 3. MFMAs: wave tile 32 n x 32 k, reduction over the batch rows ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint4 fz[2], fx[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) fz[x] = wg_frag(imz, 32 * h, wn + 16 * x, lane);
+#pragma unroll
+      for (int y = 0; y < 2; ++y) fx[y] = wg_frag(imx, 32 * h, wk + 16 * y, lane);
+      if (mb + 32 * h + 32 > a.M) {  // batch tail: rows >= M (clamped copies) contribute 0
+        const int g = lane >> 4;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          uint32_t* e = reinterpret_cast<uint32_t*>(&fz[x]);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (mb + 32 * h + 8 * g + t >= a.M) e[t >> 1] &= (t & 1) ? 0x0000ffffu : 0xffff0000u;
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, fz[x]),
+                                                              __builtin_bit_cast(wg_bf16x8, fx[y]),
+                                                              acc[x][y], 0, 0, 0);
+    }
+    // bias gradient (k-tile 0 only): column sums of the Z image
+    if (blockIdx.x == 0 && tid < 64) {
+      const int ch = tid >> 3, e = tid & 7;
+      for (int r = 0; r < 64 && mb + r < a.M; ++r) {
+        const uint16_t v = *reinterpret_cast<const uint16_t*>(imz + r * 128 + 16 * (ch ^ wg_swz(r)) + 2 * e);
+        dbias += bf16_to_f32(v);
+      }
+    }
+    __syncthreads();  // images free for the next batch block / the epilogue tile
+  }
+
+  // ---- 4. epilogue: acc -> LDS tile [64 n][64 k] -> float4 RMW of W + bf16 copy ----
+  float* tile = reinterpret_cast<float*>(lds);
+  {
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wn + 16 * x + 4 * g + r) * kWgPitch + wk + 16 * y + i] = acc[x][y][r] * a.alpha;
+  }
+  __syncthreads();
+  if (kv) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nr = n0 + rl + 16 * j;
+      if (nr >= a.N) continue;
+      const float4 gv = *reinterpret_cast<const float4*>(tile + (rl + 16 * j) * kWgPitch + cl);
+      if (a.W) {
+        float4 v = wold[j];
+        v.x -= a.lr * gv.x; v.y -= a.lr * gv.y; v.z -= a.lr * gv.z; v.w -= a.lr * gv.w;
+        __builtin_nontemporal_store(wg_f4{v.x, v.y, v.z, v.w},
+                                    reinterpret_cast<wg_f4*>(a.W + (int64_t)nr * a.ldw + kc));
+        if (a.Wb) {
+          const uint32_t lo = f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
+          const uint32_t hi = f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+          __builtin_nontemporal_store(wg_u2{lo, hi},
+                                      reinterpret_cast<wg_u2*>(a.Wb + (int64_t)nr * a.ldwb + kc));
+        }
+      } else if (a.G) {
+        *reinterpret_cast<float4*>(a.G + (int64_t)nr * a.ldg + kc) = gv;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && tid < 64 && n0 + tid < a.N) {
+    const float db = a.alpha * dbias;
+    if (a.bias) a.bias[n0 + tid] -= a.lr * db;
+    if (a.bgrad) a.bgrad[n0 + tid] = db;
+  }
+}
+
+}  // namespace
+
+hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t ldx, int M, int N,
+                     int K, float alpha, float lr, float* W, int64_t ldw, uint16_t* Wb, int64_t ldwb,
+                     float* G, int64_t ldg, float* bias, float* bgrad, hipStream_t s) {
+  if (M < 1 || N < 1 || K < 8 || (K & 3) || (ldz & 7) || (ldx & 7) || ldz < ((N + 7) & ~7) ||
+      ldx < ((K + 7) & ~7) || (((uintptr_t)Z | (uintptr_t)X) & 15))
+    return hipErrorInvalidValue;
+  if (W == nullptr && G == nullptr && bias == nullptr && bgrad == nullptr) return hipErrorInvalidValue;
+  if ((W && (((uintptr_t)W & 15) || (ldw & 3))) || (Wb && (((uintptr_t)Wb & 7) || (ldwb & 3))) ||
+      (G && (((uintptr_t)G & 15) || (ldg & 3))))
+    return hipErrorInvalidValue;
+  WgArgs a{Z, ldz, X, ldx, M, N, K, alpha, lr, W, ldw, Wb, ldwb, G, ldg, bias, bgrad};
+  hipLaunchKernelGGL(wgrad_sgd_k, dim3((K + 63) / 64, (N + 63) / 64), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dsml

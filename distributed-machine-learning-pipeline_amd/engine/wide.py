@@ -1,20 +1,24 @@
 """Wide-MLP engine (BASELINE config 4: MLP 784-4096-4096-10, bf16 on MI355X).
 
 Mixed precision: fp32 master weights (flat, same layout as models/mlp.py),
-bf16 copies of W and W^T for the MFMA GEMMs (refreshed by the fused
-update+cast kernel), bf16 activations (+ transposed copies for the weight
-gradients), fp32 accumulation, fp32 gradients all-reduced across replicas.
+ONE bf16 copy of each W in its stored [out][in] layout (refreshed by the
+weight-gradient kernel's SGD epilogue), bf16 activations, fp32 accumulation,
+fp32 gradients all-reduced across replicas.  No transposed copy of anything:
+the products that reduce over a strided dimension read their operand through
+gfx950's transposing LDS read (ds_read_b64_tr_b16).
 
-Every product is a bf16 "NT" GEMM on v_mfma_f32_16x16x32_bf16
-(kernels/gemm_bf16.hip), split-K for the skinny (M = batch) GEMMs so a step
-fills the 256 CUs; the epilogue (bias / ReLU / ReLU'-mask / casts / transposed
-copy) runs inside the GEMM, on the last K split of each tile to arrive.  The
-weight-gradient GEMMs carry the SGD update (fp32 master W and the bf16 W / W^T
-copies, vectorised through LDS) and the bias step (row sums of dZ^T) when there
-is one replica.  Per step, with L layers: 1 input cast, L forward GEMMs,
-softmax-CE, 2L-1 backward GEMMs (+ with several replicas, one all-reduce and
-one update per layer, bucketed by layer on a comm stream that overlaps the
-backward of the layers below).
+Per step, with L layers (every kernel hand-written for gfx950 MFMA):
+  cast      X (fp32) -> bf16
+  forward   H_{l+1} = relu(H_l . W_l^T + b_l)   kernels/gemm_skinny.hip NT (split-K,
+            64x64 tiles, >= 256 workgroups) or gemm_rows64 for short K
+  head      logits, softmax-CE, dZ_L and dZ_{L-1} = (dZ_L . W_{L-1}) * (H > 0)
+            in one kernel (gemm_bf16.hip head_softmax_xent)
+  dgrad     dZ_l = (dZ_{l+1} . W_l) * (H_l > 0)  gemm_skinny.hip NN (W untransposed)
+  wgrad     W_l -= lr * dZ_{l+1}^T H_l, bf16 W_l refreshed, b_l step
+            (kernels/wgrad_sgd.hip, straight from the row-major activations)
+With several replicas the wgrad kernel writes the gradient instead, and each
+layer's bucket is all-reduced + applied on a comm stream that overlaps the
+backward of the layers below.  Reference hot loop replaced: client.go:112-202.
 """
 from __future__ import annotations
 
@@ -33,11 +37,15 @@ def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def _tiles(M: int, N: int) -> int:
+    return math.ceil(M / 64) * math.ceil(N / 64)
+
+
 class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
-                 gemm: str = "rows64"):
+                 gemm: str = "skinny", overlap_wgrad: bool = False):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -48,8 +56,11 @@ class WideMlpTrainer:
             raise ValueError("batch must be a multiple of 8 (16 B bf16 rows)")
         if spec.dims[-1] > 64:
             raise ValueError("softmax kernel supports <= 64 classes")
-        if gemm not in ("rows64", "splitk"):
-            raise ValueError("gemm must be 'rows64' (full-K batch-row kernel) or 'splitk'")
+        if any(x % 8 for x in spec.dims[:-1]):
+            raise ValueError("input / hidden widths must be multiples of 8 (16 B bf16 rows)")
+        if gemm not in ("skinny", "rows64"):
+            raise ValueError("gemm must be 'skinny' (split-K 64x64 tiles) or 'rows64' (full-K "
+                             "64x16 tiles) for the forward products")
         self.spec, self.batch, self.lr, self.sync, self.gemm = spec, batch, lr, sync, gemm
         self.device = dev = self.ctx.device
         self.target_wgs = target_wgs
@@ -61,34 +72,43 @@ class WideMlpTrainer:
         self.X = data.X.to(dev, torch.float32).contiguous()
         self.y = data.y.to(dev, torch.int32).contiguous()
         self.nbatches = len(data) // batch
+        # the training shard is resident in HBM: stage it in the compute dtype
+        # once (bf16 rows padded to 16 columns) instead of casting every batch
+        self.Xb = torch.zeros(self.nbatches * batch, _rup(spec.dims[0], 16), dtype=torch.bfloat16,
+                              device=dev)
+        self.C.cast_transpose(self.X, self.nbatches * batch, spec.dims[0], self.Xb, None)
         self.P = init_params(self.layout, seed, init).to(dev)
         self.G = torch.zeros_like(self.P)
         bf = dict(dtype=torch.bfloat16, device=dev)
-        self.Wb = [torch.zeros(d[l + 1], self.pd[l], **bf) for l in range(L)]
-        self.WbT = [torch.zeros(self.pd[l], self.pd[l + 1], **bf) for l in range(L)]
-        self.H = [torch.zeros(batch, self.pd[l], **bf) for l in range(L)]
-        self.HT = [torch.zeros(self.pd[l], batch, **bf) for l in range(L)]
+        # bf16 W_l with rows padded to 16 (zeros: the dgrad reads a whole K tile of
+        # rows), double-buffered by step parity: step s reads Wb[l][s % 2] (forward,
+        # dgrad, head) while its weight-gradient kernel writes the updated copy into
+        # Wb[l][(s + 1) % 2] -- so the wgrad kernels can run on a side stream,
+        # concurrently with the dgrad chain that still reads the old weights.
+        self.Wb = [[torch.zeros(self.pd[l + 1], self.pd[l], **bf) for _ in range(2)]
+                   for l in range(L)]
+        self.H = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L)]
         self.dZ = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L + 1)]
-        self.dZT = [None] + [torch.zeros(self.pd[l], batch, **bf) for l in range(1, L + 1)]
         self.logits = torch.zeros(batch, d[L], dtype=torch.float32, device=dev)
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self.views = self.layout.views(self.P)
         self.gviews = self.layout.views(self.G)
-        # split-K plans of the batch-row GEMMs: name -> (M, N, K, splits); the
-        # weight-gradient GEMMs (K = batch) run unsplit with the SGD epilogue
+        self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
+        # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
         self.plans: Dict[str, tuple] = {}
-        ws = 0
         for l in range(L):
-            ws = max(ws, self._plan(f"f{l}", batch, d[l + 1], self.pd[l]))
-            if l > 0:
-                ws = max(ws, self._plan(f"b{l}", batch, d[l], self.pd[l + 1]))
-        self.Cp = torch.zeros(ws if gemm == "splitk" else 16, dtype=torch.float32, device=dev)
-        # split-K arrival counters (one per 64x64 tile; every GEMM leaves them 0)
-        tiles = max(math.ceil(M / 64) * math.ceil(N / 64) for (M, N, _, _) in self.plans.values())
-        self.tctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
+            if l < L - 1:
+                self._plan(f"f{l}", batch, d[l + 1], d[l], False)
+            if l > 0 and not (self.fused_head and l == L - 1):
+                self._plan(f"b{l}", batch, d[l], self.pd[l + 1], True)
+        ws = max([S * _tiles(M, N) * 4096 for (M, N, _, _, S) in self.plans.values()] + [16])
+        self.Cp = torch.zeros(ws, dtype=torch.float32, device=dev)
+        # split-K arrival tickets (one per 64x64 tile; every GEMM leaves them 0)
+        self.tctr = torch.zeros(max([_tiles(M, N) for (M, N, _, _, _) in self.plans.values()] + [1]),
+                                dtype=torch.int32, device=dev)
         self.steps_done = 0
         # One hipGraph per epoch (every batch offset baked in): replaying it
-        # removes the ~25 host launches per step.  With several replicas the
+        # removes the host launches per step.  With several replicas the
         # per-layer RCCL all-reduces and updates on the comm stream are
         # captured too (fork/join of the comm stream inside the capture); only
         # the torch.distributed fallback (sync='torch', e.g. gloo) stays eager.
@@ -108,82 +128,107 @@ class WideMlpTrainer:
                         max(lay.w_off[l] + d[l + 1] * d[l], lay.b_off[l] + d[l + 1]))
                        for l in range(L)]
         self._cs = torch.cuda.Stream(dev) if self.ctx.is_distributed else None
-        for l in range(L):  # bf16 copies of the initial weights
+        # single replica, overlap_wgrad: the weight-gradient + SGD kernels of layers
+        # >= 1 run on a side stream, concurrently with the dgrad chain.  Off by
+        # default: measured on MI355X the split-K dgrad (one 128 KiB-LDS workgroup
+        # per CU) waits for CUs held by the wgrad workgroups, 14 -> 33 us, and the
+        # step got slower (87.6 -> 99.5 us, profiles/r2_wide_*).
+        self.overlap_wgrad = overlap_wgrad and not self.ctx.is_distributed
+        self._ss = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        # an epoch graph must start at an even step (the Wb parity it baked in)
+        self.period = self.nbatches if self.nbatches % 2 == 0 else 2 * self.nbatches
+        self._refresh_bf16()
+
+    def _refresh_bf16(self) -> None:
+        """Both bf16 copies of every W_l from the fp32 masters."""
+        d = self.spec.dims
+        for l in range(self.L):
             W, _ = self.views[l]
-            self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, self.Wb[l], self.WbT[l])
+            for buf in self.Wb[l]:
+                self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, buf, None)
 
-    def _plan(self, name: str, M: int, N: int, K: int) -> int:
-        tiles = math.ceil(M / 64) * math.ceil(N / 64)
-        # ~one workgroup per CU, <= 4 K splits: the last split of a tile reads
-        # the other slabs in one batch (per-CU bytes, not HBM, bound these GEMMs)
-        splits = max(1, min(math.ceil(self.target_wgs / tiles), max(1, K // 128), 4))
-        S = self.C.gemm_num_splits(K, splits)
-        self.plans[name] = (M, N, K, splits)
-        return S * tiles * 4096  # slabs: one 64x64 fp32 tile per split
+    def wb(self, l: int) -> torch.Tensor:
+        """The bf16 copy of W_l the next step reads."""
+        return self.Wb[l][self.steps_done % 2]
 
-    def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor, **epi) -> int:
-        """One GEMM with its epilogue fused (split-K reduced in-kernel by the
-        last split of each tile)."""
-        M, N, K, splits = self.plans[name]
-        if self.gemm == "rows64":  # full K per block, no slabs
-            return self.C.gemm_bf16_nt_fused(A, B, M, N, K, splits=0, **epi)
-        return self.C.gemm_bf16_nt_fused(A, B, M, N, K, splits=splits, ws=self.Cp, ctr=self.tctr,
-                                         **epi)
+    def _plan(self, name: str, M: int, N: int, K: int, nn: bool) -> None:
+        self.plans[name] = (M, N, K, nn, self.C.gemm_skinny_splits(M, N, K, 0))
+
+    def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor, rows: int = 0, **epi) -> None:
+        """One skinny GEMM with its epilogue fused (split-K combined in-kernel
+        by the last slice of each tile to arrive); `rows` < batch for a short
+        last batch (evaluation)."""
+        M, N, K, nn, _ = self.plans[name]
+        M = rows or M
+        if not nn and (self.gemm == "rows64" or K < 1024):
+            # short K: a 64 x 16 tile per block over the full K beats a split-K tail
+            self.C.gemm_bf16_nt_fused(A, B, M, N, K, splits=0, **epi)
+            return
+        self.C.gemm_skinny(A, B, M, N, K, nn=nn, ws=self.Cp, ctr=self.tctr, **epi)
 
     # ----------------------------------------------------------------- step --
     def _step(self) -> None:
         C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
         r0 = (self.steps_done % self.nbatches) * Bt
-        C.cast_transpose(self.X[r0:r0 + Bt], Bt, d[0], self.H[0], self.HT[0])
-        fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096 and self.gemm == "rows64"
-        for l in range(L - 1 if fused_head else L):
+        p = self.steps_done % 2
+        cur = [self.Wb[l][p] for l in range(L)]       # this step's weights
+        nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
+        self.H[0] = self.Xb[r0:r0 + Bt]  # this batch's bf16 rows (a view: no copy)
+        for l in range(L - 1):
             _, b = self.views[l]
-            if l < L - 1:
-                self._gemm(f"f{l}", self.H[l], self.Wb[l], bias=b, relu=True, obf=self.H[l + 1],
-                           obfT=self.HT[l + 1])
-            else:
-                self._gemm(f"f{l}", self.H[l], self.Wb[l], bias=b, of32=self.logits)
-        if fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
+            self._gemm(f"f{l}", self.H[l], cur[l], bias=b, relu=True, obf=self.H[l + 1])
+        _, b = self.views[L - 1]
+        if self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
             # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
-            _, b = self.views[L - 1]
             prev = L >= 2
-            C.head_softmax_xent(self.H[L - 1], self.Wb[L - 1], b, Bt, self.pd[L - 1], d[L],
-                                self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], self.dZT[L],
-                                self.stats, dzp=self.dZ[L - 1] if prev else None,
-                                dzpT=self.dZT[L - 1] if prev else None)
+            C.head_softmax_xent(self.H[L - 1], cur[L - 1], b, Bt, self.pd[L - 1], d[L],
+                                self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], None,
+                                self.stats, dzp=self.dZ[L - 1] if prev else None)
         else:
+            C.gemm_bf16_nt_fused(self.H[L - 1], cur[L - 1], Bt, d[L], d[L - 1], bias=b,
+                                 of32=self.logits, splits=0)
             C.softmax_xent(self.logits, self.y[r0:r0 + Bt], Bt, d[L], 1.0 / Bt, self.dZ[L],
-                           self.dZT[L], self.stats)
+                           None, self.stats)
         world = self.ctx.world_size
         fused_sgd = world == 1
         scale = self.lr / world
+        main = torch.cuda.current_stream(self.device)
         for l in range(L - 1, -1, -1):
             W, b = self.views[l]
             gW, gb = self.gviews[l]
-            if l > 0 and not (fused_head and l == L - 1):
-                # activation gradient first: it needs the pre-update W_l^T
-                self._gemm(f"b{l}", self.dZ[l + 1], self.WbT[l], mask=self.H[l], obf=self.dZ[l],
-                           obfT=self.dZT[l])
             if fused_sgd:
-                # dW_l = dZ^T H_l with SGD fused in the GEMM epilogue: W -= lr*dW, the bf16
-                # W / W^T copies refreshed, and the bias step from the row sums of dZ^T.
-                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, sgdW=W,
-                                     lr=scale, obf=self.Wb[l], obfT=self.WbT[l], bsgd=b)
-            else:
-                C.gemm_bf16_nt_fused(self.dZT[l + 1], self.HT[l], d[l + 1], d[l], Bt, of32=gW,
-                                     bgrad=gb)
-                self._sync_layer(l, scale)
-        if not fused_sgd:
-            # the next step's forward reads every updated layer
-            torch.cuda.current_stream(self.device).wait_stream(self._cs)
+                # dW_l = dZ_{l+1}^T H_l with SGD fused: W -= lr*dW, the NEXT step's bf16
+                # copy written, the bias step from the column sums of dZ.  With
+                # overlap_wgrad, layers >= 1 go to the side stream as soon as dZ_{l+1}
+                # exists (fork here) and overlap the dgrad of layer l and below.
+                if l > 0 and self._ss is not None:
+                    self._ss.wait_stream(main)
+                    with torch.cuda.stream(self._ss):
+                        C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale, W=W,
+                                    Wb=nxt[l], bias=b)
+                else:
+                    C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale, W=W,
+                                Wb=nxt[l], bias=b)
+            if l > 0 and not (self.fused_head and l == L - 1):
+                # activation gradient (reads this step's W_l copy, not the one being written)
+                self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
+            if not fused_sgd:
+                C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], G=gW, bgrad=gb)
+                self._sync_layer(l, scale, nxt[l])
+        # join: the next step's forward reads every updated layer (and overwrites
+        # the activations the side-stream kernels read)
+        side = self._ss if fused_sgd else self._cs
+        if side is not None:
+            main.wait_stream(side)
         self.steps_done += 1
 
-    def _sync_layer(self, l: int, scale: float) -> None:
+    def _sync_layer(self, l: int, scale: float, wb_next: torch.Tensor) -> None:
         """Per-layer gradient bucket: as soon as layer l's weight gradient is
         written, its all-reduce and its SGD + bf16 refresh run on the comm stream
         while the backward of layers < l continues on the compute stream (none of
-        them reads W_l or its bf16 copies).  Buckets are whole layers, issued in
-        the same order on every rank."""
+        them reads W_l or the bf16 copy being written).  Buckets are whole
+        layers, issued in the same order on every rank.  The refreshed bf16
+        copy goes to the parity buffer the NEXT step reads."""
         C, d = self.C, self.spec.dims
         main = torch.cuda.current_stream(self.device)
         self._cs.wait_stream(main)
@@ -199,7 +244,7 @@ class WideMlpTrainer:
                 import torch.distributed as dist
 
                 dist.all_reduce(g)
-            C.sgd_cast(W, gW, d[l + 1], d[l], scale, self.Wb[l], self.WbT[l])
+            C.sgd_cast(W, gW, d[l + 1], d[l], scale, wb_next, None)
             C.sgd_update_(b, gb, scale)
 
     def _warm_comm(self) -> None:
@@ -224,7 +269,7 @@ class WideMlpTrainer:
         g = torch.cuda.CUDAGraph()
         saved = self.steps_done
         with torch.cuda.graph(g, stream=stream):
-            for _ in range(self.nbatches):
+            for _ in range(self.period):
                 self._step()
         self.steps_done = saved
         self._graph = g
@@ -232,13 +277,13 @@ class WideMlpTrainer:
     def train_steps(self, n: int) -> None:
         with torch.cuda.device(self.device):
             while n > 0:
-                if (self.graph_enabled and self.steps_done % self.nbatches == 0
-                        and n >= self.nbatches):
+                if (self.graph_enabled and self.steps_done % self.period == 0
+                        and n >= self.period):
                     if self._graph is None:
                         self._capture_epoch()
                     self._graph.replay()
-                    self.steps_done += self.nbatches
-                    n -= self.nbatches
+                    self.steps_done += self.period
+                    n -= self.period
                 else:
                     self._step()
                     n -= 1
@@ -271,24 +316,37 @@ class WideMlpTrainer:
         self.synchronize()
         self.P.copy_(sd["params"].to(self.device))
         self.steps_done = int(sd["steps_done"])
-        d = self.spec.dims
-        for l in range(self.L):  # refresh the bf16 GEMM copies from the fp32 masters
-            W, _ = self.views[l]
-            self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, self.Wb[l], self.WbT[l])
+        self._refresh_bf16()  # both bf16 GEMM copies from the fp32 masters
         self.synchronize()
 
     @torch.no_grad()
     def evaluate(self, ds: Dataset) -> Dict[str, float]:
-        """fp32 evaluation of the master weights (torch ops on the GPU)."""
-        from ..models.mlp import forward_ref
-
-        X = ds.X.to(self.device, torch.float32)
-        y = ds.y.to(self.device).long()
-        self.synchronize()
-        logits, _ = forward_ref(self.layout, self.P, X)
-        p = torch.softmax(logits, 1)
-        loss = (-torch.log(p.gather(1, y.view(-1, 1)).squeeze(1) + 1e-10)).sum().item()
-        correct = (logits.argmax(1) == y).sum().item()
+        """Loss / accuracy of the current weights on the GPU kernels the step
+        uses (bf16 GEMMs on the refreshed bf16 weight copies, fp32 accumulate,
+        fused head + softmax-CE statistics), batch by batch."""
+        C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
+        X = ds.X.to(self.device, torch.float32).contiguous()
+        y = ds.y.to(self.device, torch.int32).contiguous()
         n = X.shape[0]
-        return {"loss": loss / max(n, 1), "accuracy": 100.0 * correct / max(n, 1), "n": n}
-
+        st = torch.zeros(4, dtype=torch.float32, device=self.device)
+        xb = torch.zeros(Bt, self.pd[0], dtype=torch.bfloat16, device=self.device)
+        with torch.cuda.device(self.device):
+            self.synchronize()
+            for r0 in range(0, n, Bt):
+                m = min(Bt, n - r0)
+                C.cast_transpose(X[r0:r0 + m], m, d[0], xb, None)
+                self.H[0] = xb
+                for l in range(L - 1):
+                    _, b = self.views[l]
+                    self._gemm(f"f{l}", self.H[l], self.wb(l), rows=m, bias=b, relu=True,
+                               obf=self.H[l + 1])
+                _, b = self.views[L - 1]
+                if self.fused_head:
+                    C.head_softmax_xent(self.H[L - 1], self.wb(L - 1), b, m, self.pd[L - 1], d[L],
+                                        y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st)
+                else:
+                    C.gemm_bf16_nt_fused(self.H[L - 1], self.wb(L - 1), m, d[L], d[L - 1], bias=b,
+                                         of32=self.logits, splits=0)
+                    C.softmax_xent(self.logits, y[r0:r0 + m], m, d[L], 1.0 / m, self.dZ[L], None, st)
+            v = st.tolist()
+        return {"loss": v[0] / max(n, 1), "accuracy": 100.0 * v[1] / max(n, 1), "n": n}

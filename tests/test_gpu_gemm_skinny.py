@@ -1,0 +1,116 @@
+"""Skinny bf16 GEMMs (kernels/gemm_skinny.hip) against the fp32 torch product of
+the same bf16 operands: NT (forward, B = W [N x K]) and NN (dgrad, B = W
+[K x N] read through transposing LDS reads), split-K with the last-arriver
+reduction, every fused epilogue output, K / N / M tails."""
+import pytest
+import torch
+
+from hipdsml.ops.native import require_native
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _ref(A, B, nn):
+    return A.float() @ (B.float() if nn else B.float().t())
+
+
+def _ws(M, N, S):
+    tiles = ((N + 63) // 64) * ((M + 63) // 64)
+    return (torch.zeros(max(S, 1) * tiles * 4096, device=DEV),
+            torch.zeros(tiles, dtype=torch.int32, device=DEV))
+
+
+@pytest.mark.parametrize("nn", [False, True])
+@pytest.mark.parametrize("M,N,K,splits", [
+    (64, 4096, 4096, 0), (64, 4096, 784, 0), (64, 512, 4096, 1), (64, 512, 4096, 3),
+    (48, 136, 200, 2), (128, 256, 1024, 0), (64, 64, 64, 1), (17, 72, 1000, 0)])
+def test_skinny_matches_fp32(nn, M, N, K, splits):
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    B = (torch.randn(K, N, generator=g) if nn else torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
+    S = C.gemm_skinny_splits(M, N, K, splits)
+    ws, ctr = _ws(M, N, S)
+    out = torch.full((M, N), float("nan"), device=DEV)
+    got = C.gemm_skinny(A, B, M, N, K, nn=nn, of32=out, splits=splits, ws=ws, ctr=ctr)
+    assert got == S
+    torch.cuda.synchronize()
+    want = _ref(A, B, nn)
+    err = (out - want).abs().max().item()
+    assert err <= 2e-5 * K ** 0.5 * want.abs().max().item() + 1e-4, err
+    assert int(ctr.abs().sum().item()) == 0  # counters re-armed
+
+
+@pytest.mark.parametrize("nn", [False, True])
+def test_skinny_epilogue_bias_relu_mask_and_copies(nn):
+    C = require_native()
+    M, N, K = 64, 1024, 2048
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    B = (torch.randn(K, N, generator=g) if nn else torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV)
+    mask = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    S = C.gemm_skinny_splits(M, N, K, 0)
+    ws, ctr = _ws(M, N, S)
+    o32 = torch.empty(M, N, device=DEV)
+    obf = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    obfT = torch.empty(N, M, dtype=torch.bfloat16, device=DEV)
+    C.gemm_skinny(A, B, M, N, K, nn=nn, alpha=0.5, bias=bias, relu=True, mask=mask, of32=o32, obf=obf,
+                  obfT=obfT, ws=ws, ctr=ctr)
+    torch.cuda.synchronize()
+    want = torch.relu(0.5 * _ref(A, B, nn) + bias) * (mask.float() > 0)
+    tol = 2e-5 * K ** 0.5 * want.abs().max().item() + 1e-4
+    assert (o32 - want).abs().max().item() <= tol
+    assert torch.equal(obf, o32.to(torch.bfloat16))
+    assert torch.equal(obfT, obf.t())
+
+
+def test_skinny_repeated_calls_are_bit_identical():
+    """Split-K reduction in slice order: the same bits whichever slice lands last."""
+    C = require_native()
+    M, N, K = 64, 4096, 4096
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    ws, ctr = _ws(M, N, C.gemm_skinny_splits(M, N, K, 0))
+    outs = []
+    for _ in range(5):
+        o = torch.empty(M, N, device=DEV)
+        C.gemm_skinny(A, B, M, N, K, of32=o, ws=ws, ctr=ctr)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 4096, 4096), (64, 4096, 784), (64, 10, 4096), (48, 200, 136),
+                                   (128, 64, 256)])
+def test_wgrad_sgd_matches_fp32(M, N, K):
+    """W -= lr * alpha * Z^T X from ROW-MAJOR activations (transposing LDS reads),
+    bf16 copy refreshed, bias step from the column sums of Z."""
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(N + K + M)
+    pn, pk = (N + 15) // 16 * 16, (K + 15) // 16 * 16
+    Z = torch.zeros(M, pn, dtype=torch.bfloat16, device=DEV)
+    X = torch.zeros(M, pk, dtype=torch.bfloat16, device=DEV)
+    Z[:, :N] = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    X[:, :K] = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    W = torch.randn(N, K, generator=g).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    W0, b0 = W.clone(), b.clone()
+    Wb = torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV)
+    lr, alpha = 0.01, 0.25
+    C.wgrad_sgd(Z, X, M, N, K, alpha=alpha, lr=lr, W=W, Wb=Wb, bias=b)
+    torch.cuda.synchronize()
+    Gref = alpha * Z[:, :N].float().t() @ X[:, :K].float()
+    want = W0 - lr * Gref
+    assert (W - want).abs().max().item() < 1e-5 * max(1.0, M ** 0.5)
+    assert torch.equal(Wb[:, :K], W.to(torch.bfloat16))
+    bref = b0 - lr * alpha * Z[:, :N].float().sum(0)
+    assert (b - bref).abs().max().item() < 1e-5 * max(1.0, M ** 0.5)
+    # gradient-out form (multi-replica: all-reduced before the update)
+    G = torch.full((N, K), float("nan"), device=DEV)
+    db = torch.zeros(N, device=DEV)
+    C.wgrad_sgd(Z, X, M, N, K, alpha=alpha, G=G, bgrad=db)
+    torch.cuda.synchronize()
+    assert (G - Gref).abs().max().item() < 1e-4
+    assert (db - alpha * Z[:, :N].float().sum(0)).abs().max().item() < 1e-4

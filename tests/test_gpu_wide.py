@@ -59,8 +59,7 @@ def test_wide_step_matches_fp32_reference():
     assert st.count == 64 and abs(st.loss_sum - float(loss_sum)) / float(loss_sum) < 0.02
     # the bf16 GEMM copies match the updated fp32 master weights
     W0, _ = tr.views[0]
-    assert torch.equal(tr.Wb[0][:, :784].cpu(), W0.cpu().to(torch.bfloat16))
-    assert torch.equal(tr.WbT[0][:784, :256].cpu(), W0.cpu().to(torch.bfloat16).t())
+    assert torch.equal(tr.wb(0)[:256, :784].cpu(), W0.cpu().to(torch.bfloat16))
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -146,7 +145,7 @@ def test_head_softmax_xent(C_, K):
     assert torch.equal(dzpT.cpu()[:K].t(), dzp.cpu()[:, :K])
 
 
-@pytest.mark.parametrize("gemm", ["rows64", "splitk"])
+@pytest.mark.parametrize("gemm", ["skinny", "rows64"])
 def test_wide_gemm_variants_train_identically_close(gemm):
     spec = MlpSpec((784, 512, 256, 10))
     ds = synthetic_mnist(64 * 4, seed=8)
@@ -154,6 +153,39 @@ def test_wide_gemm_variants_train_identically_close(gemm):
     t.train_steps(8)
     st = t.read_stats()
     assert st.count == 8 * 64 and st.avg_loss < 2.5
+
+
+def test_wide_native_evaluate_matches_fp32_forward():
+    """evaluate() runs the step's bf16 kernels (incl. a short last batch) and
+    agrees with the fp32 torch forward of the master weights."""
+    from hipdsml.models.mlp import forward_ref
+
+    spec = MlpSpec((784, 512, 256, 10))
+    ds = synthetic_mnist(64 * 20, seed=9)
+    t = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=6, graph=False)
+    t.train_steps(40)
+    ev = synthetic_mnist(64 * 5 + 24, seed=10)
+    got = t.evaluate(ev)
+    assert got["n"] == len(ev)
+    logits, _ = forward_ref(t.layout, t.P, ev.X.to(DEV))
+    y = ev.y.to(DEV).long()
+    acc = 100.0 * (logits.argmax(1) == y).float().mean().item()
+    loss = torch.nn.functional.cross_entropy(logits, y).item()
+    assert abs(got["accuracy"] - acc) <= 2.0, (got, acc)
+    assert abs(got["loss"] - loss) <= 0.02 * max(1.0, loss), (got, loss)
+
+
+@pytest.mark.parametrize("nb", [4, 3])  # odd epochs: the graph covers two (Wb parity)
+def test_wide_overlapped_wgrad_is_bit_identical(nb):
+    spec = MlpSpec((784, 256, 128, 10))
+    ds = synthetic_mnist(64 * nb, seed=11)
+    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True)
+    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, overlap_wgrad=True)
+    a.train_steps(13)
+    b.train_steps(13)
+    a.synchronize(); b.synchronize()
+    assert torch.equal(a.P.cpu(), b.P.cpu())
+    assert torch.equal(a.wb(1).cpu(), b.wb(1).cpu())
 
 
 def test_wide_graph_matches_eager():

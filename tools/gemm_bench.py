@@ -62,6 +62,36 @@ def main() -> int:
                flops=2 * B * N * K)
         timeit(f"rows64_{N}x{K}", lambda: C.gemm_bf16_nt_fused(A, W, B, N, K, obf=H, splits=0),
                nbytes=N * K * 2, flops=2 * B * N * K)
+    # skinny split-K kernels (kernels/gemm_skinny.hip): forward (NT) and dgrad (NN, W untransposed)
+    for (N, K) in [(4096, 4096), (4096, 784)]:
+        A = torch.randn(B, K, device=dev).to(torch.bfloat16)
+        W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        bias = torch.randn(N, device=dev)
+        H = torch.empty(B, N, **bf)
+        HT = torch.empty(N, B, **bf)
+        S = C.gemm_skinny_splits(B, N, K, 0)
+        tiles = (N + 63) // 64
+        ws = torch.zeros(S * tiles * 4096, device=dev)
+        ctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
+        timeit(f"skinny_nt_{N}x{K}", lambda: C.gemm_skinny(A, W, B, N, K, bias=bias, relu=True, obf=H, obfT=HT,
+                                                             ws=ws, ctr=ctr), nbytes=N * K * 2, flops=2 * B * N * K)
+    for (N, K) in [(4096, 4096)]:
+        A = torch.randn(B, K, device=dev).to(torch.bfloat16)
+        W = torch.randn(K, N, device=dev).to(torch.bfloat16)
+        mask = torch.randn(B, N, device=dev).to(torch.bfloat16)
+        H = torch.empty(B, N, **bf)
+        HT = torch.empty(N, B, **bf)
+        S = C.gemm_skinny_splits(B, N, K, 0)
+        tiles = (N + 63) // 64
+        ws = torch.zeros(S * tiles * 4096, device=dev)
+        ctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
+        timeit(f"skinny_nn_{N}x{K}", lambda: C.gemm_skinny(A, W, B, N, K, nn=True, mask=mask, obf=H, obfT=HT,
+                                                             ws=ws, ctr=ctr), nbytes=N * K * 2, flops=2 * B * N * K)
+        for sp in (2, 4, 8):
+            ws8 = torch.zeros(sp * tiles * 4096, device=dev)
+            timeit(f"skinny_nn_{N}x{K}_s{sp}", lambda sp=sp, ws8=ws8: C.gemm_skinny(
+                A, W, B, N, K, nn=True, mask=mask, obf=H, obfT=HT, splits=sp, ws=ws8, ctr=ctr),
+                nbytes=N * K * 2, flops=2 * B * N * K)
     M, N = 4096, 4096
     dZT = torch.randn(M, B, device=dev).to(torch.bfloat16)
     HT = torch.randn(N, B, device=dev).to(torch.bfloat16)
@@ -71,6 +101,13 @@ def main() -> int:
     b = torch.zeros(M, device=dev)
     timeit("dw_sgd_4096x4096", lambda: C.gemm_bf16_nt_fused(dZT, HT, M, N, B, sgdW=Wf, lr=1e-6, obf=Wb, obfT=WbT, bsgd=b),
            nbytes=M * N * (4 + 4 + 2 + 2), flops=2 * B * M * N)
+    timeit("dw_sgd_noT_4096x4096", lambda: C.gemm_bf16_nt_fused(dZT, HT, M, N, B, sgdW=Wf, lr=1e-6, obf=Wb, bsgd=b),
+           nbytes=M * N * (4 + 4 + 2), flops=2 * B * M * N)
+    Zr = torch.randn(B, N, device=dev).to(torch.bfloat16)
+    Xr = torch.randn(B, N, device=dev).to(torch.bfloat16)
+    bb = torch.zeros(M, device=dev)
+    timeit("wgrad_sgd_4096x4096", lambda: C.wgrad_sgd(Zr, Xr, B, M, N, lr=1e-6, W=Wf, Wb=Wb, bias=bb),
+           nbytes=M * N * (4 + 4 + 2), flops=2 * B * M * N)
     x = torch.empty(64 << 20, device=dev)
     timeit("copy_256MB", lambda: x[: 32 << 20].copy_(x[32 << 20:]), nbytes=2 * (32 << 20) * 4)
     print(json.dumps({"flags": os.environ.get("HIPDSML_R64_FLAGS", "3"), **out}))
