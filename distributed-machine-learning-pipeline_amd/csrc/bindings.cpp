@@ -542,6 +542,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("head_set_stamping", &head_set_stamping);
+  m.def("head_set_debug", &head_set_debug);
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

@@ -250,6 +250,7 @@ hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t 
                      float* G, int64_t ldg, float* bias, float* bgrad, hipStream_t s);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
+void head_set_debug(int v);
 hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
                        float lr, hipStream_t s);
 hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,

@@ -718,6 +718,7 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 // Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
 __device__ uint64_t g_head_stamps[64][6];
 __device__ int g_head_stamp_on;
+__device__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bit 1 the dzp phase
 #define HEAD_STAMP(k)                                                               \
   do {                                                                              \
     if (g_head_stamp_on && t == 0 && m < 64) g_head_stamps[m][(k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -806,14 +807,14 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
       if (dzT) dzT[(int64_t)c * ldt + m] = hq;
     }
     if (c < kHeadMaxC) gz[c] = bf16_to_f32(hq);
-    if (c == y && stats) {
+    if (c == y && stats && !(g_head_dbg & 1)) {
       atomicAdd(stats + 0, -logf(p + 1e-10f));
       atomicAdd(stats + 1, am == y ? 1.f : 0.f);
       atomicAdd(stats + 2, 1.f);
     }
   }
   HEAD_STAMP(3);
-  if (dzp == nullptr) return;
+  if (dzp == nullptr || (g_head_dbg & 2)) return;
   // ---- fused activation gradient of the layer below (the NEXT backward GEMM):
   // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
   // chunks this thread already holds; bf16 row store + transposed copy.
@@ -853,6 +854,10 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
 hipError_t head_read_stamps(uint64_t* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_head_stamps), sizeof(uint64_t) * 64 * 6, 0,
                              hipMemcpyDeviceToHost);
+}
+void head_set_debug(int v) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dbg), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
 }
 void head_set_stamping(bool on) {
   const int v = on ? 1 : 0;

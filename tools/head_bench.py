@@ -42,6 +42,11 @@ out = {
     "no_logits_no_dzp": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, None, dz, None, stats)),
     "empty_torch_op": t(lambda: logits.zero_()),
 }
+for dbg in (1, 2, 3):
+    C.head_set_debug(dbg)
+    out[f"dbg{dbg}"] = t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, logits, dz, None, stats,
+                                                     dzp=dzp))
+C.head_set_debug(0)
 print(json.dumps(out))
 
 C.head_set_stamping(True)
