@@ -801,6 +801,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                             max_rings);
       }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20,
          py::arg("max_rings") = 0)
+      .def("reserve_ring", [](PyComm& s, int64_t count, int64_t chunk_bytes, int max_rings) {
+        s.c->reserve_ring(count, kF32, chunk_bytes, max_rings);
+      }, py::arg("count"), py::arg("chunk_bytes") = 1 << 20, py::arg("max_rings") = 0,
+         "size the fp32 ring all-reduce scratch for `count` elements up front")
       .def("broadcast_", [](PyComm& s, torch::Tensor t, int root) {
         check_cuda(t, "t");
         s.c->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());

@@ -109,6 +109,27 @@ void RcclComm::ensure_tmp(size_t bytes) {
   DSML_HIP_CHECK(hipMalloc(&tmp_, tmp_bytes_));
 }
 
+size_t RcclComm::ring_tmp_bytes(int64_t count, int32_t dtype, int64_t chunk_bytes,
+                                int max_rings) const {
+  const int n = nranks_;
+  if (n < 2 || count <= 0) return 0;
+  const size_t es = dtype_size(dtype);
+  const int64_t align = std::max<int64_t>(1, 16 / (int64_t)es);
+  const int64_t chunk = chunk_bytes > 0 ? chunk_bytes / (int64_t)es : count;
+  const auto plan = ring_schedule(n, rank_, count, align, chunk, max_rings);
+  const int R = (int)directed_rings(n, max_rings).size();
+  int64_t maxr = 0;
+  for (const auto& g : plan)
+    for (const auto& x : g)
+      if (x.reduce) maxr = std::max(maxr, x.recv_len);
+  const size_t slot = std::max<size_t>(((size_t)maxr * es + 255) & ~(size_t)255, 256);
+  return slot * (size_t)R;
+}
+
+void RcclComm::reserve_ring(int64_t count, int32_t dtype, int64_t chunk_bytes, int max_rings) {
+  ensure_tmp(ring_tmp_bytes(count, dtype, chunk_bytes, max_rings));
+}
+
 void RcclComm::allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, hipStream_t s) {
   if (aborted_) throw std::runtime_error("allreduce on aborted communicator");
   check(ncclAllReduce(buf, buf, (size_t)count, to_nccl(dtype), to_nccl_op(op), comm_, s),
@@ -127,13 +148,17 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
   const int64_t align = std::max<int64_t>(1, 16 / (int64_t)es);
   const int64_t chunk = chunk_bytes > 0 ? chunk_bytes / (int64_t)es : count;
   const auto plan = ring_schedule(n, rank_, count, align, chunk, max_rings);
+  const size_t need = ring_tmp_bytes(count, dtype, chunk_bytes, max_rings);
   const int R = (int)directed_rings(n, max_rings).size();
-  int64_t maxr = 0;
-  for (const auto& g : plan)
-    for (const auto& x : g)
-      if (x.reduce) maxr = std::max(maxr, x.recv_len);
-  const size_t slot = ((size_t)maxr * es + 255) & ~(size_t)255;
-  ensure_tmp(std::max<size_t>(slot * R, 256));
+  const size_t slot = need / (size_t)R;
+  if (need > tmp_bytes_) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cs);
+    if (cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("ring_allreduce: reduce scratch must be reserved before a graph "
+                               "capture (RcclComm::reserve_ring)");
+    ensure_tmp(need);
+  }
   uint8_t* b = static_cast<uint8_t*>(buf);
   uint8_t* tmp = static_cast<uint8_t*>(tmp_);
   const ncclDataType_t t = to_nccl(dtype);

@@ -163,6 +163,10 @@ class RcclComm {
   // rounds.  max_rings = 0: all rings; 1: the classic single ring.
   void ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, int64_t chunk_bytes,
                       hipStream_t s, int max_rings = 0);
+  // Size the ring's reduce scratch for `count` elements once, up front (the
+  // largest bucket): no hipMalloc / hipFree between buckets, and none inside a
+  // stream capture (ring_allreduce refuses to grow it while capturing).
+  void reserve_ring(int64_t count, int32_t dtype, int64_t chunk_bytes, int max_rings = 0);
   void broadcast(void* buf, int64_t count, int32_t dtype, int root, hipStream_t s);
   void send(const void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
   void recv(void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
@@ -175,6 +179,7 @@ class RcclComm {
  private:
   void check(ncclResult_t r, const char* what);
   void ensure_tmp(size_t bytes);
+  size_t ring_tmp_bytes(int64_t count, int32_t dtype, int64_t chunk_bytes, int max_rings) const;
   ncclComm_t comm_ = nullptr;
   int rank_, nranks_, device_;
   bool blocking_;

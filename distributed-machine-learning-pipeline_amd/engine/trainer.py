@@ -179,6 +179,8 @@ class MlpTrainer:
         elif self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)
+                # the in-house ring's scratch, sized once (never inside a graph capture)
+                self.comm.reserve_ring(self.layout.nparams, self._ring_chunk)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
         if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain and _xgmi_eligible(

@@ -45,7 +45,7 @@ class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
-                 gemm: str = "skinny", overlap_wgrad: bool = False):
+                 gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -128,6 +128,13 @@ class WideMlpTrainer:
                         max(lay.w_off[l] + d[l + 1] * d[l], lay.b_off[l] + d[l + 1]))
                        for l in range(L)]
         self._cs = torch.cuda.Stream(dev) if self.ctx.is_distributed else None
+        # serial_sync: each bucket's all-reduce + update on the compute stream (no
+        # overlap) -- the reference the overlapped schedule must match bit for bit
+        self.serial_sync = serial_sync
+        self._comm_delay_cycles = 0  # test hook: stall the comm stream before each bucket
+        if self.comm is not None and sync == "ring":
+            # the in-house ring's reduce scratch, sized once for the largest bucket
+            self.comm.reserve_ring(max(hi - lo for lo, hi in self._gspan), 4 << 20)
         # single replica, overlap_wgrad: the weight-gradient + SGD kernels of layers
         # >= 1 run on a side stream, concurrently with the dgrad chain.  Off by
         # default: measured on MI355X the split-K dgrad (one 128 KiB-LDS workgroup
@@ -231,11 +238,14 @@ class WideMlpTrainer:
         copy goes to the parity buffer the NEXT step reads."""
         C, d = self.C, self.spec.dims
         main = torch.cuda.current_stream(self.device)
-        self._cs.wait_stream(main)
+        cs = main if self.serial_sync else self._cs
+        cs.wait_stream(main)
         W, b = self.views[l]
         gW, gb = self.gviews[l]
         lo, hi = self._gspan[l]
-        with torch.cuda.stream(self._cs):
+        with torch.cuda.stream(cs):
+            if self._comm_delay_cycles:
+                torch.cuda._sleep(self._comm_delay_cycles)
             g = self.G[lo:hi]
             if self.comm is not None:
                 (self.comm.ring_allreduce_(g, 0, 4 << 20) if self.sync == "ring"

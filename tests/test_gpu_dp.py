@@ -39,7 +39,10 @@ def _worker(rank, world, port, outdir, kind):
 
         spec = MlpSpec((784, 256, 128, 10))
         ds = synthetic_mnist(64 * 4, seed=200 + rank)
-        tr = WideMlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7, sync="torch")
+        tr = WideMlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7, sync="torch",
+                            serial_sync=kind == "wide_serial")
+        if kind == "wide_delay":
+            tr._comm_delay_cycles = 2_000_000  # ~1 ms stall ahead of every bucket on the comm stream
     tr.train_steps(4)
     tr.synchronize()
     torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
@@ -66,3 +69,19 @@ def test_two_replicas_one_gpu(kind):
         P = P - 0.05 * g / world
     err = (outs[0] - P).abs().max().item()
     assert err < (2e-5 if kind == "fused" else 5e-3), err
+
+
+def test_wide_bucket_overlap_matches_serial_sync():
+    """Per-layer buckets all-reduced + applied on the comm stream while the
+    backward continues (with the comm stream artificially stalled) give the
+    same bits as all-reducing each bucket in line on the compute stream."""
+    world = 2
+    got = {}
+    for kind in ("wide_delay", "wide_serial"):
+        with tempfile.TemporaryDirectory() as d:
+            mp.start_processes(_worker, args=(world, _free_port(), d, kind), nprocs=world,
+                               start_method="spawn", join=True)
+            got[kind] = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"]
+                         for r in range(world)]
+    assert torch.equal(got["wide_delay"][0], got["wide_delay"][1])
+    assert torch.equal(got["wide_delay"][0], got["wide_serial"][0])
