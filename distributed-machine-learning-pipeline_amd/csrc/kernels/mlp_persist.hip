@@ -83,7 +83,10 @@ constexpr int kLdsFloats = L1Lay::TOTAL > ChLay::TOTAL ? L1Lay::TOTAL : ChLay::T
 static_assert(kLdsFloats * 4 <= 160 * 1024, "LDS budget");
 
 // ---- exchange buffer layout (8-byte granules) -----------------------------------
-// PART[32][64][16]   layer-1 partials (b1 added by gk == 0 blocks)
+// PART[32][16][64]   layer-1 partials, PLAIN fp32 column-major per block (b1
+//                    added by gk == 0 blocks), published by one flag per block
+//                    and step (PF): the chain reads 32 KiB of values instead of
+//                    64 KiB of granules and checks 32 tags instead of 8192
 // DZ1 [64][128]      activation gradient of layer 1
 // CX  [2][4][kCXG]   chain exchange (parity by step), PLAIN fp32 (no tags):
 //                    H1 rows [16][128], H2 rows [16][64], dZ2 rows [16][64],
@@ -95,7 +98,8 @@ constexpr int kDz1G = kB * kD1;
 constexpr int kCXG = 16 * kD1 + 16 * kD2 + 16 * kD2 + 16 * 16;  // 4352
 constexpr int64_t kOffPart = 0, kOffDz1 = kOffPart + kPartG, kOffCx = kOffDz1 + kDz1G;
 constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCXG / 2;  // CX holds floats: 2 per granule
-constexpr int64_t kTotalG = kOffCxf + 2 * kNCH;
+constexpr int64_t kOffPf = kOffCxf + 2 * kNCH;                // PF[32]: partial flags
+constexpr int64_t kTotalG = kOffPf + kNL1;
 static_assert(kCXG % 4 == 0, "exchange rows travel as 16-B vectors");
 
 constexpr int kSc1 = 16;  // buffer aux: sc1 (write-through store / L1-bypassing load)
@@ -273,13 +277,16 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
           else acc0 = mfma_f32_16x16x4(xv[u], wv[u], acc0);
         }
       }
+      // column i, rows 16w + 4q .. +3: one 16-B write-through store per lane
       const float bn = B1[i];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * w + 4 * q + r;
-        st_gran(rb, kOffPart + ((int64_t)lb * kB + m) * 16 + i, acc0[r] + acc1[r] + bn, tag);
-      }
+      const f32x4 z = {acc0[0] + acc1[0] + bn, acc0[1] + acc1[1] + bn, acc0[2] + acc1[2] + bn,
+                       acc0[3] + acc1[3] + bn};
+      const int off = (int)(((kOffPart * 2 + ((int64_t)lb * 16 + i) * kB + 16 * w + 4 * q)) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4v, z), rb, off, 0, kSc1);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __syncthreads();
+    if (tid == 0) st_gran(rb, kOffPf + lb, __uint_as_float(tag), tag);
     PK_STAMP(0, 1);
     // next step's X into the other buffer (its last reader, the previous
     // step's backward, finished before the barrier that ended that step)
@@ -414,42 +421,37 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     const int par = (int)(s & 1);
     const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * kB;
 
-    // ---- H1 rows = relu(sum of the 4 k-partials): thread -> (row, 8 columns) ----
+    // ---- H1 rows = relu(sum of the 4 k-partials) ----
+    // the 32 layer-1 blocks' flags (one lane each), then this chain's 16 rows of
+    // every partial in one bulk read: thread -> (gn, column n, 8 rows), 4 gk
     {
-      const int r = tid >> 4, nc = tid & 15;
-      const int gn = nc >> 1, half = nc & 1;
-      uint4 v[kGK][4];
-      poll.start();
-      for (;;) {
-        bool all = true;
-#pragma unroll
-        for (int gk = 0; gk < kGK; ++gk) {
-          const int64_t g = kOffPart + ((int64_t)(gn + kGN * gk) * kB + rb0 + r) * 16 + half * 8;
-#pragma unroll
-          for (int p = 0; p < 4; ++p) v[gk][p] = ld_gran2(rb, g + 2 * p);
+      if (tid < kNL1) {
+        poll.start();
+        for (;;) {
+          const uint4 f = ld_gran2(rb, (kOffPf + tid) & ~(int64_t)1);
+          const uint32_t ft = ((kOffPf + tid) & 1) ? f.w : f.y;
+          if (ft == tag) break;
+          if (!poll.again()) { ok = false; break; }
         }
-#pragma unroll
-        for (int gk = 0; gk < kGK; ++gk)
-#pragma unroll
-          for (int p = 0; p < 4; ++p) all = all && v[gk][p].y == tag && v[gk][p].w == tag;
-        if (all) break;
-        if (!poll.again()) { ok = false; break; }
       }
-      float hv[8];
+      ok = __syncthreads_and(ok ? 1 : 0) != 0;
+      if (!ok) break;
+      const int gn = tid >> 5, n = (tid >> 1) & 15, half = tid & 1;
+      nu4v v[kGK][2];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        float e0 = 0.f, e1 = 0.f;
-#pragma unroll
-        for (int gk = 0; gk < kGK; ++gk) {
-          e0 += __uint_as_float(v[gk][p].x);
-          e1 += __uint_as_float(v[gk][p].z);
-        }
-        hv[2 * p] = fmaxf(e0, 0.f);
-        hv[2 * p + 1] = fmaxf(e1, 0.f);
+      for (int gk = 0; gk < kGK; ++gk) {
+        const int lb = gn + kGN * gk;
+        const int off = (int)(((kOffPart * 2 + ((int64_t)lb * 16 + n) * kB + rb0 + 8 * half)) * 4);
+        v[gk][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, kSc1);
+        v[gk][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, off + 16, 0, kSc1);
       }
-      float* dst = H1 + (rb0 + r) * kS1 + nc * 8;
-      *reinterpret_cast<float4*>(dst) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float z = 0.f;
+#pragma unroll
+        for (int gk = 0; gk < kGK; ++gk) z += __uint_as_float(v[gk][e >> 2][e & 3]);
+        H1[(rb0 + 8 * half + e) * kS1 + 16 * gn + n] = fmaxf(z, 0.f);
+      }
     }
     int y = -1;
     const int srow = w * 4 + (lane >> 4);  // softmax: 16 lanes per row, 4 rows per wave
