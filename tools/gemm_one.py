@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run ONE wide-MLP GEMM variant back to back (for rocprofv3 --pmc passes):
-gemm_one.py rows64|splitk4|dwsgd [N K iters]."""
+gemm_one.py rows64|splitk4|dwsgd|skinny_nt|skinny_nn|wgrad [N K iters]."""
 import os
 import sys
 
@@ -30,9 +30,18 @@ def main() -> int:
     Wb = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
     WbT = torch.empty(K, N, dtype=torch.bfloat16, device=dev)
     bb = torch.zeros(N, device=dev)
+    Wt = torch.randn(K, N, device=dev).to(torch.bfloat16)  # dgrad operand: W stored [K rows][N]
+    Zr = torch.randn(B, N, device=dev).to(torch.bfloat16)  # row-major dZ
+    Xr = torch.randn(B, K, device=dev).to(torch.bfloat16)  # row-major H
     for _ in range(iters):
         if kind == "rows64":
             C.gemm_bf16_nt_fused(A, W, B, N, K, obf=H, splits=0)
+        elif kind == "skinny_nt":
+            C.gemm_skinny(A, W, B, N, K, obf=H, ws=ws, ctr=ctr)
+        elif kind == "skinny_nn":
+            C.gemm_skinny(A, Wt, B, N, K, nn=True, obf=H, ws=ws, ctr=ctr)
+        elif kind == "wgrad":
+            C.wgrad_sgd(Zr, Xr, B, N, K, lr=1e-6, W=Wf, Wb=Wb, bias=bb)
         elif kind == "splitk4":
             C.gemm_bf16_nt_fused(A, W, B, N, K, obf=H, splits=4, ws=ws, ctr=ctr)
         else:
