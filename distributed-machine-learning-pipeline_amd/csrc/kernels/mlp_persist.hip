@@ -531,20 +531,30 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     }
     __syncthreads();
     // ---- dZ1 = (dZ2 W2) * (H1 > 0), published to the layer-1 blocks ----
-#pragma unroll
-    for (int t = w; t < kD1 / 16; t += 4) {
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-      const int n = 16 * t + i;
+    // wave w: n tiles w and w + 4, their four accumulator chains interleaved
+    {
+      f32x4 a0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f32x4 a1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < kD2 / 4; ks += 2) {
-        a0 = mfma_f32_16x16x4(DZ2[(rb0 + i) * kS2 + 4 * ks + q], W2[(4 * ks + q) * kS1 + n], a0);
-        a1 = mfma_f32_16x16x4(DZ2[(rb0 + i) * kS2 + 4 * ks + 4 + q], W2[(4 * ks + 4 + q) * kS1 + n], a1);
+        const float d0 = DZ2[(rb0 + i) * kS2 + 4 * ks + q];
+        const float d1 = DZ2[(rb0 + i) * kS2 + 4 * ks + 4 + q];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int n = 16 * (w + 4 * tt) + i;
+          a0[tt] = mfma_f32_16x16x4(d0, W2[(4 * ks + q) * kS1 + n], a0[tt]);
+          a1[tt] = mfma_f32_16x16x4(d1, W2[(4 * ks + 4 + q) * kS1 + n], a1[tt]);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = rb0 + 4 * q + r;
-        const float v = H1[m * kS1 + n] > 0.f ? a0[r] + a1[r] : 0.f;
-        st_gran(rb, kOffDz1 + (int64_t)m * kD1 + n, v, tag);
+      for (int tt = 0; tt < 2; ++tt) {
+        const int n = 16 * (w + 4 * tt) + i;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rb0 + 4 * q + r;
+          const float v = H1[m * kS1 + n] > 0.f ? a0[tt][r] + a1[tt][r] : 0.f;
+          st_gran(rb, kOffDz1 + (int64_t)m * kD1 + n, v, tag);
+        }
       }
     }
 
@@ -615,50 +625,37 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     // tiles.  Operands are read from LDS in batches ahead of their MFMAs (one
     // read per MFMA, issued just before it, would serialise on LDS latency).
     {
+      // dW3 [16 o][64 h] = dZ3^T H2 (o >= 10 rows are zero, wave w -> h tile w)
+      // and the biases through the MFMA pipe (dZ2^T . ones, dZ3^T . ones, the
+      // latter applied by wave 0) ride along in the same batches: their single-accumulator
+      // chains get eight independent dW2 MFMAs between consecutive steps
+      // instead of stalling on the MFMA latency one after another.  Every
+      // accumulation still runs over the rows in order 0..63.
       f32x4 g[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 g3 = {0.f, 0.f, 0.f, 0.f}, gb2 = {0.f, 0.f, 0.f, 0.f}, gb3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int mb = 0; mb < kB / 4; mb += 4) {
-        float av[4], bv[4][8];
+        float av[4], bv[4][8], a3[4], b3[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int m = 4 * (mb + u) + q;
           av[u] = DZ2[m * kS2 + 16 * w + i];
 #pragma unroll
           for (int t = 0; t < 8; ++t) bv[u][t] = H1[m * kS1 + 16 * t + i];
+          a3[u] = DZ3[m * kS3 + i];
+          b3[u] = H2[m * kS2 + 16 * w + i];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u) {
 #pragma unroll
-          for (int t = 0; t < 8; ++t) g[t] = mfma_f32_16x16x4(av[u], bv[u][t], g[t]);
-      }
-      // dW3 [16 o][64 h] = dZ3^T H2 (o >= 10 rows are zero): wave w -> h tile w
-      f32x4 g3 = {0.f, 0.f, 0.f, 0.f};
-      {
-        float a3[16], b3[16];
-#pragma unroll
-        for (int ms = 0; ms < kB / 4; ++ms) {
-          const int m = 4 * ms + q;
-          a3[ms] = DZ3[m * kS3 + i];
-          b3[ms] = H2[m * kS2 + 16 * w + i];
-        }
-#pragma unroll
-        for (int ms = 0; ms < kB / 4; ++ms) g3 = mfma_f32_16x16x4(a3[ms], b3[ms], g3);
-      }
-      // biases through the MFMA pipe: dZ2^T . ones (wave w: h tile w) and
-      // dZ3^T . ones (wave 0) — 16 MFMAs each instead of a 64-deep serial sum
-      f32x4 gb2 = {0.f, 0.f, 0.f, 0.f}, gb3 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ms = 0; ms < kB / 4; ++ms) {
-        const int m = 4 * ms + q;
-        gb2 = mfma_f32_16x16x4(DZ2[m * kS2 + 16 * w + i], 1.f, gb2);
-      }
-      if (w == 0) {
-#pragma unroll
-        for (int ms = 0; ms < kB / 4; ++ms) {
-          const int m = 4 * ms + q;
-          gb3 = mfma_f32_16x16x4(DZ3[m * kS3 + i], 1.f, gb3);
+          for (int t = 0; t < 8; ++t) {
+            g[t] = mfma_f32_16x16x4(av[u], bv[u][t], g[t]);
+            if (t == 1) g3 = mfma_f32_16x16x4(a3[u], b3[u], g3);
+            if (t == 3) gb2 = mfma_f32_16x16x4(av[u], 1.f, gb2);
+            if (t == 5) gb3 = mfma_f32_16x16x4(a3[u], 1.f, gb3);  // used by wave 0
+          }
         }
       }
       // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above)
