@@ -179,10 +179,12 @@ def run(a) -> int:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     tr.train_steps(a.steps)
-    tr.synchronize()
     if tr.backend == "hip":
-        torch.cuda.synchronize()
+        torch.cuda.synchronize()  # device-wide: every stream's steps are done
+    else:
+        tr.synchronize()
     t1 = time.perf_counter()
+    tr.synchronize()  # error checks (peer / hand-off timeouts) on the finished work
     ctx.barrier()
     elapsed = t1 - t0
     elapsed = ctx.all_reduce_scalars(elapsed, op="max")[0] if ctx.is_distributed else elapsed

@@ -462,18 +462,28 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 
     // ---- layer 2: H2 = relu(H1 W2^T + b2), wave w -> 16 output columns ----
     {
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      // four interleaved accumulator chains (a dependent MFMA waits out the
+      // previous one's latency), summed in a fixed order
+      f32x4 ac[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f},
+                     {0.f, 0.f, 0.f, 0.f}};
       const float* ha = H1 + (rb0 + i) * kS1 + q;
       const float* wb = W2 + (16 * w + i) * kS1 + q;
 #pragma unroll
-      for (int ks = 0; ks < kD1 / 4; ks += 2) {
-        a0 = mfma_f32_16x16x4(ha[4 * ks], wb[4 * ks], a0);
-        a1 = mfma_f32_16x16x4(ha[4 * ks + 4], wb[4 * ks + 4], a1);
+      for (int ks = 0; ks < kD1 / 4; ks += 4) {
+        float hv[4], wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          hv[u] = ha[4 * (ks + u)];
+          wv[u] = wb[4 * (ks + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ac[u] = mfma_f32_16x16x4(hv[u], wv[u], ac[u]);
       }
       const int n = 16 * w + i;
       const float bn = B2[n];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) H2[(rb0 + 4 * q + r) * kS2 + n] = fmaxf(a0[r] + a1[r] + bn, 0.f);
+      for (int r = 0; r < 4; ++r)
+        H2[(rb0 + 4 * q + r) * kS2 + n] = fmaxf((ac[0][r] + ac[1][r]) + (ac[2][r] + ac[3][r]) + bn, 0.f);
     }
     __syncthreads();
     // ---- layer 3 partial logits: K = 64 split over the 4 waves ----
@@ -626,15 +636,16 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     // read per MFMA, issued just before it, would serialise on LDS latency).
     {
       // dW3 [16 o][64 h] = dZ3^T H2 (o >= 10 rows are zero, wave w -> h tile w)
-      // and the biases through the MFMA pipe (dZ2^T . ones, dZ3^T . ones, the
-      // latter applied by wave 0) ride along in the same batches: their single-accumulator
-      // chains get eight independent dW2 MFMAs between consecutive steps
-      // instead of stalling on the MFMA latency one after another.  Every
-      // accumulation still runs over the rows in order 0..63.
+      // rides along in the same batches: its single-accumulator chain gets
+      // eight independent dW2 MFMAs between consecutive steps instead of
+      // stalling on the MFMA latency.  The bias gradients (column sums of dZ2,
+      // dZ3) are VALU sums of the same operands.  Every accumulation runs over
+      // the rows in a fixed order, identical in the four chains.
       f32x4 g[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 g3 = {0.f, 0.f, 0.f, 0.f}, gb2 = {0.f, 0.f, 0.f, 0.f}, gb3 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 g3 = {0.f, 0.f, 0.f, 0.f};
+      float sb2 = 0.f, sb3 = 0.f;  // bias-gradient partial sums (VALU, rows m = q mod 4)
 #pragma unroll
       for (int mb = 0; mb < kB / 4; mb += 4) {
         float av[4], bv[4][8], a3[4], b3[4];
@@ -647,36 +658,48 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           a3[u] = DZ3[m * kS3 + i];
           b3[u] = H2[m * kS2 + 16 * w + i];
         }
+        // keep the batch's LDS reads ahead of its MFMAs (one exposed LDS
+        // latency per batch instead of one per MFMA pair)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
 #pragma unroll
           for (int t = 0; t < 8; ++t) {
             g[t] = mfma_f32_16x16x4(av[u], bv[u][t], g[t]);
             if (t == 1) g3 = mfma_f32_16x16x4(a3[u], b3[u], g3);
-            if (t == 3) gb2 = mfma_f32_16x16x4(av[u], 1.f, gb2);
-            if (t == 5) gb3 = mfma_f32_16x16x4(a3[u], 1.f, gb3);  // used by wave 0
           }
+          sb2 += av[u];
+          sb3 += a3[u];
         }
       }
-      // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above)
+      // column sums over the 4 row phases q (lanes 16 apart), fixed order
+      sb2 += __shfl_xor(sb2, 16, 64);
+      sb2 += __shfl_xor(sb2, 32, 64);
+      sb3 += __shfl_xor(sb3, 16, 64);
+      sb3 += __shfl_xor(sb3, 32, 64);
+      PK_STAMP(1, 6);
+      // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above):
+      // all old values read first, then all the updated ones written
+      float w2o[8][4], w3o[4];
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i] -= a.lr * g[t][r];
+        for (int r = 0; r < 4; ++r) w2o[t][r] = W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = 4 * q + r;
-        if (o < kD3) W3[o * kS2 + 16 * w + i] -= a.lr * g3[r];
+      for (int r = 0; r < 4; ++r) w3o[r] = W3[(4 * q + r) * kS2 + 16 * w + i];
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i] = w2o[t][r] - a.lr * g[t][r];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * q + r < kD3) W3[(4 * q + r) * kS2 + 16 * w + i] = w3o[r] - a.lr * g3[r];
+      if (q == 0) {
+        B2[16 * w + i] -= a.lr * sb2;                     // h = 16 w + i
+        if (w == 0 && i < kD3) B3[i] -= a.lr * sb3;       // class i
       }
-      if (i == 0) {  // every column of the ones-product holds the sum
-#pragma unroll
-        for (int r = 0; r < 4; ++r) B2[16 * w + 4 * q + r] -= a.lr * gb2[r];
-        if (w == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (4 * q + r < kD3) B3[4 * q + r] -= a.lr * gb3[r];
-        }
-      }
+      PK_STAMP(1, 7);
     }
     __syncthreads();
     PK_STAMP(1, 5);

@@ -399,6 +399,11 @@ class MlpTrainer:
         """Enqueue `n` optimizer steps (asynchronous on GPU)."""
         if n <= 0:
             return
+        if self.pk_buf is not None and self.runner.persist_active():
+            # single replica, persistent step: ONE launch for the n steps
+            self.runner.step(n)
+            self.steps_done += n
+            return
         if self.backend == "torch":
             for _ in range(n):
                 self._torch_step()

@@ -38,6 +38,9 @@ out["step_us"] = round(statistics.median(steps), 3)
 # cross-role: chain partial-wait end vs layer-1 publish
 out["l1_publish_to_chain_ready_us"] = round(statistics.median(
     [(st[1][s][1] - st[0][s][1]) / 100.0 for s in range(8)]), 3)
+out["chain"]["dW2 MFMAs (wave 0)"] = round(statistics.median([(st[1][s][6] - st[1][s][4]) / 100.0 for s in range(8)]), 3)
+out["chain"]["W2/W3/b updates (wave 0)"] = round(statistics.median([(st[1][s][7] - st[1][s][6]) / 100.0 for s in range(8)]), 3)
+out["chain"]["barrier wait after wave 0"] = round(statistics.median([(st[1][s][5] - st[1][s][7]) / 100.0 for s in range(8)]), 3)
 out["chain_dz1_publish_to_l1_ready_us"] = round(statistics.median(
     [(st[0][s][2] - st[1][s][3]) / 100.0 for s in range(8)]), 3)
 
