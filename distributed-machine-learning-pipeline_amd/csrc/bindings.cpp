@@ -543,6 +543,37 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("head_set_stamping", &head_set_stamping);
   m.def("head_set_debug", &head_set_debug);
+  m.def("wgrad_sgd_multi", [bf16p](py::list layers) {
+    // each item: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad); tensors may be None
+    std::vector<WgLayer> v;
+    auto opt = [](py::handle h) -> c10::optional<torch::Tensor> {
+      if (h.is_none()) return c10::nullopt;
+      return h.cast<torch::Tensor>();
+    };
+    for (py::handle it : layers) {
+      py::tuple t = it.cast<py::tuple>();
+      TORCH_CHECK(t.size() == 12, "wgrad_sgd_multi: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad)");
+      torch::Tensor Z = t[0].cast<torch::Tensor>(), X = t[1].cast<torch::Tensor>();
+      const int64_t M = t[2].cast<int64_t>(), N = t[3].cast<int64_t>(), K = t[4].cast<int64_t>();
+      TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
+      TORCH_CHECK(Z.size(0) >= M && X.size(0) >= M && Z.size(1) >= ((N + 7) / 8) * 8 &&
+                  X.size(1) >= ((K + 7) / 8) * 8, "Z / X too small");
+      WgLayer a{};
+      a.Z = bf16p(Z, "Z"); a.ldz = Z.stride(0); a.X = bf16p(X, "X"); a.ldx = X.stride(0);
+      a.M = (int)M; a.N = (int)N; a.K = (int)K;
+      a.alpha = (float)t[5].cast<double>(); a.lr = (float)t[6].cast<double>();
+      auto chk2 = [&](const torch::Tensor& x, const char* nm) {
+        TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= N && x.size(1) >= K, nm, " shape");
+      };
+      if (auto W = opt(t[7])) { chk2(*W, "W"); check_f32(*W, "W"); a.W = W->data_ptr<float>(); a.ldw = W->stride(0); }
+      if (auto Wb = opt(t[8])) { chk2(*Wb, "Wb"); a.Wb = bf16p(*Wb, "Wb"); a.ldwb = Wb->stride(0); }
+      if (auto G = opt(t[9])) { chk2(*G, "G"); check_f32(*G, "G"); a.G = G->data_ptr<float>(); a.ldg = G->stride(0); }
+      if (auto b = opt(t[10])) { check_f32(*b, "bias"); TORCH_CHECK(b->numel() >= N, "bias"); a.bias = b->data_ptr<float>(); }
+      if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
+      v.push_back(a);
+    }
+    hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream()), "wgrad_sgd_multi");
+  }, py::arg("layers"));
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

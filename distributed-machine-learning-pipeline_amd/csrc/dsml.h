@@ -248,6 +248,24 @@ hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_
 hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t ldx, int M, int N,
                      int K, float alpha, float lr, float* W, int64_t ldw, uint16_t* Wb, int64_t ldwb,
                      float* G, int64_t ldg, float* bias, float* bgrad, hipStream_t s);
+struct WgLayer {
+  const uint16_t* Z;  // [M x >= N] bf16, ldz
+  int64_t ldz;
+  const uint16_t* X;  // [M x >= K] bf16, ldx
+  int64_t ldx;
+  int M, N, K;
+  float alpha, lr;
+  float* W;  // [N x K] fp32, ldw (SGD target), or null with G
+  int64_t ldw;
+  uint16_t* Wb;  // bf16 copy of the updated W (nullable), ldwb
+  int64_t ldwb;
+  float* G;  // alpha * gradient out (nullable), ldg
+  int64_t ldg;
+  float* bias;   // b -= lr * alpha * colsum(Z) (nullable)
+  float* bgrad;  // alpha * colsum(Z) out (nullable)
+};
+// Up to 4 layers' wgrad_sgd in one launch (one flattened tile grid).
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 void head_set_debug(int v);

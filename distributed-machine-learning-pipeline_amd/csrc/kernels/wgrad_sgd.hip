@@ -34,21 +34,17 @@ constexpr int kWgPitch = 68;      // floats per row of the fp32 epilogue tile
 
 __device__ __forceinline__ int wg_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
 
-struct WgArgs {
-  const uint16_t* Z;  // [M x >= N] bf16, ldz
-  int64_t ldz;
-  const uint16_t* X;  // [M x >= K] bf16, ldx
-  int64_t ldx;
-  int M, N, K;
-  float alpha, lr;
-  float* W;  // [N x K] fp32, ldw (SGD target) — or null with G
-  int64_t ldw;
-  uint16_t* Wb;  // bf16 copy of the updated W (nullable), ldwb
-  int64_t ldwb;
-  float* G;  // alpha * gradient out (nullable; used when W is null), ldg
-  int64_t ldg;
-  float* bias;   // b -= lr * db (nullable)
-  float* bgrad;  // db out (nullable)
+typedef WgLayer WgArgs;  // dsml.h: one layer's operands, targets and step
+
+// Several layers' weight gradients in ONE launch (flattened tile grid): the
+// step's last kernel updates every layer, one launch ramp and tail instead of
+// one per layer.
+constexpr int kWgMaxLayers = 4;
+struct WgMulti {
+  WgArgs l[kWgMaxLayers];
+  int start[kWgMaxLayers + 1];  // first tile of each layer (prefix sums)
+  int ktiles[kWgMaxLayers];
+  int n;
 };
 
 // Operand fragment of the 16 x 16 x 32 MFMA: lane (i, g) gets image column
@@ -65,12 +61,13 @@ __device__ __forceinline__ uint4 wg_frag(const char* img, int m0, int c0, int la
   return make_uint4(l2.x, l2.y, h2.x, h2.y);
 }
 
-__global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
-  // two operand images (16 KiB), later the fp32 epilogue tile (17 KiB)
-  __shared__ __attribute__((aligned(16))) char lds[64 * kWgPitch * 4];
-  static_assert(64 * kWgPitch * 4 >= 2 * kWgImg, "LDS carve");
+constexpr int kWgLds = 64 * kWgPitch * 4;  // two operand images (16 KiB), later the fp32 tile (17 KiB)
+static_assert(kWgLds >= 2 * kWgImg, "LDS carve");
+
+// One 64 (n) x 64 (k) tile of layer `a`: k tile kt, n tile nt.
+__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int k0 = kt * 64, n0 = nt * 64;
   char* imz = lds;
   char* imx = lds + kWgImg;
 
@@ -139,7 +136,7 @@ __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
                                                               acc[x][y], 0, 0, 0);
     }
     // bias gradient (k-tile 0 only): column sums of the Z image
-    if (blockIdx.x == 0 && tid < 64) {
+    if (kt == 0 && tid < 64) {
       const int ch = tid >> 3, e = tid & 7;
       for (int r = 0; r < 64 && mb + r < a.M; ++r) {
         const uint16_t v = *reinterpret_cast<const uint16_t*>(imz + r * 128 + 16 * (ch ^ wg_swz(r)) + 2 * e);
@@ -184,11 +181,45 @@ __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
       }
     }
   }
-  if (blockIdx.x == 0 && tid < 64 && n0 + tid < a.N) {
+  if (kt == 0 && tid < 64 && n0 + tid < a.N) {
     const float db = a.alpha * dbias;
     if (a.bias) a.bias[n0 + tid] -= a.lr * db;
     if (a.bgrad) a.bgrad[n0 + tid] = db;
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  wgrad_tile(a, blockIdx.x, blockIdx.y, lds);
+}
+
+__global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
+  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  const int b = blockIdx.x;
+  int j = 0;
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (q < m.n && b >= m.start[q]) j = q;
+  const int t = b - m.start[j];
+  // layers are few: select the operands with uniform branches, no dynamic
+  // indexing of the kernel-argument array
+  WgArgs a = m.l[0];
+  int kts = m.ktiles[0];
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
+  wgrad_tile(a, t % kts, t / kts, lds);
+}
+
+bool wg_valid(const WgArgs& a) {
+  if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
+      a.ldz < ((a.N + 7) & ~7) || a.ldx < ((a.K + 7) & ~7) || (((uintptr_t)a.Z | (uintptr_t)a.X) & 15))
+    return false;
+  if (a.W == nullptr && a.G == nullptr && a.bias == nullptr && a.bgrad == nullptr) return false;
+  if ((a.W && (((uintptr_t)a.W & 15) || (a.ldw & 3))) || (a.Wb && (((uintptr_t)a.Wb & 7) || (a.ldwb & 3))) ||
+      (a.G && (((uintptr_t)a.G & 15) || (a.ldg & 3))))
+    return false;
+  return true;
 }
 
 }  // namespace
@@ -196,15 +227,27 @@ __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
 hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t ldx, int M, int N,
                      int K, float alpha, float lr, float* W, int64_t ldw, uint16_t* Wb, int64_t ldwb,
                      float* G, int64_t ldg, float* bias, float* bgrad, hipStream_t s) {
-  if (M < 1 || N < 1 || K < 8 || (K & 3) || (ldz & 7) || (ldx & 7) || ldz < ((N + 7) & ~7) ||
-      ldx < ((K + 7) & ~7) || (((uintptr_t)Z | (uintptr_t)X) & 15))
-    return hipErrorInvalidValue;
-  if (W == nullptr && G == nullptr && bias == nullptr && bgrad == nullptr) return hipErrorInvalidValue;
-  if ((W && (((uintptr_t)W & 15) || (ldw & 3))) || (Wb && (((uintptr_t)Wb & 7) || (ldwb & 3))) ||
-      (G && (((uintptr_t)G & 15) || (ldg & 3))))
-    return hipErrorInvalidValue;
   WgArgs a{Z, ldz, X, ldx, M, N, K, alpha, lr, W, ldw, Wb, ldwb, G, ldg, bias, bgrad};
+  if (!wg_valid(a)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wgrad_sgd_k, dim3((K + 63) / 64, (N + 63) / 64), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s) {
+  if (n < 1 || n > kWgMaxLayers) return hipErrorInvalidValue;
+  WgMulti m{};
+  m.n = n;
+  int t = 0;
+  for (int j = 0; j < n; ++j) {
+    if (!wg_valid(layers[j])) return hipErrorInvalidValue;
+    m.l[j] = layers[j];
+    m.start[j] = t;
+    m.ktiles[j] = (layers[j].K + 63) / 64;
+    t += m.ktiles[j] * ((layers[j].N + 63) / 64);
+  }
+  for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
+  for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
+  hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
   return hipGetLastError();
 }
 

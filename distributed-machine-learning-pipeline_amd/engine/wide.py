@@ -200,6 +200,21 @@ class WideMlpTrainer:
         fused_sgd = world == 1
         scale = self.lr / world
         main = torch.cuda.current_stream(self.device)
+        if fused_sgd and self._ss is None:
+            # every dgrad first (they read this step's bf16 weights), then ONE
+            # launch updates every layer: W -= lr * dZ_{l+1}^T H_l, the next step's
+            # bf16 copies, the biases (kernels/wgrad_sgd.hip, flattened tile grid)
+            for l in range(L - 2 if self.fused_head else L - 1, 0, -1):
+                self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
+            layers = []
+            for l in range(L - 1, -1, -1):
+                W, b = self.views[l]
+                layers.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, W, nxt[l],
+                               None, b, None))
+            for i in range(0, len(layers), 4):
+                C.wgrad_sgd_multi(layers[i:i + 4])
+            self.steps_done += 1
+            return
         for l in range(L - 1, -1, -1):
             W, b = self.views[l]
             gW, gb = self.gviews[l]

@@ -114,3 +114,29 @@ def test_wgrad_sgd_matches_fp32(M, N, K):
     torch.cuda.synchronize()
     assert (G - Gref).abs().max().item() < 1e-4
     assert (db - alpha * Z[:, :N].float().sum(0)).abs().max().item() < 1e-4
+
+
+def test_wgrad_sgd_multi_matches_per_layer_launches():
+    """Three layers' updates in one flattened launch == one launch per layer, bit for bit."""
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(77)
+    shapes = [(10, 4096), (4096, 4096), (4096, 784)]  # (N, K) of the wide MLP's layers, top down
+    M = 64
+    args_a, args_b = [], []
+    for N, K in shapes:
+        pn, pk = (N + 15) // 16 * 16, (K + 15) // 16 * 16
+        Z = torch.zeros(M, pn, dtype=torch.bfloat16)
+        X = torch.zeros(M, pk, dtype=torch.bfloat16)
+        Z[:, :N] = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        X[:, :K] = torch.randn(M, K, generator=g).to(torch.bfloat16)
+        W = torch.randn(N, K, generator=g)
+        b = torch.randn(N, generator=g)
+        for lst in (args_a, args_b):
+            lst.append((Z.to(DEV), X.to(DEV), M, N, K, 1.0, 0.01, W.to(DEV),
+                        torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV), None, b.to(DEV), None))
+    C.wgrad_sgd_multi(args_a)
+    for (Z, X, M_, N, K, al, lr, W, Wb, G, b, bg) in args_b:
+        C.wgrad_sgd(Z, X, M_, N, K, alpha=al, lr=lr, W=W, Wb=Wb, bias=b)
+    torch.cuda.synchronize()
+    for a, b in zip(args_a, args_b):
+        assert torch.equal(a[7], b[7]) and torch.equal(a[8], b[8]) and torch.equal(a[10], b[10])
