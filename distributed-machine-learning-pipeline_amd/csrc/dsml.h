@@ -220,6 +220,8 @@ hipError_t softmax_xent(const float* logits, int64_t ldl, const int32_t* labels,
                         int Cp, float inv_batch, uint16_t* dz, int64_t ldz, uint16_t* dzT,
                         int64_t ldt, float* stats, hipStream_t s);
 // Classifier head fused with softmax-CE (C <= 16, K <= 4096): logits = H . W^T
+// (row_stats: loss / correct / count accumulate in stats[4m ..] per row m,
+// summed by the reader, instead of atomics on stats[0..2])
 // + b per row, then the softmax_xent outputs.  `logits` may be null.  With
 // `dzp`, also the next backward product: dzp = (dz . W) * (H > 0) in bf16
 // (+ the transposed copy dzpT), from operands the kernel already holds.
@@ -228,7 +230,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp = nullptr, int64_t ldzp = 0, uint16_t* dzpT = nullptr,
-                             int64_t ldpt = 0);
+                             int64_t ldpt = 0, int row_stats = 0);
 // Skinny GEMMs (kernels/gemm_skinny.hip): C[M x N] = A[M x K] . B^T for
 // B [N x K] (nn = false) or A . B for B [K x N] (nn = true: W read in its
 // stored layout through transposing LDS reads), 64 x 64 tiles, K split S ways

@@ -730,7 +730,8 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
     float inv_batch, float* __restrict__ logits, int64_t ldl, uint16_t* __restrict__ dz,
     int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats,
-    uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt) {
+    uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt,
+    int row_stats) {
   __shared__ float part[kHeadMaxC][257];  // per-thread partial dot products, per class
   __shared__ float zsum[kHeadMaxC];
   __shared__ float gz[kHeadMaxC];         // bf16-rounded dLogits of this row
@@ -808,9 +809,18 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     }
     if (c < kHeadMaxC) gz[c] = bf16_to_f32(hq);
     if (c == y && stats && !(g_head_dbg & 1)) {
-      atomicAdd(stats + 0, -logf(p + 1e-10f));
-      atomicAdd(stats + 1, am == y ? 1.f : 0.f);
-      atomicAdd(stats + 2, 1.f);
+      if (row_stats) {
+        // this row's own accumulators (stats[4m .. 4m+2]: only this workgroup
+        // writes them): no same-address atomics from 64 workgroups per step
+        float* r = stats + 4 * (int64_t)m;
+        r[0] += -logf(p + 1e-10f);
+        r[1] += am == y ? 1.f : 0.f;
+        r[2] += 1.f;
+      } else {
+        atomicAdd(stats + 0, -logf(p + 1e-10f));
+        atomicAdd(stats + 1, am == y ? 1.f : 0.f);
+        atomicAdd(stats + 2, 1.f);
+      }
     }
   }
   HEAD_STAMP(3);
@@ -869,7 +879,8 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              const float* bias, int B, int K, int C, const int32_t* labels,
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
-                             uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt) {
+                             uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt,
+                             int row_stats) {
   if (dzp && ((ldzp & 7) || ((uintptr_t)dzp & 15))) return hipErrorInvalidValue;
   if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
       (ldw & 7) ||
@@ -877,7 +888,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_softmax_xent_k, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
                      labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
-                     ldpt);
+                     ldpt, row_stats);
   return hipGetLastError();
 }
 

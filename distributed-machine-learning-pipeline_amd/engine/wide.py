@@ -90,7 +90,9 @@ class WideMlpTrainer:
         self.H = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L)]
         self.dZ = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L + 1)]
         self.logits = torch.zeros(batch, d[L], dtype=torch.float32, device=dev)
-        self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
+        # per-row loss / correct / count accumulators (the head kernel's row_stats
+        # form: no same-address atomics), summed by read_stats
+        self.stats = torch.zeros(batch * 4, dtype=torch.float32, device=dev)
         self.views = self.layout.views(self.P)
         self.gviews = self.layout.views(self.G)
         self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
@@ -190,7 +192,7 @@ class WideMlpTrainer:
             prev = L >= 2
             C.head_softmax_xent(self.H[L - 1], cur[L - 1], b, Bt, self.pd[L - 1], d[L],
                                 self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], None,
-                                self.stats, dzp=self.dZ[L - 1] if prev else None)
+                                self.stats, dzp=self.dZ[L - 1] if prev else None, row_stats=True)
         else:
             C.gemm_bf16_nt_fused(self.H[L - 1], cur[L - 1], Bt, d[L], d[L - 1], bias=b,
                                  of32=self.logits, splits=0)
@@ -318,7 +320,7 @@ class WideMlpTrainer:
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         self.synchronize()
-        v = self.stats.tolist()
+        v = self.stats.view(-1, 4).sum(0).tolist()
         if reset:
             self.stats.zero_()
         s = StepStats(v[0], v[1], v[2])
@@ -353,7 +355,7 @@ class WideMlpTrainer:
         X = ds.X.to(self.device, torch.float32).contiguous()
         y = ds.y.to(self.device, torch.int32).contiguous()
         n = X.shape[0]
-        st = torch.zeros(4, dtype=torch.float32, device=self.device)
+        st = torch.zeros(Bt * 4, dtype=torch.float32, device=self.device)
         xb = torch.zeros(Bt, self.pd[0], dtype=torch.bfloat16, device=self.device)
         with torch.cuda.device(self.device):
             self.synchronize()
@@ -368,10 +370,11 @@ class WideMlpTrainer:
                 _, b = self.views[L - 1]
                 if self.fused_head:
                     C.head_softmax_xent(self.H[L - 1], self.wb(L - 1), b, m, self.pd[L - 1], d[L],
-                                        y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st)
+                                        y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st,
+                                        row_stats=True)
                 else:
                     C.gemm_bf16_nt_fused(self.H[L - 1], self.wb(L - 1), m, d[L], d[L - 1], bias=b,
                                          of32=self.logits, splits=0)
                     C.softmax_xent(self.logits, y[r0:r0 + m], m, d[L], 1.0 / m, self.dZ[L], None, st)
-            v = st.tolist()
+            v = st.view(-1, 4).sum(0).tolist()
         return {"loss": v[0] / max(n, 1), "accuracy": 100.0 * v[1] / max(n, 1), "n": n}

@@ -131,6 +131,14 @@ def test_head_softmax_xent(C_, K):
     assert stats[2].item() == B
     loss = -torch.log(p.gather(1, y.long().view(-1, 1)) + 1e-10).sum().item()
     assert abs(stats[0].item() - loss) / loss < 1e-3
+    # per-row accumulators (no atomics): the rows' sums equal the atomic totals
+    rows = torch.zeros(B * 4, device=DEV)
+    C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
+                        dzT, rows, row_stats=True)
+    torch.cuda.synchronize()
+    tot = rows.view(-1, 4).sum(0)
+    assert tot[2].item() == B and torch.all(rows.view(-1, 4)[:, 2] == 1)
+    assert abs(tot[0].item() - loss) / loss < 1e-3 and tot[1].item() == stats[1].item()
     # fused next activation gradient: dZ_prev = (bf16(dZ) . W) * (H > 0)
     Kp = (K + 15) // 16 * 16
     dzp = torch.zeros(B, Kp, dtype=torch.bfloat16, device=DEV)
