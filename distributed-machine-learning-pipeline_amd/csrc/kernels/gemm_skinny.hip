@@ -56,6 +56,30 @@ __device__ __forceinline__ f32x4 sk_mfma(uint4 a, uint4 b, f32x4 c) {
 }
 __device__ __forceinline__ float sk_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float sk_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+// LDS fragment reads as inline asm: the compiler cannot tell which LDS-DMA
+// wrote which ring buffer, so before any ds_read it emits itself it waits for
+// ALL outstanding DMA (vmcnt(0)) — including the next stage's, which collapses
+// the double buffer.  Ordering is explicit instead: the per-stage vmcnt wait
+// before the reads, and sk_lgkm0 after them (it also carries the read
+// results, so no use can be scheduled above it).
+typedef uint32_t sk_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sk_la(const void* p) { return (uint32_t)(uintptr_t)(sk_lptr)p; }
+__device__ __forceinline__ sk_u4 sk_ds128(uint32_t addr) {
+  sk_u4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ sk_u2 sk_dstr(uint32_t addr) {
+  sk_u2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void sk_lgkm0(sk_u4 (&a)[4], sk_u4 (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
+               :: "memory");
+}
+
 // 16-B chunk swizzles of the two image kinds (row pitch 128 B, 8 chunks).
 __device__ __forceinline__ int sk_swz_row(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int sk_swz_tr(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
@@ -124,37 +148,42 @@ __device__ __forceinline__ void sk_compute(const SkArgs& a, const char* ring, in
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const bool kv = stage * kSkStage + 32 * h + 8 * g < a.K;
-    uint4 fa[4], fb[4];
+    const uint32_t la = sk_la(img_a), lb = sk_la(img_b);
+    sk_u4 fa[4], fb[4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int r = 16 * x + i;
-      const uint4 v = *reinterpret_cast<const uint4*>(img_a + r * 128 + 16 * ((4 * h + g) ^ sk_swz_row(r)));
-      fa[x] = kv ? v : make_uint4(0u, 0u, 0u, 0u);
+      fa[x] = sk_ds128(la + r * 128 + 16 * ((4 * h + g) ^ sk_swz_row(r)));
     }
     if (NN) {
       const int q = (lane & 15) >> 2, p = lane & 3;
+      sk_u2 lo[4], hi[4];
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
         const int c = 2 * y + (p >> 1);
         const int r0 = 32 * h + 8 * g + q, r1 = r0 + 4;
-        const sk_i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (sk_lv4)(img_b + r0 * 128 + 16 * (c ^ sk_swz_tr(r0)) + 8 * (p & 1)));
-        const sk_i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (sk_lv4)(img_b + r1 * 128 + 16 * (c ^ sk_swz_tr(r1)) + 8 * (p & 1)));
-        const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-        fb[y] = make_uint4(l2.x, l2.y, h2.x, h2.y);
+        lo[y] = sk_dstr(lb + r0 * 128 + 16 * (c ^ sk_swz_tr(r0)) + 8 * (p & 1));
+        hi[y] = sk_dstr(lb + r1 * 128 + 16 * (c ^ sk_swz_tr(r1)) + 8 * (p & 1));
       }
+#pragma unroll
+      for (int y = 0; y < 4; ++y) fb[y] = sk_u4{lo[y].x, lo[y].y, hi[y].x, hi[y].y};
     } else {
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
         const int r = 16 * y + i;
-        fb[y] = *reinterpret_cast<const uint4*>(img_b + r * 128 + 16 * ((4 * h + g) ^ sk_swz_row(r)));
+        fb[y] = sk_ds128(lb + r * 128 + 16 * ((4 * h + g) ^ sk_swz_row(r)));
       }
+    }
+    sk_lgkm0(fa, fb);
+    if (!kv) {  // K tail (clamped loads): zero contribution
+#pragma unroll
+      for (int x = 0; x < 4; ++x) fa[x] = sk_u4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
-      for (int y = 0; y < 4; ++y) acc[x][y] = sk_mfma(fa[x], fb[y], acc[x][y]);
+      for (int y = 0; y < 4; ++y)
+        acc[x][y] = sk_mfma(__builtin_bit_cast(uint4, fa[x]), __builtin_bit_cast(uint4, fb[y]), acc[x][y]);
   }
 }
 
