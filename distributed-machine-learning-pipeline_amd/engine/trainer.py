@@ -71,7 +71,8 @@ class MlpTrainer:
                  params: Optional[torch.Tensor] = None, external_comm=None,
                  capture_collectives: Optional[bool] = None, xchg_timeout_ms: float = 10000.0,
                  xact_waves: int = 0, auto_fallback: str = "rccl",
-                 stream: Optional["torch.cuda.Stream"] = None, persist: Optional[bool] = None):
+                 stream: Optional["torch.cuda.Stream"] = None, persist: Optional[bool] = None,
+                 grad_allreduce=None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -100,6 +101,10 @@ class MlpTrainer:
         self.steps_done = 0
         self._stats_cpu = StepStats()
         self.comm = external_comm
+        # host replicas without a process group (device servers on CPU): a
+        # callable that sums the flat fp32 gradient over the replicas in place
+        # (the device-driven gRPC ring, rpc/device_server.py _rpc_ring)
+        self.grad_allreduce = grad_allreduce
         self.xchg = None
         if capture_collectives is None:  # RCCL collectives recorded into the step graphs
             import os
@@ -568,7 +573,9 @@ class MlpTrainer:
         self._stats_cpu.correct += float(correct)
         self._stats_cpu.count += self.batch
         world = self.ctx.world_size
-        if self.ctx.is_distributed:
+        if self.grad_allreduce is not None:
+            self.grad_allreduce(g)
+        elif self.ctx.is_distributed:
             import torch.distributed as dist
 
             with self.ctx.guard("gradient all_reduce"):

@@ -81,7 +81,11 @@ class TrainingClient:
     def train_device_mode(self, epochs: int, samples_per_rank: int, graph_steps: int = 50,
                           sync: str = "rccl", eval_samples: int = 10000) -> dict:
         n = len(self.devs)
-        self.comm_init("rccl" if n > 1 else "rpc")
+        # GPU device servers sum gradients over RCCL; host (CPU) device servers
+        # over the device-driven gRPC ring (DeviceAllReduce's transfers)
+        backends = {s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata.backend
+                    for s in self.devs}
+        self.comm_init("rccl" if n > 1 and backends == {"hip"} else "rpc")
 
         def cfg(i, s):
             return s.ConfigureModel(pb.ConfigureModelRequest(

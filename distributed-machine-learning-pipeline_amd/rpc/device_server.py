@@ -20,7 +20,7 @@ import torch
 
 from ..runtime.device import (DT_SIZE, STATUS_FAILED, STATUS_IN_PROGRESS, STATUS_SUCCESS,
                               TORCH_DTYPES, OutOfRange, _Device, make_device)
-from .proto import pb
+from .proto import DT_FLOAT32, SUM, pb
 from .stubs import GPUDeviceStub, connect, serve
 
 log = logging.getLogger("hipdsml.device")
@@ -458,19 +458,53 @@ class GPUDeviceServicer:
             params = layout.from_reference(np.frombuffer(raw, dtype=np.float32))
         ctx = DistContext(rank=rank, world_size=world, device=self._torch_device())
         comm = self.comms.get(request.commId) if world > 1 else None
-        if world > 1 and comm is None and self.dev.backend == "hip":
-            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
-                          "data-parallel TrainSteps needs an RCCL comm (CommInit backend=rccl)")
+        host_ar = None
+        if world > 1 and comm is None:
+            if self.dev.backend == "hip":
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                              "data-parallel TrainSteps needs an RCCL comm (CommInit backend=rccl)")
+            meta = self.comm_meta.get(request.commId)
+            if meta is None or meta["nranks"] != world or meta["rank"] != rank:
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                              f"data-parallel TrainSteps on host devices needs comm {request.commId} "
+                              f"set up with rank {rank} of {world} (CommInit backend=rpc)")
+            host_ar = self._host_grad_allreduce(request.commId, world, layout.nparams * 4)
         try:
             self.trainer = MlpTrainer(spec, ds, batch=batch, lr=request.lr or 0.01, ctx=ctx,
                                       seed=request.seed, momentum=request.momentum,
                                       graph_steps=request.graphSteps, params=params,
-                                      external_comm=comm, sync=request.sync or "rccl")
+                                      external_comm=comm, sync=request.sync or "rccl",
+                                      grad_allreduce=host_ar)
         except (ValueError, RuntimeError) as e:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         return pb.ConfigureModelResponse(success=True, numParams=spec.num_params,
                                          batchesPerEpoch=self.trainer.nbatches,
                                          paramBytes=layout.nparams * 4)
+
+    def _host_grad_allreduce(self, cid: int, n: int, nbytes: int):
+        """Gradient sum for host replicas trained by TrainSteps: each step's flat
+        fp32 gradient is staged in this device's private scratch window, summed
+        over the communicator by the device-driven gRPC ring (`_rpc_ring`, the
+        same transfers as DeviceAllReduce) and read back.  The ring's receive
+        segment sits at the bottom of the window, the gradient right above it.
+        Every replica applies the same summed gradient, so they stay identical
+        (the reference instead broadcast weights after each step,
+        client.go:596-647)."""
+        seg = (-(-(nbytes // 4) // n) + 3) // 4 * 16
+        gaddr = self.dev.scratch_addr + (seg + 255) // 256 * 256
+        if gaddr + nbytes > self.dev.max_addr + self.dev.scratch_size:
+            raise ValueError(f"gradient of {nbytes} B does not fit the {self.dev.scratch_size} B "
+                             "ring scratch window")
+
+        def allreduce(g: torch.Tensor) -> None:
+            self.dev.write(gaddr, g.detach().float().contiguous().numpy().tobytes(), internal=True,
+                           record=False)
+            self._rpc_ring(cid, gaddr, nbytes, DT_FLOAT32, SUM, 0)
+            g.copy_(torch.frombuffer(bytearray(self.dev.read(gaddr, nbytes, internal=True)),
+                                     dtype=torch.float32).view_as(g))
+            self.counters["allreduces"] += 1
+
+        return allreduce
 
     def _need_trainer(self, context):
         if self.trainer is None:
@@ -479,9 +513,6 @@ class GPUDeviceServicer:
 
     def TrainSteps(self, request, context):
         tr = self._need_trainer(context)
-        if tr.backend == "torch" and tr.ctx.world_size > 1:
-            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
-                          "host devices train data-parallel through the RPC ring (client rpc mode)")
         t0 = time.perf_counter()
         try:
             tr.train_steps(int(request.steps))

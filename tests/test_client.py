@@ -55,3 +55,38 @@ def test_device_mode_single_host_device():
     assert lines[1].startswith("Epoch 1 complete") and lines[2].startswith("Epoch 2 complete")
     assert lines[-1].startswith("Final Test Accuracy:")
     assert res["steps_per_epoch"] == 20
+
+
+def test_device_mode_host_data_parallel_matches_reference():
+    """ConfigureModel + TrainSteps on 3 host device servers (the reference's
+    3-device client, client.go:532-539): each server trains its own shard and
+    sums every step's gradient over the device-driven gRPC ring.  Replicas stay
+    identical and equal single-process SGD on the averaged gradient."""
+    n, batch, spe, epochs = 3, 16, 5, 2
+    dims = (784, 32, 16, 10)
+    lines = []
+    with cluster(n_devices=n, mem_size=1 << 20) as c:
+        cl = TrainingClient(c.coord_addr, c.addresses, dims, batch=batch, lr=0.05, seed=3,
+                            out=lines.append)
+        try:
+            res = cl.train_device_mode(epochs=epochs, samples_per_rank=batch * spe, graph_steps=0,
+                                       eval_samples=128)
+        finally:
+            cl.close()
+        got = [c.devices[i][2].trainer.P.clone() for i in range(n)]
+        stats = [c.devices[i][2].counters["allreduces"] for i in range(n)]
+    for g in got[1:]:
+        assert torch.equal(g, got[0])
+    assert stats == [epochs * spe] * n
+    spec = MlpSpec(dims)
+    lay = MlpLayout(spec, batch, 1)
+    P = init_params(lay, 3)
+    shards = [synthetic_mnist(batch * spe, seed=1000 + r, dim=784) for r in range(n)]
+    for s in range(epochs * spe):
+        b = s % spe
+        g = sum(grads_ref(lay, P, d.X[b * batch:(b + 1) * batch], d.y[b * batch:(b + 1) * batch])[0]
+                for d in shards)
+        P = P - 0.05 * g / n
+    assert (got[0] - P).abs().max().item() < 1e-5
+    assert res["steps_per_epoch"] == spe
+    assert lines[1].startswith("Epoch 1 complete") and lines[-1].startswith("Final Test Accuracy:")
