@@ -64,26 +64,48 @@ __device__ __forceinline__ uint4 wg_frag(const char* img, int m0, int c0, int la
 constexpr int kWgLds = 64 * kWgPitch * 4;  // two operand images (16 KiB), later the fp32 tile (17 KiB)
 static_assert(kWgLds >= 2 * kWgImg, "LDS carve");
 
-// One 64 (n) x 64 (k) tile of layer `a`: k tile kt, n tile nt.
-__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
+// 1. a tile's W loads (rows rl + 16j, columns cl..cl+3), issued before anything else
+__device__ __forceinline__ void wg_load_w(const WgArgs& a, int kt, int nt, float4 (&wold)[4]) {
+  const int tid = threadIdx.x, rl = tid >> 4, kc = kt * 64 + 4 * (tid & 15);
+  const bool kv = kc < a.K;  // K % 4 == 0: a 4-column group is whole or absent
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nr = min(nt * 64 + rl + 16 * j, a.N - 1);
+    wold[j] = (kv && a.W) ? *reinterpret_cast<const float4*>(a.W + (int64_t)nr * a.ldw + kc)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// 2. Z[mb.., n0..] and X[mb.., k0..] as row-major images: 2 LDS-DMA pieces per wave each
+__device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb, char* lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  char* imz = lds;
+  char* imx = lds + kWgImg;
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) {
+    const int piece = 2 * w + pc;  // 8 rows x 128 B
+    const int r = 8 * piece + (lane >> 3), p = lane & 7;
+    const int m = min(mb + r, a.M - 1);
+    const int zc = min(n0 + 8 * (p ^ wg_swz(r)), (int)((a.N + 7) & ~7) - 8);
+    const int xc = min(k0 + 8 * (p ^ wg_swz(r)), (int)((a.K + 7) & ~7) - 8);
+    __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + zc),
+                                     (wg_lptr)(imz + piece * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + xc),
+                                     (wg_lptr)(imx + piece * 1024), 16, 0, 0);
+  }
+}
+
+// 2-4. One 64 (n) x 64 (k) tile of layer `a` (k tile kt, n tile nt) whose W
+// loads are already in flight in `wold`.
+__device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt, char* lds,
+                                                const float4 (&wold)[4]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int k0 = kt * 64, n0 = nt * 64;
   char* imz = lds;
   char* imx = lds + kWgImg;
-
-  // ---- 1. the W tile's loads go out first (rows rl + 16j, columns cl..cl+3) ----
   const int rl = tid >> 4, cl = 4 * (tid & 15);
   const int kc = k0 + cl;
-  const bool kv = kc < a.K;  // K % 4 == 0: a 4-column group is whole or absent
-  float4 wold[4];
-  if (a.W) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nr = min(n0 + rl + 16 * j, a.N - 1);
-      wold[j] = kv ? *reinterpret_cast<const float4*>(a.W + (int64_t)nr * a.ldw + kc)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
+  const bool kv = kc < a.K;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -94,19 +116,8 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
   const int wn = (w >> 1) * 32, wk = (w & 1) * 32;
 
   for (int mb = 0; mb < a.M; mb += 64) {
-    // ---- 2. Z[mb.., n0..] and X[mb.., k0..] row-major images, 2 LDS-DMA pieces per wave each ----
-#pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-      const int piece = 2 * w + pc;  // 8 rows x 128 B
-      const int r = 8 * piece + (lane >> 3), p = lane & 7;
-      const int m = min(mb + r, a.M - 1);
-      const int zc = min(n0 + 8 * (p ^ wg_swz(r)), (int)((a.N + 7) & ~7) - 8);
-      const int xc = min(k0 + 8 * (p ^ wg_swz(r)), (int)((a.K + 7) & ~7) - 8);
-      __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + zc),
-                                       (wg_lptr)(imz + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + xc),
-                                       (wg_lptr)(imx + piece * 1024), 16, 0, 0);
-    }
+    // ---- 2. Z[mb.., n0..] and X[mb.., k0..] row-major images ----
+    wg_stage(a, k0, n0, mb, lds);
     full_barrier();  // every piece landed (vmcnt(0) also retires the W loads: issued earlier)
 
     // ---- 3. MFMAs: wave tile 32 n x 32 k, reduction over the batch rows ----
@@ -143,7 +154,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
         dbias += bf16_to_f32(v);
       }
     }
-    __syncthreads();  // images free for the next batch block / the epilogue tile
+    lds_barrier();  // images free for the next batch block / the epilogue tile (no DMA in flight here)
   }
 
   // ---- 4. epilogue: acc -> LDS tile [64 n][64 k] -> float4 RMW of W + bf16 copy ----
@@ -188,6 +199,12 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
   }
 }
 
+__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
+  float4 wold[4];
+  wg_load_w(a, kt, nt, wold);
+  wgrad_tile_body(a, kt, nt, lds, wold);
+}
+
 __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kWgLds];
   wgrad_tile(a, blockIdx.x, blockIdx.y, lds);
@@ -209,6 +226,50 @@ __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
   for (int q = 1; q < kWgMaxLayers; ++q)
     if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
   wgrad_tile(a, t % kts, t / kts, lds);
+}
+
+// Tile selection of the flattened multi-layer grid (probe kernels below).
+__device__ __forceinline__ void wg_pick(const WgMulti& m, int b, WgArgs& a, int& kt, int& nt) {
+  int j = 0;
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (q < m.n && b >= m.start[q]) j = q;
+  const int t = b - m.start[j];
+  a = m.l[0];
+  int kts = m.ktiles[0];
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
+  kt = t % kts;
+  nt = t / kts;
+}
+
+// roofline probes (variant 20 / 21): the tile kernel without operand staging
+// and MFMAs, and a plain grid-stride stream of the same bytes (W fp32 RMW +
+// bf16 copy)
+__global__ __launch_bounds__(256) void wgrad_nomma_k(WgMulti m) {
+  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  WgArgs a;
+  int kt, nt;
+  wg_pick(m, blockIdx.x, a, kt, nt);
+  a.M = 0;
+  wgrad_tile(a, kt, nt, lds);
+}
+
+__global__ __launch_bounds__(256) void wgrad_stream_k(WgMulti m) {
+  for (int j = 0; j < m.n; ++j) {
+    const WgArgs a = m.l[j];
+    const int64_t n4 = (int64_t)a.N * a.K / 4;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+      const int64_t e = 4 * i, r = e / a.K, c = e % a.K;
+      float4 v = *reinterpret_cast<const float4*>(a.W + r * a.ldw + c);
+      v.x -= a.lr; v.y -= a.lr; v.z -= a.lr; v.w -= a.lr;
+      __builtin_nontemporal_store(wg_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<wg_f4*>(a.W + r * a.ldw + c));
+      const uint32_t lo = f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
+      const uint32_t hi = f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+      __builtin_nontemporal_store(wg_u2{lo, hi}, reinterpret_cast<wg_u2*>(a.Wb + r * a.ldwb + c));
+    }
+  }
 }
 
 bool wg_valid(const WgArgs& a) {
@@ -233,7 +294,7 @@ hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t 
   return hipGetLastError();
 }
 
-hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s) {
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int variant, int grid) {
   if (n < 1 || n > kWgMaxLayers) return hipErrorInvalidValue;
   WgMulti m{};
   m.n = n;
@@ -247,7 +308,13 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s) {
   }
   for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
   for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
-  hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
+  if (variant == 20) {
+    hipLaunchKernelGGL(wgrad_nomma_k, dim3(t), dim3(256), 0, s, m);
+  } else if (variant == 21) {
+    hipLaunchKernelGGL(wgrad_stream_k, dim3(grid > 0 ? grid : 8192), dim3(256), 0, s, m);
+  } else {
+    hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
+  }
   return hipGetLastError();
 }
 
