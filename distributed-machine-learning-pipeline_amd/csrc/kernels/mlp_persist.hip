@@ -41,6 +41,7 @@
 // fault ends the launch instead of hanging the GPU.
 #include "common.h"
 #include "../dsml.h"
+#include <cstdlib>
 
 namespace dsml {
 
@@ -188,6 +189,7 @@ struct PersistArgs {
   uint32_t* err;
   uint32_t* herr;  // host-mapped mirror of err (nullable): read without a copy
   uint64_t timeout_ticks;
+  int32_t place;  // block -> role map: 1 = chains at b % 8 == 0 (one XCD, default), 0 = chains last
 };
 
 // A block that gave up leaves a mark in host memory on its way out, so the
@@ -733,10 +735,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
 void mlp_persist_k(PersistArgs a) {
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
-  if ((int)blockIdx.x < kNL1)
-    pk_layer1(a, lds, blockIdx.x);
+  const int b = blockIdx.x;
+  if (a.place == 1) {
+    // the 4 chain blocks exchange rows every step: blocks 0, 8, 16, 24 share
+    // one XCD under round-robin placement (speed only, the hand-offs are
+    // placement-independent)
+    if (b < 8 * kNCH && (b & 7) == 0)
+      pk_chain(a, lds, b >> 3);
+    else
+      pk_layer1(a, lds, b < 8 * kNCH ? b - (b >> 3) - 1 : b - kNCH);
+    return;
+  }
+  if (b < kNL1)
+    pk_layer1(a, lds, b);
   else
-    pk_chain(a, lds, blockIdx.x - kNL1);
+    pk_chain(a, lds, b - kNL1);
 }
 
 hipError_t mlp_persist_read_stamps(uint64_t* host_out) {
@@ -782,6 +795,11 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   a.err = err;
   a.herr = herr;
   a.timeout_ticks = timeout_ticks;
+  static const int place = [] {
+    const char* e = getenv("HIPDSML_PK_PLACE");  // 0: the old map (A/B only)
+    return e ? atoi(e) : 1;
+  }();
+  a.place = place;
   const size_t lds = (size_t)kLdsFloats * sizeof(float);
   static bool attr = false;
   if (!attr) {
