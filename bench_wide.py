@@ -19,7 +19,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="784-4096-4096-10")
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--sync", default="rccl", choices=["rccl", "ring", "torch"])
+    ap.add_argument("--sync", default="xact", choices=["xact", "rccl", "ring", "torch"],
+                    help="N > 1: xact = all-gather the bf16 activations (about 2 MB per replica "
+                         "per step), rccl / ring = all-reduce the fp32 gradients (80 MB)")
     a = ap.parse_args()
     import bench
 

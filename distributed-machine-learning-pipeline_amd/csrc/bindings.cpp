@@ -842,6 +842,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         check_cuda(t, "t");
         s.c->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());
       })
+      .def("allgather_", [](PyComm& s, torch::Tensor t) {
+        check_cuda(t, "t");
+        TORCH_CHECK(t.is_contiguous() && t.numel() % s.c->nranks() == 0,
+                    "allgather_: contiguous, nranks equal parts");
+        s.c->allgather(t.data_ptr(), t.numel() / s.c->nranks(), dtype_of(t), cur_stream());
+      }, py::arg("t"), "in-place all-gather: rank r contributes part r of t")
       .def("send", [](PyComm& s, torch::Tensor t, int peer) {
         check_cuda(t, "t");
         s.c->send(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());

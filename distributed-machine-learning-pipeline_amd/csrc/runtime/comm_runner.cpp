@@ -184,6 +184,14 @@ void RcclComm::broadcast(void* buf, int64_t count, int32_t dtype, int root, hipS
   check(ncclBroadcast(buf, buf, (size_t)count, to_nccl(dtype), root, comm_, s), "ncclBroadcast");
 }
 
+void RcclComm::allgather(void* buf, int64_t count, int32_t dtype, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("allgather on aborted communicator");
+  uint8_t* b = static_cast<uint8_t*>(buf);
+  check(ncclAllGather(b + (size_t)rank_ * (size_t)count * dtype_size(dtype), b, (size_t)count,
+                      to_nccl(dtype), comm_, s),
+        "ncclAllGather");
+}
+
 void RcclComm::send(const void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s) {
   check(ncclSend(buf, (size_t)count, to_nccl(dtype), peer, comm_, s), "ncclSend");
 }

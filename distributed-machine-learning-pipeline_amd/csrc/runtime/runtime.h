@@ -168,6 +168,8 @@ class RcclComm {
   // stream capture (ring_allreduce refuses to grow it while capturing).
   void reserve_ring(int64_t count, int32_t dtype, int64_t chunk_bytes, int max_rings = 0);
   void broadcast(void* buf, int64_t count, int32_t dtype, int root, hipStream_t s);
+  // in-place all-gather: rank r's `count` elements sit at buf + r * count
+  void allgather(void* buf, int64_t count, int32_t dtype, hipStream_t s);
   void send(const void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
   void recv(void* buf, int64_t count, int32_t dtype, int peer, hipStream_t s);
   void barrier(hipStream_t s);

@@ -16,9 +16,20 @@ Per step, with L layers (every kernel hand-written for gfx950 MFMA):
   dgrad     dZ_l = (dZ_{l+1} . W_l) * (H_l > 0)  gemm_skinny.hip NN (W untransposed)
   wgrad     W_l -= lr * dZ_{l+1}^T H_l, bf16 W_l refreshed, b_l step
             (kernels/wgrad_sgd.hip, straight from the row-major activations)
-With several replicas the wgrad kernel writes the gradient instead, and each
-layer's bucket is all-reduced + applied on a comm stream that overlaps the
-backward of the layers below.  Reference hot loop replaced: client.go:112-202.
+With several replicas, two gradient syncs:
+  rccl / ring / torch   the wgrad kernel writes the gradient instead, and each
+            layer's bucket is all-reduced + applied on a comm stream that
+            overlaps the backward of the layers below (fp32, 4 B per weight:
+            80 MB per step for 784-4096-4096-10);
+  xact      activation exchange: every weight gradient of a 64-row batch is
+            dZ_{l+1}^T H_l, so instead of the 80 MB of gradients the replicas
+            all-gather the bf16 activations and activation gradients (H_l,
+            dZ_l: 64 x 4096 x 2 B = 512 KB each, about 2 MB per replica per
+            step) on the comm stream as each is produced, and every replica
+            runs the fused weight-gradient + SGD launch over the whole global
+            batch (M = 64 N rows, alpha = 1/N).  Identical inputs, identical
+            kernel: the replicas stay bit-identical with no gradient all-reduce.
+Reference hot loop replaced: client.go:112-202.
 """
 from __future__ import annotations
 
@@ -58,6 +69,9 @@ class WideMlpTrainer:
             raise ValueError("softmax kernel supports <= 64 classes")
         if any(x % 8 for x in spec.dims[:-1]):
             raise ValueError("input / hidden widths must be multiples of 8 (16 B bf16 rows)")
+        if sync not in ("rccl", "ring", "torch", "xact"):
+            raise ValueError("sync must be 'rccl', 'ring', 'torch' (gradient all-reduce) or 'xact' "
+                             "(activation all-gather)")
         if gemm not in ("skinny", "rows64"):
             raise ValueError("gemm must be 'skinny' (split-K 64x64 tiles) or 'rows64' (full-K "
                              "64x16 tiles) for the forward products")
@@ -89,6 +103,7 @@ class WideMlpTrainer:
                    for l in range(L)]
         self.H = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L)]
         self.dZ = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L + 1)]
+        self.xact = self.ctx.is_distributed and sync == "xact"
         self.logits = torch.zeros(batch, d[L], dtype=torch.float32, device=dev)
         # per-row loss / correct / count accumulators (the head kernel's row_stats
         # form: no same-address atomics), summed by read_stats
@@ -117,7 +132,8 @@ class WideMlpTrainer:
         import os
 
         self.comm = None
-        if self.ctx.is_distributed and sync in ("rccl", "ring"):
+        if self.ctx.is_distributed and (sync in ("rccl", "ring") or
+                                        (sync == "xact" and self.ctx.backend == "nccl")):
             self.comm = make_native_comm(self.ctx)
         capture_comm = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "1") != "0"
         self.graph_enabled = graph and (not self.ctx.is_distributed or
@@ -146,7 +162,71 @@ class WideMlpTrainer:
         self._ss = torch.cuda.Stream(dev) if self.overlap_wgrad else None
         # an epoch graph must start at an even step (the Wb parity it baked in)
         self.period = self.nbatches if self.nbatches % 2 == 0 else 2 * self.nbatches
+        if self.xact:
+            self._init_xact(batch)
         self._refresh_bf16()
+
+    def _init_xact(self, batch: int) -> None:
+        """Gathered activation buffers: every H_l / dZ_l is a [N * batch, width]
+        bf16 buffer whose rank-r rows are rank r's batch (this replica computes
+        straight into its own slice; an in-place all-gather fills the rest).
+        The inputs are exchanged once: all replicas' bf16 training shards,
+        interleaved batch-major ([batch index][rank][row]), so each step's
+        global input block is one contiguous [N * batch, 784] slice."""
+        n, rk = self.ctx.world_size, self.ctx.rank
+        lo, hi = self.ctx.all_reduce_scalars(float(self.nbatches), op="min")[0], \
+            self.ctx.all_reduce_scalars(float(self.nbatches), op="max")[0]
+        if lo != hi:
+            raise ValueError("sync='xact' needs the same number of batches on every replica")
+        bf = dict(dtype=torch.bfloat16, device=self.device)
+        L = self.L
+        self.Hall = [None] + [torch.zeros(n * batch, self.pd[l], **bf) for l in range(1, L)]
+        self.dZall = [None] + [torch.zeros(n * batch, self.pd[l], **bf) for l in range(1, L + 1)]
+        own = slice(rk * batch, (rk + 1) * batch)
+        self.H = [None] + [self.Hall[l][own] for l in range(1, L)]
+        self.dZ = [None] + [self.dZall[l][own] for l in range(1, L + 1)]
+        rows = self.nbatches * batch
+        full = torch.zeros(n * rows, self.Xb.shape[1], **bf)
+        full[rk * rows:(rk + 1) * rows] = self.Xb[:rows]
+        self._allgather_now(full)
+        # [rank][batch][row] -> [batch][rank][row]
+        self.Xall = (full.view(n, self.nbatches, batch, -1).transpose(0, 1).contiguous()
+                     .view(self.nbatches * n * batch, -1))
+        self.Xb = None  # the local rows are read from Xall
+
+    def _allgather_now(self, full: torch.Tensor) -> None:
+        """In-place all-gather of `full` (rank r's rows in part r) on the
+        current stream: RCCL when the job has it, else torch.distributed with
+        host staging (gloo rehearsals on one GPU)."""
+        n = self.ctx.world_size
+        if self.comm is not None:
+            self.comm.allgather_(full)
+            return
+        import torch.distributed as dist
+
+        host = full.cpu()
+        parts = list(host.chunk(n))
+        mine = parts[self.ctx.rank].clone()
+        dist.all_gather(parts, mine)
+        full.copy_(torch.cat(parts))
+
+    def _gather(self, full: torch.Tensor) -> None:
+        """All-gather one activation buffer on the comm stream once the compute
+        stream has produced this replica's rows (in issue order on every rank)."""
+        main = torch.cuda.current_stream(self.device)
+        cs = main if self.serial_sync else self._cs
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            if self._comm_delay_cycles:
+                torch.cuda._sleep(self._comm_delay_cycles)
+            self._allgather_now(full)
+
+    def _xb_rows(self, b: int) -> torch.Tensor:
+        """This replica's bf16 input rows of batch b."""
+        if self.xact:
+            n, rk, Bt = self.ctx.world_size, self.ctx.rank, self.batch
+            return self.Xall[(b * n + rk) * Bt:(b * n + rk + 1) * Bt]
+        return self.Xb[b * self.batch:(b + 1) * self.batch]
 
     def _refresh_bf16(self) -> None:
         """Both bf16 copies of every W_l from the fp32 masters."""
@@ -178,14 +258,17 @@ class WideMlpTrainer:
     # ----------------------------------------------------------------- step --
     def _step(self) -> None:
         C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
-        r0 = (self.steps_done % self.nbatches) * Bt
+        bi = self.steps_done % self.nbatches
+        r0 = bi * Bt
         p = self.steps_done % 2
         cur = [self.Wb[l][p] for l in range(L)]       # this step's weights
         nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
-        self.H[0] = self.Xb[r0:r0 + Bt]  # this batch's bf16 rows (a view: no copy)
+        self.H[0] = self._xb_rows(bi)  # this batch's bf16 rows (a view: no copy)
         for l in range(L - 1):
             _, b = self.views[l]
             self._gemm(f"f{l}", self.H[l], cur[l], bias=b, relu=True, obf=self.H[l + 1])
+            if self.xact:
+                self._gather(self.Hall[l + 1])
         _, b = self.views[L - 1]
         if self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
             # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
@@ -202,6 +285,27 @@ class WideMlpTrainer:
         fused_sgd = world == 1
         scale = self.lr / world
         main = torch.cuda.current_stream(self.device)
+        if self.xact:
+            self._gather(self.dZall[L])
+            if self.fused_head and L >= 2:
+                self._gather(self.dZall[L - 1])
+            for l in range(L - 2 if self.fused_head else L - 1, 0, -1):
+                self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
+                self._gather(self.dZall[l])
+            main.wait_stream(self._cs)
+            # every replica: the whole global batch's weight gradients (M = N x batch
+            # rows, averaged by alpha = 1/N) with SGD fused, in one launch
+            n, M = world, world * Bt
+            Hall0 = self.Xall[bi * M:(bi + 1) * M]
+            layers = []
+            for l in range(L - 1, -1, -1):
+                W, b = self.views[l]
+                layers.append((self.dZall[l + 1], Hall0 if l == 0 else self.Hall[l], M, d[l + 1], d[l],
+                               1.0 / n, self.lr, W, nxt[l], None, b, None))
+            for i in range(0, len(layers), 4):
+                C.wgrad_sgd_multi(layers[i:i + 4])
+            self.steps_done += 1
+            return
         if fused_sgd and self._ss is None:
             # every dgrad first (they read this step's bf16 weights), then ONE
             # launch updates every layer: W -= lr * dZ_{l+1}^T H_l, the next step's
@@ -282,6 +386,11 @@ class WideMlpTrainer:
         if self.comm is None:
             return
         with torch.cuda.stream(self._cs):
+            if self.xact:
+                for buf in self.Hall[1:] + self.dZall[1:]:
+                    self.comm.allgather_(buf)
+                torch.cuda.synchronize(self.device)
+                return
             for lo, hi in self._gspan:
                 g = self.G[lo:hi]
                 (self.comm.ring_allreduce_(g, 0, 4 << 20) if self.sync == "ring"

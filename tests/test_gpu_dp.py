@@ -39,9 +39,10 @@ def _worker(rank, world, port, outdir, kind):
 
         spec = MlpSpec((784, 256, 128, 10))
         ds = synthetic_mnist(64 * 4, seed=200 + rank)
-        tr = WideMlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7, sync="torch",
-                            serial_sync=kind == "wide_serial")
-        if kind == "wide_delay":
+        tr = WideMlpTrainer(spec, ds, batch=64, lr=0.05, ctx=ctx, seed=7,
+                            sync="xact" if "xact" in kind else "torch",
+                            serial_sync=kind.endswith("_serial"))
+        if kind.endswith("_delay"):
             tr._comm_delay_cycles = 2_000_000  # ~1 ms stall ahead of every bucket on the comm stream
     tr.train_steps(4)
     tr.synchronize()
@@ -49,7 +50,7 @@ def _worker(rank, world, port, outdir, kind):
     ctx.destroy()
 
 
-@pytest.mark.parametrize("kind", ["fused", "wide"])
+@pytest.mark.parametrize("kind", ["fused", "wide", "wide_xact"])
 def test_two_replicas_one_gpu(kind):
     from hipdsml.data.mnist import synthetic_mnist
     from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
@@ -71,17 +72,19 @@ def test_two_replicas_one_gpu(kind):
     assert err < (2e-5 if kind == "fused" else 5e-3), err
 
 
-def test_wide_bucket_overlap_matches_serial_sync():
-    """Per-layer buckets all-reduced + applied on the comm stream while the
-    backward continues (with the comm stream artificially stalled) give the
-    same bits as all-reducing each bucket in line on the compute stream."""
+@pytest.mark.parametrize("sync", ["", "_xact"])
+def test_wide_bucket_overlap_matches_serial_sync(sync):
+    """Per-layer buckets all-reduced + applied (or, with the activation
+    exchange, the activation buffers all-gathered) on the comm stream while the
+    backward continues, with the comm stream artificially stalled, give the
+    same bits as running each collective in line on the compute stream."""
     world = 2
     got = {}
-    for kind in ("wide_delay", "wide_serial"):
+    for kind in (f"wide{sync}_delay", f"wide{sync}_serial"):
         with tempfile.TemporaryDirectory() as d:
             mp.start_processes(_worker, args=(world, _free_port(), d, kind), nprocs=world,
                                start_method="spawn", join=True)
             got[kind] = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"]
                          for r in range(world)]
-    assert torch.equal(got["wide_delay"][0], got["wide_delay"][1])
-    assert torch.equal(got["wide_delay"][0], got["wide_serial"][0])
+    assert torch.equal(got[f"wide{sync}_delay"][0], got[f"wide{sync}_delay"][1])
+    assert torch.equal(got[f"wide{sync}_delay"][0], got[f"wide{sync}_serial"][0])
