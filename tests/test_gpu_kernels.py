@@ -188,8 +188,13 @@ def test_rccl_single_rank_comm():
     t = torch.arange(1024, dtype=torch.float32, device=DEV)
     comm.allreduce_(t, 0)
     comm.ring_allreduce_(t, 0, 4096)
+    hb = torch.arange(512, device=DEV).to(torch.bfloat16)
+    comm.allgather_(hb)  # in-place all-gather (the wide engine's activation exchange)
     torch.cuda.synchronize()
     assert torch.equal(t.cpu(), torch.arange(1024, dtype=torch.float32))
+    assert torch.equal(hb.cpu(), torch.arange(512).to(torch.bfloat16))
+    with pytest.raises(Exception, match="nranks equal parts|contiguous"):
+        comm.allgather_(hb[::2])
     assert comm.async_error() == ""
     comm.abort()
     assert comm.aborted
@@ -209,15 +214,20 @@ def test_rccl_collectives_captured_in_graph(blocking):
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream(DEV)
     s.wait_stream(torch.cuda.current_stream())
+    hb = x[:1024].to(torch.bfloat16)
+    comm.allgather_(hb)  # eager first: RCCL connects outside the capture
+    torch.cuda.synchronize()
     with torch.cuda.graph(g, stream=s):
         comm.allreduce_(buf, 0)
         buf.mul_(2.0)
         comm.allreduce_(buf, 0)
+        comm.allgather_(hb)
     for _ in range(3):
         buf.copy_(x)
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(buf, 2.0 * eager)
+    assert torch.equal(hb, x[:1024].to(torch.bfloat16))
     assert comm.async_error() == ""
 
 
