@@ -236,13 +236,26 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 
   if (lb == 0) PK_EDGE(0);
   // ---- prologue: W1 tile, b1 slice, X of the first step ----
+  // every load of the tile in one batch (one memory round trip), then the LDS stores
   const float* W1g = a.P + a.w_off[0];
-  for (int e = tid; e < 16 * (kKC / 4); e += kThreads) {
+  constexpr int kW1F4 = 16 * (kKC / 4), kW1Per = (kW1F4 + kThreads - 1) / kThreads;
+  float4 w1v[kW1Per];
+#pragma unroll
+  for (int j = 0; j < kW1Per; ++j) {
+    const int e = min(tid + j * kThreads, kW1F4 - 1);
     const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
-    *reinterpret_cast<float4*>(Wl + r * kXS + 4 * c4) =
-        *reinterpret_cast<const float4*>(W1g + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4);
+    w1v[j] = *reinterpret_cast<const float4*>(W1g + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4);
   }
-  if (tid < 16) B1[tid] = gk == 0 ? a.P[a.b_off[0] + n0 + tid] : 0.f;
+  const float b1v = (tid < 16 && gk == 0) ? a.P[a.b_off[0] + n0 + tid] : 0.f;
+#pragma unroll
+  for (int j = 0; j < kW1Per; ++j) {
+    const int e = tid + j * kThreads;
+    if (e < kW1F4) {
+      const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+      *reinterpret_cast<float4*>(Wl + r * kXS + 4 * c4) = w1v[j];
+    }
+  }
+  if (tid < 16) B1[tid] = b1v;
   constexpr int kXF4 = kB * (kKC / 4);                 // float4 of one X tile (3136)
   constexpr int kXPer = (kXF4 + kThreads - 1) / kThreads;  // 13
   pk_glds_x(a, lds, 0, s0, lane, w, k0);
@@ -398,17 +411,36 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 
   if (c == 0) PK_EDGE(3);
   // ---- prologue: W2, W3 (rows padded to 16 with zeros), b2, b3 ----
-  for (int e = tid; e < kD2 * (kD1 / 4); e += kThreads) {
-    const int r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
-    *reinterpret_cast<float4*>(W2 + r * kS1 + 4 * c4) =
-        *reinterpret_cast<const float4*>(a.P + a.w_off[1] + (int64_t)r * kD1 + 4 * c4);
+  // every load in one batch (one memory round trip), then the LDS stores
+  constexpr int kW2Per = kD2 * (kD1 / 4) / kThreads;  // 8 float4 per thread
+  constexpr int kW3Per = 16 * kD2 / kThreads;          // 4 floats per thread
+  static_assert(kW2Per * kThreads == kD2 * (kD1 / 4) && kW3Per * kThreads == 16 * kD2, "prologue split");
+  float4 w2v[kW2Per];
+  float w3v[kW3Per];
+#pragma unroll
+  for (int j = 0; j < kW2Per; ++j) {
+    const int e = tid + j * kThreads, r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
+    w2v[j] = *reinterpret_cast<const float4*>(a.P + a.w_off[1] + (int64_t)r * kD1 + 4 * c4);
   }
-  for (int e = tid; e < 16 * kD2; e += kThreads) {
-    const int r = e / kD2, col = e - r * kD2;
-    W3[r * kS2 + col] = r < kD3 ? a.P[a.w_off[2] + (int64_t)r * kD2 + col] : 0.f;
+#pragma unroll
+  for (int j = 0; j < kW3Per; ++j) {
+    const int e = tid + j * kThreads, r = e / kD2, col = e - r * kD2;
+    w3v[j] = r < kD3 ? a.P[a.w_off[2] + (int64_t)min(r, kD3 - 1) * kD2 + col] : 0.f;
   }
-  if (tid < kD2) B2[tid] = a.P[a.b_off[1] + tid];
-  if (tid < 16) B3[tid] = tid < kD3 ? a.P[a.b_off[2] + tid] : 0.f;
+  const float b2v = tid < kD2 ? a.P[a.b_off[1] + tid] : 0.f;
+  const float b3v = tid < kD3 ? a.P[a.b_off[2] + tid] : 0.f;
+#pragma unroll
+  for (int j = 0; j < kW2Per; ++j) {
+    const int e = tid + j * kThreads, r = e / (kD1 / 4), c4 = e - r * (kD1 / 4);
+    *reinterpret_cast<float4*>(W2 + r * kS1 + 4 * c4) = w2v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < kW3Per; ++j) {
+    const int e = tid + j * kThreads, r = e / kD2, col = e - r * kD2;
+    W3[r * kS2 + col] = w3v[j];
+  }
+  if (tid < kD2) B2[tid] = b2v;
+  if (tid < 16) B3[tid] = b3v;
   for (int e = tid; e < kB * kS3; e += kThreads) DZ3[e] = 0.f;
   float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
   __syncthreads();
