@@ -168,7 +168,7 @@ def run(a) -> int:
         sync_us = tr.sync_times  # auto already timed every candidate
     elif n > 1 and tr.backend == "hip" and not a.no_sync_sweep:
         # every sync candidate's µs/step, measured the way training runs it
-        cands = ["xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu else ["xact", "xgmi", "torch"]
+        cands = ["pk", "xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu else ["pk", "xact", "xgmi", "torch"]
         sync_us = tr.time_sync_modes(cands, steps=max(100, a.graph_steps * 2))
     tr.train_steps(a.warmup)
     tr.synchronize()

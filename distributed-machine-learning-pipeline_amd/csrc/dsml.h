@@ -96,7 +96,13 @@ int64_t mlp_persist_xbuf_granules();
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
-                             hipStream_t s);
+                             hipStream_t s, const struct XchgArgs* xa = nullptr,
+                             const struct XchgTab* tab = nullptr);
+// Data-parallel form (xa->nranks > 1): the receive buffers / flags each replica
+// needs (PeerExchange half >= px_half(n), ntiles >= px_ntiles(n)); lr is passed
+// as lr / n.
+int64_t px_half(int n);
+int px_ntiles(int n);
 
 // ---- peer exchange: gradient all-reduce fused into K_C over xGMI -------------
 // Every replica's K_C publishes each weight-gradient tile into its own

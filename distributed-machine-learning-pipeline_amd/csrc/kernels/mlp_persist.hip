@@ -152,6 +152,24 @@ __device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- replica exchange (nrep > 1): system-coherent 16-B accesses as two 8-B
+// relaxed atomics (the idiom of kernels/xchg.hip), one flag per slot ----
+typedef __attribute__((address_space(1))) uint64_t px_g64;
+__device__ __forceinline__ void px_st4(float* p, float4 v) {
+  px_g64* q = (px_g64*)p;
+  __hip_atomic_store(q, (uint64_t)__float_as_uint(v.x) | ((uint64_t)__float_as_uint(v.y) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, (uint64_t)__float_as_uint(v.z) | ((uint64_t)__float_as_uint(v.w) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float4 px_ld4(const float* p) {
+  const px_g64* q = (const px_g64*)p;
+  const uint64_t x = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_float4(__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)),
+                     __uint_as_float((uint32_t)y), __uint_as_float((uint32_t)(y >> 32)));
+}
+
 }  // namespace
 
 // Phase stamps (s_memrealtime, 100 MHz) of layer-1 block 0 and chain block 0
@@ -190,7 +208,70 @@ struct PersistArgs {
   uint32_t* herr;  // host-mapped mirror of err (nullable): read without a copy
   uint64_t timeout_ticks;
   int32_t place;  // block -> role map: 1 = chains at b % 8 == 0 (one XCD, default), 0 = chains last
+  // Data parallelism over nrep replicas (nrep > 1): every step, each weight
+  // gradient slot is pushed into every peer's receive buffer (xt.buf[d], this
+  // replica's slot; parity by step), flagged (xt.flags[d]), and summed over
+  // the replicas in rank order from the local buffer -- identical bytes and
+  // order on every replica, so the weights stay bit-identical.  lr is already
+  // lr / nrep.
+  XchgTab xt;
+  int32_t nrep, rep;
+  int64_t xhalf;   // floats per parity half of a receive buffer (>= px_half)
+  uint32_t* xerr;  // the exchange's error word (a peer that did not arrive)
 };
+
+// Receive-buffer layout per parity half: [src][layer-1 block][wave] slots of
+// 64 lanes x 16 floats (the wave's dW1 fragments, db1 included), then
+// [src][chain wave] slots of 64 lanes x 40 floats (dW2 h-tile fragments, dW3,
+// db2, db3).  Flags: [src][block][wave], then [src][wave].
+constexpr int kPxL1 = 64 * 16, kPxCh = 64 * 40;
+int64_t px_half(int n) { return (int64_t)n * (kNL1 * 4 * kPxL1 + 4 * kPxCh); }
+int px_ntiles(int n) { return n * (kNL1 * 4 + 4); }
+
+// One wave's slot: push v (this replica's) to every peer d with d % mod == sel,
+// raise their flags, wait for every peer's slot here, then v = the rank-ordered
+// sum over all replicas.  false: a peer did not arrive in time.
+template <int NV>
+__device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
+                                                  int64_t base, int64_t per_src, int flag_base,
+                                                  int flag_per_src, int mod, int sel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const uint64_t tag = s + 1;
+  for (int d = 0; d < a.nrep; ++d) {
+    if (d == a.rep || d % mod != sel) continue;
+    float* dst = a.xt.buf[d] + poff + base + (int64_t)a.rep * per_src + lane * (4 * NV);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) px_st4(dst + 4 * j, v[j]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot landed before its flag
+  if (lane == 0)
+    for (int d = 0; d < a.nrep; ++d)
+      if (d != a.rep && d % mod == sel)
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + flag_base + a.rep * flag_per_src), tag,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = true;
+  if (lane < a.nrep && lane != a.rep)
+    ok = poll_flag_ge<1>(a.xt.flags[a.rep] + flag_base + lane * flag_per_src, tag, a.xerr,
+                      a.timeout_ticks);
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  asm volatile("" ::: "memory");
+  if (!ok) return false;
+  const float* mine = a.xt.buf[a.rep] + poff + base + lane * (4 * NV);
+  float4 acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int src = 0; src < a.nrep; ++src) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float4 x = src == a.rep ? v[j] : px_ld4(mine + src * per_src + 4 * j);
+      acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = acc[j];
+  return true;
+}
 
 // A block that gave up leaves a mark in host memory on its way out, so the
 // host learns the launch failed without a device->host copy.
@@ -358,6 +439,17 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
         for (int ms = 0; ms < kB / 4; ++ms)
           g[t] = mfma_f32_16x16x4(dv[ms], kc < kKC ? xv[ms] : pad, g[t]);
       }
+    }
+    if (a.nrep > 1) {  // data parallel: sum this wave's fragments over the replicas
+      float4 v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+      bool xok = px_allreduce_wave<4>(a, s, v, (int64_t)(lb * 4 + w) * kPxL1,
+                                      (int64_t)kNL1 * 4 * kPxL1, lb * 4 + w, kNL1 * 4, 1, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+      ok = __syncthreads_and(xok ? 1 : 0) != 0;
+      if (!ok) break;
     }
     // every wave read this step's W1 tile in the forward, before the barrier above
 #pragma unroll
@@ -711,6 +803,24 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       sb2 += __shfl_xor(sb2, 32, 64);
       sb3 += __shfl_xor(sb3, 16, 64);
       sb3 += __shfl_xor(sb3, 32, 64);
+      if (a.nrep > 1) {  // data parallel: sum this wave's h tile over the replicas
+        // (chain c pushes to the peers d with d % 4 == c; every chain reads all)
+        float4 v[10];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+        v[8] = make_float4(g3[0], g3[1], g3[2], g3[3]);
+        v[9] = make_float4(sb2, sb3, 0.f, 0.f);
+        const int64_t chb = (int64_t)a.nrep * kNL1 * 4 * kPxL1;
+        bool xok = px_allreduce_wave<10>(a, s, v, chb + (int64_t)w * kPxCh, 4 * kPxCh,
+                                         a.nrep * kNL1 * 4 + w, 4, kNCH, c);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+        g3 = f32x4{v[8].x, v[8].y, v[8].z, v[8].w};
+        sb2 = v[9].x;
+        sb3 = v[9].y;
+        ok = __syncthreads_and(xok ? 1 : 0) != 0;
+        if (!ok) break;
+      }
       PK_STAMP(1, 6);
       // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above):
       // all old values read first, then all the updated ones written
@@ -804,7 +914,7 @@ int64_t mlp_persist_xbuf_granules() { return kTotalG; }
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
-                             hipStream_t s) {
+                             hipStream_t s, const XchgArgs* xa, const XchgTab* tab) {
   if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
       (ldx % 4) != 0)
     return hipErrorInvalidValue;
@@ -827,6 +937,17 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   a.err = err;
   a.herr = herr;
   a.timeout_ticks = timeout_ticks;
+  a.nrep = 1;
+  if (xa != nullptr && xa->nranks > 1) {
+    if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks) ||
+        xa->err == nullptr)
+      return hipErrorInvalidValue;
+    a.xt = *tab;
+    a.nrep = xa->nranks;
+    a.rep = xa->rank;
+    a.xhalf = xa->half;
+    a.xerr = xa->err;
+  }
   static const int place = [] {
     const char* e = getenv("HIPDSML_PK_PLACE");  // 0: the old map (A/B only)
     return e ? atoi(e) : 1;

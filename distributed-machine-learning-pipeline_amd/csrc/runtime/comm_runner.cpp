@@ -264,7 +264,7 @@ bool MlpRunner::captured(int steps) const {
 }
 
 void MlpRunner::set_comm(RcclComm* c, int algo, int64_t chunk_bytes) {
-  if (c != nullptr && c->nranks() > 1) pk_xb_ = nullptr;  // the persistent step is single-replica
+  if (c != nullptr && c->nranks() > 1) pk_xb_ = nullptr, pk_x_ = nullptr;  // leaves the persistent step
   comm_ = c;
   algo_ = algo;
   chunk_bytes_ = chunk_bytes;
@@ -279,7 +279,7 @@ void MlpRunner::set_exchange(PeerExchange* x) {
     if (x->ntiles() != mlp_wgrad_tiles(d_) || x->half() < b_.nparams)
       throw std::invalid_argument("set_exchange: exchange buffers sized for another model");
   }
-  if (x != nullptr) pk_xb_ = nullptr;  // the persistent step is single-replica
+  if (x != nullptr) pk_xb_ = nullptr, pk_x_ = nullptr;  // leaves the persistent step
   xchg_ = x;
   xact_ = false;
   reset_graph();
@@ -302,7 +302,8 @@ void MlpRunner::set_act_exchange(PeerExchange* x, const float* Xall, int64_t xst
     throw std::invalid_argument("set_act_exchange: exchange buffers sized for another model");
   if (Xall == nullptr || xstride < (int64_t)d_.nbatches * 64 * d_.dims[0])
     throw std::invalid_argument("set_act_exchange: replicated input shards too small");
-  pk_xb_ = nullptr;  // the persistent step is single-replica
+  pk_xb_ = nullptr;  // leaves the persistent step
+  pk_x_ = nullptr;
   xchg_ = x;
   xact_ = true;
   if (waves != 0 && waves != 4 && waves != 8)
@@ -340,18 +341,28 @@ void MlpRunner::enqueue_update(hipStream_t s) {
     DSML_HIP_CHECK(sgd_update_f32(b_.P, b_.G, b_.nparams, lr_ * gscale, s));
 }
 
-void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms) {
+void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x) {
   if (xbuf == nullptr) {
     pk_xb_ = nullptr;
     pk_err_ = nullptr;
+    pk_x_ = nullptr;
     reset_graph();
     return;
   }
   if (!mlp_persist_supported(d_))
     throw std::invalid_argument("set_persist: the persistent step covers 784-128-64-10 at batch 64");
   if (mom_ != 0.f || wd_ != 0.f) throw std::invalid_argument("set_persist: plain SGD only");
-  if (comm_ != nullptr || xchg_ != nullptr || world_ != 1)
-    throw std::invalid_argument("set_persist: single replica only");
+  if (x != nullptr) {
+    const int n = x->nranks();
+    if (!x->connected() || n < 2 || n != world_)
+      throw std::invalid_argument("set_persist: the replica exchange must connect world_size >= 2 ranks");
+    if (x->ntiles() < px_ntiles(n) || x->half() < px_half(n))
+      throw std::invalid_argument("set_persist: exchange buffers too small for the persistent step");
+    xchg_ = nullptr;  // the three-launch exchanges are off while the persistent step runs
+  } else if (comm_ != nullptr || xchg_ != nullptr || world_ != 1) {
+    throw std::invalid_argument("set_persist: single replica only (or pass the replica exchange)");
+  }
+  pk_x_ = x;
   if (err == nullptr) throw std::invalid_argument("set_persist: needs an error word");
   if (pk_herr_ == nullptr) {
     void* h = nullptr;
@@ -368,8 +379,13 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms) {
 void MlpRunner::enqueue_steps(int n, hipStream_t s) {
   if (n <= 0) return;
   if (pk_xb_ != nullptr) {
-    DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
-                                     b_.stats, pk_err_, pk_herr_, pk_timeout_, s));
+    if (pk_x_ != nullptr)
+      DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_,
+                                       lr_ / (float)pk_x_->nranks(), n, pk_xb_, b_.stats, pk_err_,
+                                       pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table()));
+    else
+      DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
+                                       b_.stats, pk_err_, pk_herr_, pk_timeout_, s));
     return;
   }
   for (int i = 0; i < n; ++i) enqueue_step(s);

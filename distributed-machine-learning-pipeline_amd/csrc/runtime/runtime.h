@@ -280,7 +280,9 @@ class MlpRunner {
   void set_act_exchange(PeerExchange* x, const float* Xall, int64_t xstride, int waves = 0);
   // Persistent fused step (kernels/mlp_persist.hip): every enqueue of n steps
   // is ONE launch.  Single replica, plain SGD, the flagship shape only.
-  void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms);
+  // With `x` (>= 2 ranks): the data-parallel persistent step, every weight
+  // gradient summed over the replicas inside the launch through x's buffers.
+  void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x = nullptr);
   bool persist_active() const { return pk_xb_ != nullptr; }
   // Whether a persistent launch gave up on a hand-off (read from host-mapped
   // memory the kernel marks on the way out: valid after a stream sync, no copy).
@@ -325,6 +327,7 @@ class MlpRunner {
   int64_t xstride_ = 0;
   int xact_waves_ = 0;
   uint64_t* pk_xb_ = nullptr;
+  PeerExchange* pk_x_ = nullptr;  // replica exchange of the persistent step (nranks > 1)
   uint32_t* pk_err_ = nullptr;
   uint32_t* pk_herr_ = nullptr;  // hipHostMalloc'd, device-visible
   uint64_t pk_timeout_ = 0;

@@ -26,8 +26,9 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("auto", "xact", "xgmi", "rccl", "ring", "torch")
-EXCHANGE_MODES = ("xact", "xgmi")  # fused into K_C over xGMI peer memory
+SYNC_MODES = ("auto", "pk", "xact", "xgmi", "rccl", "ring", "torch")
+# fused over xGMI peer memory: into K_C (xact, xgmi) or into the persistent step (pk)
+EXCHANGE_MODES = ("pk", "xact", "xgmi")
 
 
 @dataclass
@@ -224,6 +225,12 @@ class MlpTrainer:
         """Point the native runner at one gradient-sync mode.  None keeps the
         RCCL communicator as configured; 'rccl' / 'ring' select ncclAllReduce
         or the in-house multi-ring send/recv all-reduce on it."""
+        if mode == "pk":
+            self.xchg = self._exchanges["pk"]
+            self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0, self.xchg)
+            return
+        if self.pk_buf is not None:
+            self.runner.set_persist(None)  # leave the persistent step
         if mode in (None, "rccl", "ring", "torch"):
             self.runner.set_exchange(None)
             self.xchg = None
@@ -243,7 +250,17 @@ class MlpTrainer:
         from ..parallel import xchg as X
 
         try:
-            if mode == "xact":
+            if mode == "pk":
+                C = self.runner_module()
+                if not (self._want_persist and C.mlp_persist_supported(self.layout.desc_list())):
+                    raise X.ExchangeUnavailable("the persistent step covers 784-128-64-10 at batch 64")
+                half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size)
+                x = X.make_exchange(self.ctx, half, ntiles, self.xchg_timeout_ms)
+                if self.pk_buf is None:
+                    self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64,
+                                              device=self.device)
+                    self.pk_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            elif mode == "xact":
                 if not X.act_supported(self.layout):
                     raise X.ExchangeUnavailable("activation exchange needs batch <= 64 and "
                                                 "layer input dims that are multiples of 16")
@@ -258,6 +275,7 @@ class MlpTrainer:
         self._activate(mode)
         diff = X.verify_against_allreduce(self)  # collective, same result on all ranks
         self._activate(None)
+        self._rewound()  # the step counter went back: stale persistent hand-off tags
         return "" if diff <= 1e-5 else f"self-test mismatch {diff}"
 
     def _init_exchanges(self) -> None:
@@ -274,7 +292,7 @@ class MlpTrainer:
         self._exchanges: Dict[str, object] = {}
         self.Xall = None
         strict = self.sync in EXCHANGE_MODES
-        modes = [self.sync] if strict else ["xact", "xgmi"]
+        modes = [self.sync] if strict else ["pk", "xact", "xgmi"]
         ok = []
         for m in modes:
             err = self._setup_exchange(m)
@@ -296,6 +314,12 @@ class MlpTrainer:
         self._set_mode(choice or self.sync_active)
         if self.sync_active != "xact":
             self.Xall = None  # the replicated inputs are only read by xact
+
+    @staticmethod
+    def runner_module():
+        from ..ops.native import require_native
+
+        return require_native()
 
     def _set_mode(self, mode: str) -> None:
         self._activate(mode)

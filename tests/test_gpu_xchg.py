@@ -179,11 +179,16 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
                     ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0,
                     xact_waves=xact_waves, auto_fallback="torch")
     if sync == "auto":  # every candidate self-tested and timed; any may win on a shared GPU
-        assert tr.sync_active in ("xact", "xgmi", "torch"), tr.sync_active
-        assert set(tr.sync_times) == {"xact", "xgmi", "torch"}, tr.sync_times
+        assert tr.sync_active in ("pk", "xact", "xgmi", "torch"), tr.sync_active
+        assert set(tr.sync_times) == {"pk", "xact", "xgmi", "torch"}, tr.sync_times
     else:
         assert tr.sync_active == sync
-    tr.train_steps(6)
+    if sync == "pk":  # launches split anywhere: the step counter and tags carry over
+        assert tr.persistent
+        tr.train_steps(2)
+        tr.train_steps(4)
+    else:
+        tr.train_steps(6)
     tr.synchronize()
     torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
     ctx.destroy()
@@ -191,7 +196,7 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
 
 @pytest.mark.parametrize("world,graph_steps,sync", [(2, 0, "xgmi"), (2, 3, "xgmi"), (2, 0, "xact"),
                                                     (2, 3, "xact"), (3, 3, "xact"), (3, 3, "xgmi"),
-                                                    (2, 3, "auto")])
+                                                    (2, 0, "pk"), (3, 0, "pk"), (2, 3, "auto")])
 def test_two_processes_ipc(world, graph_steps, sync):
     """N processes sharing the GPU through IPC handles.  Sharing one GPU, every
     process's spinning weight-gradient launch must be resident at once: the
@@ -199,7 +204,9 @@ def test_two_processes_ipc(world, graph_steps, sync):
     the 8-wave form is covered in-process above), and groups stay at <= 3
     processes — with 4 or more, the hardware scheduler can leave a process's
     queue unmapped while its peers spin (seen as a timed-out self-test).  On a
-    node each GPU runs one process and one launch."""
+    node each GPU runs one process and one launch.  sync='pk' runs the
+    persistent step in every process (36 workgroups each, all resident) with
+    the weight gradients summed over the replicas inside the launch."""
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync,
                                               4 if sync in ("xact", "auto") else 0), nprocs=world,
