@@ -247,8 +247,10 @@ def main(argv=None) -> int:
     ap.add_argument("--model", default="784-128-64-10")
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--sync", default="auto", choices=["auto", "xact", "xgmi", "rccl", "ring", "torch"],
-                    help="gradient sync (N>1): xact = activation exchange over xGMI (every GPU "
+    ap.add_argument("--sync", default="auto", choices=["auto", "pk", "xact", "xgmi", "rccl", "ring", "torch"],
+                    help="gradient sync (N>1): pk = the one-launch persistent step with the weight "
+                         "gradients summed over the replicas inside the launch (xGMI pushes), "
+                         "xact = activation exchange over xGMI (every GPU "
                          "pushes its activations and computes the global-batch weight gradients), "
                          "xgmi = one-shot gradient exchange fused into the weight-gradient kernel, "
                          "rccl = ncclAllReduce, ring = multi-ring all-reduce on ncclSend/ncclRecv; "

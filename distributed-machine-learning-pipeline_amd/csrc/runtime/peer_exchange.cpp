@@ -139,6 +139,9 @@ void PeerExchange::reset(hipStream_t s) {
   DSML_HIP_CHECK(hipSetDevice(device_));
   DSML_HIP_CHECK(hipMemsetAsync(flags(), 0, (size_t)ntiles_ * sizeof(uint64_t), s));
   DSML_HIP_CHECK(hipMemsetAsync(err_, 0, sizeof(uint32_t), s));
+  // the payload too: protocols that tag the data itself ({value, step} granules,
+  // the persistent step) must not match a stale slot after a rewind
+  DSML_HIP_CHECK(hipMemsetAsync(buf(), 0, (size_t)2 * (size_t)half_ * sizeof(float), s));
 }
 
 uint32_t PeerExchange::error(hipStream_t s) {
