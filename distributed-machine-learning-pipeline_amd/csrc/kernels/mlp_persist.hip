@@ -218,7 +218,6 @@ struct PersistArgs {
   int32_t nrep, rep;
   int64_t xhalf;   // floats per parity half of a receive buffer (>= px_half)
   uint32_t* xerr;  // the exchange's error word (a peer that did not arrive)
-  int32_t pxgran;  // 1: slots of {value, step tag} granules polled directly (no flag round)
 };
 
 // Receive-buffer layout per parity half: [src][layer-1 block][wave] slots of
@@ -226,8 +225,7 @@ struct PersistArgs {
 // [src][chain wave] slots of 64 lanes x 40 floats (dW2 h-tile fragments, dW3,
 // db2, db3).  Flags: [src][block][wave], then [src][wave].
 constexpr int kPxL1 = 64 * 16, kPxCh = 64 * 40;
-// (sized for the granule form: every slot float travels as an 8-B granule)
-int64_t px_half(int n) { return 2 * (int64_t)n * (kNL1 * 4 * kPxL1 + 4 * kPxCh); }
+int64_t px_half(int n) { return (int64_t)n * (kNL1 * 4 * kPxL1 + 4 * kPxCh); }
 int px_ntiles(int n) { return n * (kNL1 * 4 + 4); }
 
 // One wave's slot: push v (this replica's) to every peer d with d % mod == sel,
@@ -275,73 +273,6 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   return true;
 }
 
-// Granule form of the same slot exchange: every float is pushed as one 8-B
-// {value, tag = step + 1} granule (never torn), and the receiver polls the
-// slot itself until every tag matches -- no store drain, no flag round trip.
-// base / per_src count granules.
-template <int NV>
-__device__ __forceinline__ bool px_allreduce_wave_g(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
-                                                    int64_t base, int64_t per_src, int mod, int sel) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t tag = (uint32_t)(s + 1);
-  const uint64_t hi = (uint64_t)tag << 32;
-  const int64_t poff = (int64_t)(s & 1) * (a.xhalf / 2);
-  for (int d = 0; d < a.nrep; ++d) {
-    if (d == a.rep || d % mod != sel) continue;
-    px_g64* dst = (px_g64*)a.xt.buf[d] + poff + base + (int64_t)a.rep * per_src + lane * (4 * NV);
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      __hip_atomic_store(dst + 4 * j + 0, hi | __float_as_uint(v[j].x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(dst + 4 * j + 1, hi | __float_as_uint(v[j].y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(dst + 4 * j + 2, hi | __float_as_uint(v[j].z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(dst + 4 * j + 3, hi | __float_as_uint(v[j].w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  float4 acc[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const px_g64* mine = (const px_g64*)a.xt.buf[a.rep] + poff + base + lane * (4 * NV);
-  for (int src = 0; src < a.nrep; ++src) {
-    float4 x[NV];
-    if (src == a.rep) {
-#pragma unroll
-      for (int j = 0; j < NV; ++j) x[j] = v[j];
-    } else {
-      const px_g64* p = mine + src * per_src;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (uint32_t it = 0;; ++it) {
-        bool got = true;
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const uint64_t g0 = __hip_atomic_load(p + 4 * j + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          const uint64_t g1 = __hip_atomic_load(p + 4 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          const uint64_t g2 = __hip_atomic_load(p + 4 * j + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          const uint64_t g3 = __hip_atomic_load(p + 4 * j + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          got = got && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag &&
-                (uint32_t)(g2 >> 32) == tag && (uint32_t)(g3 >> 32) == tag;
-          x[j] = make_float4(__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1),
-                             __uint_as_float((uint32_t)g2), __uint_as_float((uint32_t)g3));
-        }
-        if (__builtin_amdgcn_ballot_w64(!got) == 0) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-          if (lane == 0) __hip_atomic_fetch_or(a.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          return false;
-        }
-        if ((it & 63u) == 63u &&
-            __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
-          return false;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      acc[j].x += x[j].x; acc[j].y += x[j].y; acc[j].z += x[j].z; acc[j].w += x[j].w;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NV; ++j) v[j] = acc[j];
-  return true;
-}
 
 // A block that gave up leaves a mark in host memory on its way out, so the
 // host learns the launch failed without a device->host copy.
@@ -514,11 +445,8 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
       float4 v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
-      bool xok = a.pxgran
-                     ? px_allreduce_wave_g<4>(a, s, v, (int64_t)(lb * 4 + w) * kPxL1,
-                                              (int64_t)kNL1 * 4 * kPxL1, 1, 0)
-                     : px_allreduce_wave<4>(a, s, v, (int64_t)(lb * 4 + w) * kPxL1,
-                                            (int64_t)kNL1 * 4 * kPxL1, lb * 4 + w, kNL1 * 4, 1, 0);
+      bool xok = px_allreduce_wave<4>(a, s, v, (int64_t)(lb * 4 + w) * kPxL1,
+                                      (int64_t)kNL1 * 4 * kPxL1, lb * 4 + w, kNL1 * 4, 1, 0);
 #pragma unroll
       for (int t = 0; t < 4; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
       ok = __syncthreads_and(xok ? 1 : 0) != 0;
@@ -884,10 +812,8 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         v[8] = make_float4(g3[0], g3[1], g3[2], g3[3]);
         v[9] = make_float4(sb2, sb3, 0.f, 0.f);
         const int64_t chb = (int64_t)a.nrep * kNL1 * 4 * kPxL1;
-        bool xok = a.pxgran
-                       ? px_allreduce_wave_g<10>(a, s, v, chb + (int64_t)w * kPxCh, 4 * kPxCh, kNCH, c)
-                       : px_allreduce_wave<10>(a, s, v, chb + (int64_t)w * kPxCh, 4 * kPxCh,
-                                               a.nrep * kNL1 * 4 + w, 4, kNCH, c);
+        bool xok = px_allreduce_wave<10>(a, s, v, chb + (int64_t)w * kPxCh, 4 * kPxCh,
+                                         a.nrep * kNL1 * 4 + w, 4, kNCH, c);
 #pragma unroll
         for (int t = 0; t < 8; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
         g3 = f32x4{v[8].x, v[8].y, v[8].z, v[8].w};
@@ -1022,11 +948,6 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     a.rep = xa->rank;
     a.xhalf = xa->half;
     a.xerr = xa->err;
-    static const int gran = [] {
-      const char* e = getenv("HIPDSML_PK_GRAN");
-      return e ? atoi(e) : 0;
-    }();
-    a.pxgran = gran;
   }
   static const int place = [] {
     const char* e = getenv("HIPDSML_PK_PLACE");  // 0: the old map (A/B only)
