@@ -152,22 +152,22 @@ __device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---- replica exchange (nrep > 1): system-coherent 16-B accesses as two 8-B
-// relaxed atomics (the idiom of kernels/xchg.hip), one flag per slot ----
+// ---- replica exchange (nrep > 1): 16-B vector accesses at system scope
+// (sc0 sc1) through a buffer descriptor on the wave-uniform slot base, so a
+// wave's slot moves as coalesced 1 KiB instructions.  (Two 8-B system atomics
+// per float4, the xchg.hip idiom, are one fabric transaction per lane each:
+// measured 13 us for a chain wave's 40-float slot.) ----
 typedef __attribute__((address_space(1))) uint64_t px_g64;
-__device__ __forceinline__ void px_st4(float* p, float4 v) {
-  px_g64* q = (px_g64*)p;
-  __hip_atomic_store(q, (uint64_t)__float_as_uint(v.x) | ((uint64_t)__float_as_uint(v.y) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(q + 1, (uint64_t)__float_as_uint(v.z) | ((uint64_t)__float_as_uint(v.w) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+constexpr int kScSys = 17;  // buffer aux: sc0 | sc1 (system scope)
+__device__ __forceinline__ void px_st4(const __amdgpu_buffer_rsrc_t& r, int off_bytes, float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4v, x), r, off_bytes, 0, kScSys);
 }
-__device__ __forceinline__ float4 px_ld4(const float* p) {
-  const px_g64* q = (const px_g64*)p;
-  const uint64_t x = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint64_t y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return make_float4(__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)),
-                     __uint_as_float((uint32_t)y), __uint_as_float((uint32_t)(y >> 32)));
+__device__ __forceinline__ float4 px_ld4(const __amdgpu_buffer_rsrc_t& r, int off_bytes) {
+  const nu4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, kScSys);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
 }
 
 }  // namespace
@@ -240,9 +240,9 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   const uint64_t tag = s + 1;
   for (int d = 0; d < a.nrep; ++d) {
     if (d == a.rep || d % mod != sel) continue;
-    float* dst = a.xt.buf[d] + poff + base + (int64_t)a.rep * per_src + lane * (4 * NV);
+    const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[d] + poff + base + (int64_t)a.rep * per_src);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) px_st4(dst + 4 * j, v[j]);
+    for (int j = 0; j < NV; ++j) px_st4(r, (lane * (4 * NV) + 4 * j) * 4, v[j]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot landed before its flag
   if (lane == 0)
@@ -257,14 +257,15 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
   if (!ok) return false;
-  const float* mine = a.xt.buf[a.rep] + poff + base + lane * (4 * NV);
+  const float* mine = a.xt.buf[a.rep] + poff + base;
   float4 acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int src = 0; src < a.nrep; ++src) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      const float4 x = src == a.rep ? v[j] : px_ld4(mine + src * per_src + 4 * j);
+      const float4 x = src == a.rep ? v[j] : px_ld4(r, (lane * (4 * NV) + 4 * j) * 4);
       acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
     }
   }
