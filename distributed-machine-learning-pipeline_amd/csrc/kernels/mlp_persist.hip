@@ -305,6 +305,7 @@ __device__ __forceinline__ void pk_glds_x(const PersistArgs& a, float* lds, int 
   }
 }
 
+template <bool DP>
 __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int lb) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
@@ -442,7 +443,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
           g[t] = mfma_f32_16x16x4(dv[ms], kc < kKC ? xv[ms] : pad, g[t]);
       }
     }
-    if (a.nrep > 1) {  // data parallel: sum this wave's fragments over the replicas
+    if (DP) {  // data parallel: sum this wave's fragments over the replicas
       float4 v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
@@ -486,6 +487,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 // -----------------------------------------------------------------------------
 // Chain block
 // -----------------------------------------------------------------------------
+template <bool DP>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
@@ -805,7 +807,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       sb2 += __shfl_xor(sb2, 32, 64);
       sb3 += __shfl_xor(sb3, 16, 64);
       sb3 += __shfl_xor(sb3, 32, 64);
-      if (a.nrep > 1) {  // data parallel: sum this wave's h tile over the replicas
+      if (DP) {  // data parallel: sum this wave's h tile over the replicas
         // (chain c pushes to the peers d with d % 4 == c; every chain reads all)
         float4 v[10];
 #pragma unroll
@@ -875,6 +877,9 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (c == 0) PK_EDGE(5);
 }
 
+// DP: the data-parallel form (replica exchange compiled in); the single-replica
+// launch runs the exchange-free code.
+template <bool DP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void mlp_persist_k(PersistArgs a) {
   extern __shared__ float4 lds4[];
@@ -885,15 +890,15 @@ void mlp_persist_k(PersistArgs a) {
     // one XCD under round-robin placement (speed only, the hand-offs are
     // placement-independent)
     if (b < 8 * kNCH && (b & 7) == 0)
-      pk_chain(a, lds, b >> 3);
+      pk_chain<DP>(a, lds, b >> 3);
     else
-      pk_layer1(a, lds, b < 8 * kNCH ? b - (b >> 3) - 1 : b - kNCH);
+      pk_layer1<DP>(a, lds, b < 8 * kNCH ? b - (b >> 3) - 1 : b - kNCH);
     return;
   }
   if (b < kNL1)
-    pk_layer1(a, lds, b);
+    pk_layer1<DP>(a, lds, b);
   else
-    pk_chain(a, lds, b - kNL1);
+    pk_chain<DP>(a, lds, b - kNL1);
 }
 
 hipError_t mlp_persist_read_stamps(uint64_t* host_out) {
@@ -958,12 +963,17 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   const size_t lds = (size_t)kLdsFloats * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_persist_k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(mlp_persist_k<false>),
+                          reinterpret_cast<const void*>(mlp_persist_k<true>)}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
-  hipLaunchKernelGGL(mlp_persist_k, dim3(kNL1 + kNCH), dim3(kThreads), lds, s, a);
+  if (a.nrep > 1)
+    hipLaunchKernelGGL(mlp_persist_k<true>, dim3(kNL1 + kNCH), dim3(kThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL(mlp_persist_k<false>, dim3(kNL1 + kNCH), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
