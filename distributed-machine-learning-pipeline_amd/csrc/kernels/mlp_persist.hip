@@ -228,13 +228,12 @@ constexpr int kPxL1 = 64 * 16, kPxCh = 64 * 40;
 int64_t px_half(int n) { return (int64_t)n * (kNL1 * 4 * kPxL1 + 4 * kPxCh); }
 int px_ntiles(int n) { return n * (kNL1 * 4 + 4); }
 
-// One wave's slot: push v (this replica's) to every peer d with d % mod == sel,
-// raise their flags, wait for every peer's slot here, then v = the rank-ordered
-// sum over all replicas.  false: a peer did not arrive in time.
+// One wave's slot, push half: v (this replica's) into every peer d with
+// d % mod == sel, then raise their flags.
 template <int NV>
-__device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
-                                                  int64_t base, int64_t per_src, int flag_base,
-                                                  int flag_per_src, int mod, int sel) {
+__device__ __forceinline__ void px_push_wave(const PersistArgs& a, uint64_t s, const float4 (&v)[NV],
+                                             int64_t base, int64_t per_src, int flag_base,
+                                             int flag_per_src, int mod, int sel) {
   const int lane = threadIdx.x & 63;
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const uint64_t tag = s + 1;
@@ -250,10 +249,22 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
       if (d != a.rep && d % mod == sel)
         __hip_atomic_store((px_g64*)(a.xt.flags[d] + flag_base + a.rep * flag_per_src), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Pull half: wait for every peer's slot of step s here, then v (this
+// replica's own values on entry) = the rank-ordered sum over all replicas.
+// false: a peer did not arrive in time.
+template <int NV>
+__device__ __forceinline__ bool px_pull_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
+                                             int64_t base, int64_t per_src, int flag_base,
+                                             int flag_per_src) {
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const uint64_t tag = s + 1;
   bool ok = true;
   if (lane < a.nrep && lane != a.rep)
     ok = poll_flag_ge<1>(a.xt.flags[a.rep] + flag_base + lane * flag_per_src, tag, a.xerr,
-                      a.timeout_ticks);
+                         a.timeout_ticks);
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
   if (!ok) return false;
@@ -272,6 +283,15 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = acc[j];
   return true;
+}
+
+// Both halves back to back (the layer-1 blocks: their update is needed at once).
+template <int NV>
+__device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
+                                                  int64_t base, int64_t per_src, int flag_base,
+                                                  int flag_per_src, int mod, int sel) {
+  px_push_wave<NV>(a, s, v, base, per_src, flag_base, flag_per_src, mod, sel);
+  return px_pull_wave<NV>(a, s, v, base, per_src, flag_base, flag_per_src);
 }
 
 
@@ -487,6 +507,55 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 // -----------------------------------------------------------------------------
 // Chain block
 // -----------------------------------------------------------------------------
+// A chain wave's SGD step on its LDS copies: W2 rows of h tile w, W3 columns
+// of h tile w, b2 of h tile w, b3 (wave 0).  Every wave is past its reads of
+// the old values (a barrier separates them): all old values read first, then
+// all the updated ones written.
+__device__ __forceinline__ void pk_chain_update(const PersistArgs& a, float* lds, int w, int q, int i,
+                                                const f32x4 (&g)[8], const f32x4& g3, float sb2,
+                                                float sb3) {
+  float* W2 = lds + ChLay::W2;
+  float* W3 = lds + ChLay::W3;
+  float* B2 = lds + ChLay::B2;
+  float* B3 = lds + ChLay::B3;
+  float w2o[8][4], w3o[4];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w2o[t][r] = W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) w3o[r] = W3[(4 * q + r) * kS2 + 16 * w + i];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i] = w2o[t][r] - a.lr * g[t][r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (4 * q + r < kD3) W3[(4 * q + r) * kS2 + 16 * w + i] = w3o[r] - a.lr * g3[r];
+  if (q == 0) {
+    B2[16 * w + i] -= a.lr * sb2;                     // h = 16 w + i
+    if (w == 0 && i < kD3) B3[i] -= a.lr * sb3;       // class i
+  }
+}
+
+// Pull the step s_pend slot of every replica (rank-ordered sum into v) and
+// apply it.  false: a peer did not arrive in time.
+__device__ __forceinline__ bool pk_chain_pull_apply(const PersistArgs& a, float* lds, uint64_t s_pend,
+                                                    const float4 (&pend)[10], int64_t chb, int w,
+                                                    int q, int i) {
+  float4 v[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) v[j] = pend[j];
+  if (!px_pull_wave<10>(a, s_pend, v, chb + (int64_t)w * kPxCh, 4 * kPxCh, a.nrep * kNL1 * 4 + w, 4))
+    return false;
+  f32x4 g[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+  pk_chain_update(a, lds, w, q, i, g, f32x4{v[8].x, v[8].y, v[8].z, v[8].w}, v[9].x, v[9].y);
+  return true;
+}
+
 template <bool DP>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -544,6 +613,10 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 
   bool ok = true;
   const int stamp_on = g_pk_stamp_on && c == 0;
+  float4 pend[10];  // DP: this wave's last pushed gradient slot, applied after the next partials
+  bool have_pend = false;
+  uint64_t s_pend = 0;
+  const int64_t chb = (int64_t)a.nrep * kNL1 * 4 * kPxL1;  // chain slots' base
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(1, 0);
     const uint64_t s = s0 + (uint64_t)it;
@@ -588,6 +661,12 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     y = a.labels[r0 + rb0 + srow];
     ok = __syncthreads_and(ok ? 1 : 0) != 0;
     if (!ok) break;
+    if (DP && have_pend) {  // the previous step's gradient summed over the replicas, applied
+      ok = __syncthreads_and(pk_chain_pull_apply(a, lds, s_pend, pend, chb, w, q, i) ? 1 : 0) != 0;
+      if (!ok) break;
+      have_pend = false;
+      __syncthreads();  // W2 / W3 / b updated before layer 2 reads them
+    }
     PK_STAMP(1, 1);
 
     // ---- layer 2: H2 = relu(H1 W2^T + b2), wave w -> 16 output columns ----
@@ -807,50 +886,31 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       sb2 += __shfl_xor(sb2, 32, 64);
       sb3 += __shfl_xor(sb3, 16, 64);
       sb3 += __shfl_xor(sb3, 32, 64);
-      if (DP) {  // data parallel: sum this wave's h tile over the replicas
-        // (chain c pushes to the peers d with d % 4 == c; every chain reads all)
-        float4 v[10];
+      if (DP) {
+        // data parallel: push this wave's h tile to the peers now (chain c to
+        // the peers d with d % 4 == c; every chain reads all), sum and apply it
+        // after the next step's partials arrived -- the exchange latency hides
+        // behind that wait.  Nothing reads W2 / W3 / b before then.
+        pend[8] = make_float4(g3[0], g3[1], g3[2], g3[3]);
+        pend[9] = make_float4(sb2, sb3, 0.f, 0.f);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
-        v[8] = make_float4(g3[0], g3[1], g3[2], g3[3]);
-        v[9] = make_float4(sb2, sb3, 0.f, 0.f);
-        const int64_t chb = (int64_t)a.nrep * kNL1 * 4 * kPxL1;
-        bool xok = px_allreduce_wave<10>(a, s, v, chb + (int64_t)w * kPxCh, 4 * kPxCh,
-                                         a.nrep * kNL1 * 4 + w, 4, kNCH, c);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
-        g3 = f32x4{v[8].x, v[8].y, v[8].z, v[8].w};
-        sb2 = v[9].x;
-        sb3 = v[9].y;
-        ok = __syncthreads_and(xok ? 1 : 0) != 0;
-        if (!ok) break;
+        for (int t = 0; t < 8; ++t) pend[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+        px_push_wave<10>(a, s, pend, chb + (int64_t)w * kPxCh, 4 * kPxCh, a.nrep * kNL1 * 4 + w, 4,
+                         kNCH, c);
+        have_pend = true;
+        s_pend = s;
+      } else {
+        PK_STAMP(1, 6);
+        pk_chain_update(a, lds, w, q, i, g, g3, sb2, sb3);
+        PK_STAMP(1, 7);
       }
-      PK_STAMP(1, 6);
-      // every wave is past its dZ1 / layer-2 reads of W2, W3 (barrier above):
-      // all old values read first, then all the updated ones written
-      float w2o[8][4], w3o[4];
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) w2o[t][r] = W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w3o[r] = W3[(4 * q + r) * kS2 + 16 * w + i];
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          W2[(16 * w + 4 * q + r) * kS1 + 16 * t + i] = w2o[t][r] - a.lr * g[t][r];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * q + r < kD3) W3[(4 * q + r) * kS2 + 16 * w + i] = w3o[r] - a.lr * g3[r];
-      if (q == 0) {
-        B2[16 * w + i] -= a.lr * sb2;                     // h = 16 w + i
-        if (w == 0 && i < kD3) B3[i] -= a.lr * sb3;       // class i
-      }
-      PK_STAMP(1, 7);
     }
     __syncthreads();
     PK_STAMP(1, 5);
+  }
+  if (DP && have_pend && ok) {  // the last step's summed gradient, before the write-back
+    ok = __syncthreads_and(pk_chain_pull_apply(a, lds, s_pend, pend, chb, w, q, i) ? 1 : 0) != 0;
+    __syncthreads();
   }
 
   // ---- epilogue: stats; chain 0 writes W2, b2, W3, b3 back ----

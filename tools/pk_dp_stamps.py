@@ -2,7 +2,8 @@
 two processes share cuda:0 through IPC (a rehearsal of two GPUs), rank 0
 records the in-kernel stamps of layer-1 block 0 and chain block 0 for steps
 8..15 of a launch (same phases as tools/pk_stamps.py; the replica exchange
-sits inside "bwd+update" and "dW2/dW3+update").  Prints JSON; argv[1] = file."""
+sits inside "bwd+xchg+update" and, for the chains, is split between the
+push after dW2 and the pull after the next partials).  Prints JSON; argv[1] = file."""
 import json
 import os
 import socket
@@ -42,14 +43,15 @@ def _worker(rank, world, port, out):
         v = C.mlp_persist_stamps()
         st = [[[v[(r * 8 + s) * 8 + p] for p in range(8)] for s in range(8)] for r in range(3)]
         L1 = ["fwd+publish", "dZ1 wait", "bwd+xchg+update"]
-        CH = ["partials wait", "L2/L3 fwd+softmax", "dZ2,dZ1 publish", "row exchange", "dW2/dW3+xchg+update"]
+        # the chain pushes its gradient after dW2 and sums + applies it after the
+        # next step's partials arrived: "partials wait" includes that pull
+        CH = ["partials wait + xchg pull/update", "L2/L3 fwd+softmax", "dZ2,dZ1 publish", "row exchange",
+              "dW2/dW3 + xchg push"]
         res = {"layer1": {}, "chain": {}}
         for name, role, labels in (("layer1", 0, L1), ("chain", 1, CH)):
             for k, lab in enumerate(labels):
                 res[name][lab] = round(statistics.median(
                     [(st[role][s][k + 1] - st[role][s][k]) / 100.0 for s in range(8)]), 3)
-        res["chain"]["dW2 MFMAs + xchg (wave 0)"] = round(statistics.median(
-            [(st[1][s][6] - st[1][s][4]) / 100.0 for s in range(8)]), 3)
         res["step_us"] = round(statistics.median(
             [(st[0][s + 1][0] - st[0][s][0]) / 100.0 for s in range(7)]), 3)
         json.dump(res, open(out, "w"), indent=1)
