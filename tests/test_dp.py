@@ -3,18 +3,12 @@ per replica, exactly as bench.py runs one rank per GPU.  Checks that every
 replica ends bit-identical and equal to single-process SGD on the averaged
 gradient of all shards (what the reference's identity "ring" never did)."""
 import os
-import socket
 import tempfile
 
 import pytest
 import torch
-import torch.multiprocessing as mp
+from spawn_util import spawn_group
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _worker(rank, world, port, outdir, momentum):
@@ -41,8 +35,7 @@ def test_gloo_data_parallel(world, momentum):
     from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
 
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, momentum), nprocs=world,
-                           start_method="spawn", join=True)
+        spawn_group(_worker, world, lambda port: (world, port, d, momentum))
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
     for o in outs[1:]:
         assert torch.equal(o["P"], outs[0]["P"])

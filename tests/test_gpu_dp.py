@@ -4,20 +4,14 @@ This exercises exactly the N>1 step structure of bench.py — fused HIP
 fwd/bwd writing gradients, all-reduce, HIP SGD update — except the RCCL call
 itself (covered on 8 GPUs by the driver's scaling run)."""
 import os
-import socket
 import tempfile
 
 import pytest
 import torch
-import torch.multiprocessing as mp
+from spawn_util import spawn_group
 
 pytestmark = pytest.mark.gpu
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _worker(rank, world, port, outdir, kind):
@@ -57,8 +51,7 @@ def test_two_replicas_one_gpu(kind):
 
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, kind), nprocs=world,
-                           start_method="spawn", join=True)
+        spawn_group(_worker, world, lambda port: (world, port, d, kind))
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
     assert torch.equal(outs[0], outs[1])
     dims = (784, 128, 64, 10) if kind == "fused" else (784, 256, 128, 10)
@@ -82,8 +75,7 @@ def test_wide_bucket_overlap_matches_serial_sync(sync):
     got = {}
     for kind in (f"wide{sync}_delay", f"wide{sync}_serial"):
         with tempfile.TemporaryDirectory() as d:
-            mp.start_processes(_worker, args=(world, _free_port(), d, kind), nprocs=world,
-                               start_method="spawn", join=True)
+            spawn_group(_worker, world, lambda port: (world, port, d, kind))
             got[kind] = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"]
                          for r in range(world)]
     assert torch.equal(got[f"wide{sync}_delay"][0], got[f"wide{sync}_delay"][1])

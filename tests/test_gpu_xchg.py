@@ -3,7 +3,6 @@ kernel) on ONE MI355X: N replicas share the GPU, either inside one process
 (pointers exchanged directly) or as separate processes (IPC handles) — the
 same kernel and flag protocol that runs across GPUs of a node."""
 import os
-import socket
 import tempfile
 
 import pytest
@@ -16,6 +15,7 @@ from hipdsml.models.mlp import MlpLayout, MlpSpec, grads_ref, init_params
 from hipdsml.parallel.dist import DistContext
 from hipdsml.parallel.xchg import (make_local_act_group, make_local_group, replica_streams,
                                    swizzle_inputs)
+from spawn_util import spawn_group
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -165,11 +165,6 @@ def test_act_exchange_missing_peer_times_out():
     _fresh(_case_act_missing_peer)
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
 
 def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=0):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
@@ -208,9 +203,8 @@ def test_two_processes_ipc(world, graph_steps, sync):
     persistent step in every process (36 workgroups each, all resident) with
     the weight gradients summed over the replicas inside the launch."""
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ipc_worker, args=(world, _free_port(), d, graph_steps, sync,
-                                              4 if sync in ("xact", "auto") else 0), nprocs=world,
-                           start_method="spawn", join=True)
+        spawn_group(_ipc_worker, world, lambda port: (world, port, d, graph_steps, sync,
+                                              4 if sync in ("xact", "auto") else 0))
         Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(world)]
     for P in Ps[1:]:
         assert torch.equal(Ps[0], P)
@@ -240,8 +234,7 @@ def _ar_worker(rank, world, port, outdir, algo="oneshot"):
 def test_standalone_allreduce_ipc(algo):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ar_worker, args=(world, _free_port(), d, algo), nprocs=world,
-                           start_method="spawn", join=True)
+        spawn_group(_ar_worker, world, lambda port: (world, port, d, algo))
         for r in range(world):
             res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["res"]
             for it in range(4):
@@ -279,8 +272,7 @@ def _ar_values_worker(rank, world, port, outdir, algo):
 @pytest.mark.parametrize("algo", ["oneshot", "twoshot"])
 def test_standalone_allreduce_values_ipc(world, algo):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ar_values_worker, args=(world, _free_port(), d, algo), nprocs=world,
-                           start_method="spawn", join=True)
+        spawn_group(_ar_values_worker, world, lambda port: (world, port, d, algo))
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
     for n in SIZES:
         g = torch.Generator().manual_seed(n)
