@@ -227,7 +227,10 @@ class MlpTrainer:
         or the in-house multi-ring send/recv all-reduce on it."""
         if mode == "pk":
             self.xchg = self._exchanges["pk"]
-            self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0, self.xchg)
+            # waits on peers are bounded like the other exchanges' (ranks can enter
+            # a launch seconds apart, e.g. around a checkpoint)
+            self.runner.set_persist(self.pk_buf, self.pk_err, max(2000.0, self.xchg_timeout_ms),
+                                    self.xchg)
             return
         if self.pk_buf is not None:
             self.runner.set_persist(None)  # leave the persistent step
