@@ -15,6 +15,8 @@
 //   softmax_xent_k   : fp32 logits -> CE stats, dZ = (p - y)/B in bf16 (+ ^T)
 //   rowsum_bf16_k    : bias gradients  db[n] = sum_m dZ^T[n][m]
 //   sgd_cast_k       : fp32 master W -= lr*g, refresh bf16 W and bf16 W^T
+#include <cstdlib>
+
 #include "common.h"
 #include "../dsml.h"
 
@@ -479,8 +481,16 @@ hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, i
   dim3 grid((N + 15) / 16, (M + 63) / 64);
   // Long K: 8 waves (512 threads) each streaming K/8 with 8 K-steps of loads
   // in flight: twice the bytes in flight per CU of the 4-wave form.
+  // Mid K (the 784-wide input layer): 8 waves of 4 K-steps, so every wave's
+  // whole K range (<= 128) is ONE load batch instead of two dependent rounds.
+  static const int mid8 = [] {
+    const char* e = getenv("HIPDSML_ROWS64_MID");  // off until measured on MI355X
+    return e ? atoi(e) : 0;
+  }();
   if (K >= 8 * 32 * 8)
     hipLaunchKernelGGL((gemm_rows64_k<8, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  else if (K >= 4 * 32 * 4 && K <= 8 * 128 && mid8)
+    hipLaunchKernelGGL((gemm_rows64_k<4, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
   else if (K >= 4 * 32 * 4)
     hipLaunchKernelGGL((gemm_rows64_k<4, 4>), grid, dim3(256), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
   else
