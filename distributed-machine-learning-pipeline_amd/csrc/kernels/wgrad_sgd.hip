@@ -63,6 +63,8 @@ __device__ __forceinline__ uint4 wg_frag(const char* img, int m0, int c0, int la
 
 constexpr int kWgLds = 64 * kWgPitch * 4;  // two operand images (16 KiB), later the fp32 tile (17 KiB)
 static_assert(kWgLds >= 2 * kWgImg, "LDS carve");
+// + the bias gradient's 4 row-group partials per column ([4][64] floats)
+constexpr int kWgLdsTot = kWgLds + 4 * 64 * 4;
 
 // 1. a tile's W loads (rows rl + 16j, columns cl..cl+3), issued before anything else
 __device__ __forceinline__ void wg_load_w(const WgArgs& a, int kt, int nt, float4 (&wold)[4]) {
@@ -146,10 +148,14 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
                                                               __builtin_bit_cast(wg_bf16x8, fx[y]),
                                                               acc[x][y], 0, 0, 0);
     }
-    // bias gradient (k-tile 0 only): column sums of the Z image
-    if (kt == 0 && tid < 64) {
-      const int ch = tid >> 3, e = tid & 7;
-      for (int r = 0; r < 64 && mb + r < a.M; ++r) {
+    // bias gradient (k-tile 0 only): column sums of the Z image, all 256
+    // threads (column tid & 63, rows 16 (tid >> 6) .. +15): a quarter of the
+    // serial LDS reads of one 64-thread loop, which made these tiles the grid's
+    // stragglers
+    if (kt == 0) {
+      const int c = tid & 63, ch = c >> 3, e = c & 7, r0 = 16 * (tid >> 6);
+#pragma unroll 1  // (unrolled, the loads raise VGPRs past occupancy 5)
+      for (int r = r0; r < r0 + 16 && mb + r < a.M; ++r) {
         const uint16_t v = *reinterpret_cast<const uint16_t*>(imz + r * 128 + 16 * (ch ^ wg_swz(r)) + 2 * e);
         dbias += bf16_to_f32(v);
       }
@@ -169,6 +175,8 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
         for (int r = 0; r < 4; ++r)
           tile[(wn + 16 * x + 4 * g + r) * kWgPitch + wk + 16 * y + i] = acc[x][y][r] * a.alpha;
   }
+  float* bsum = reinterpret_cast<float*>(lds + kWgLds);
+  if (kt == 0) bsum[tid] = dbias;  // [row group][column]
   __syncthreads();
   if (kv) {
 #pragma unroll
@@ -193,7 +201,7 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
     }
   }
   if (kt == 0 && tid < 64 && n0 + tid < a.N) {
-    const float db = a.alpha * dbias;
+    const float db = a.alpha * (((bsum[tid] + bsum[64 + tid]) + bsum[128 + tid]) + bsum[192 + tid]);
     if (a.bias) a.bias[n0 + tid] -= a.lr * db;
     if (a.bgrad) a.bgrad[n0 + tid] = db;
   }
@@ -206,12 +214,12 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
 }
 
 __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
   wgrad_tile(a, blockIdx.x, blockIdx.y, lds);
 }
 
 __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
-  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
   const int b = blockIdx.x;
   int j = 0;
 #pragma unroll
@@ -248,7 +256,7 @@ __device__ __forceinline__ void wg_pick(const WgMulti& m, int b, WgArgs& a, int&
 // and MFMAs, and a plain grid-stride stream of the same bytes (W fp32 RMW +
 // bf16 copy)
 __global__ __launch_bounds__(256) void wgrad_nomma_k(WgMulti m) {
-  __shared__ __attribute__((aligned(16))) char lds[kWgLds];
+  __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
   WgArgs a;
   int kt, nt;
   wg_pick(m, blockIdx.x, a, kt, nt);
