@@ -17,7 +17,7 @@ from hipdsml.parallel.dist import DistContext  # noqa: E402
 C = require_native()
 spec = MlpSpec.parse(sys.argv[1] if len(sys.argv) > 1 else "784-128-64-10")
 tr = MlpTrainer(spec, synthetic_mnist(64 * 20, seed=0, dim=spec.dims[0]), batch=64,
-                ctx=DistContext(device=torch.device("cuda", 0)))
+                ctx=DistContext(device=torch.device("cuda", 0)), persist=False)
 tr.train_steps(20)
 tr.synchronize()
 C.mlp_set_stamping(True)
