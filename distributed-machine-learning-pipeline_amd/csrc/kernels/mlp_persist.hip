@@ -464,13 +464,24 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
       }
     }
     if (DP) {  // data parallel: sum this wave's fragments over the replicas
-      float4 v[4];
+      // (waves 1-3 own 3 k tiles, wave 0 four: only real tiles travel)
+      bool xok;
+      const int64_t slot = (int64_t)(lb * 4 + w) * kPxL1, per = (int64_t)kNL1 * 4 * kPxL1;
+      if (w == 0) {
+        float4 v[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
-      bool xok = px_allreduce_wave<4>(a, s, v, (int64_t)(lb * 4 + w) * kPxL1,
-                                      (int64_t)kNL1 * 4 * kPxL1, lb * 4 + w, kNL1 * 4, 1, 0);
+        for (int t = 0; t < 4; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+        xok = px_allreduce_wave<4>(a, s, v, slot, per, lb * 4 + w, kNL1 * 4, 1, 0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+        for (int t = 0; t < 4; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+      } else {
+        float4 v[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) v[t] = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+        xok = px_allreduce_wave<3>(a, s, v, slot, per, lb * 4 + w, kNL1 * 4, 1, 0);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) g[t] = f32x4{v[t].x, v[t].y, v[t].z, v[t].w};
+      }
       ok = __syncthreads_and(xok ? 1 : 0) != 0;
       if (!ok) break;
     }
