@@ -14,7 +14,9 @@ the weight-gradient kernel over xGMI, RCCL's all-reduce, or the in-house
 multi-ring all-reduce on RCCL send/recv — chosen at init by a self-test + timing
 of every candidate), SGD update.  For N>1 the JSON also carries the µs/step of
 every sync candidate and the 1 MiB device all-reduce latency of each algorithm
-(BASELINE's second metric: ring all-reduce at 1 MiB).
+(BASELINE's second metric: ring all-reduce at 1 MiB).  Every N>1 run ends
+with a cross-rank bit-identity check of the parameters ("replicas_identical";
+exit 3 when they differ).
 
 Launch:
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -189,6 +191,11 @@ def run(a) -> int:
     elapsed = t1 - t0
     elapsed = ctx.all_reduce_scalars(elapsed, op="max")[0] if ctx.is_distributed else elapsed
     st = tr.read_stats(global_=True)
+    if a.inject_divergence is not None and ctx.rank == a.inject_divergence:
+        tr.P.view(-1)[0] += 1e-3  # fault injection (tests): this replica drifts off
+    # every replica applied the same summed gradient: the parameters must be
+    # bit-identical on all ranks after the timed steps (no weight broadcast)
+    identical = ctx.replicas_identical(tr.P, "bench/P") if n > 1 else True
     ar_us = None
     if n > 1 and tr.backend == "hip" and not a.no_allreduce_probe:
         ar_us = allreduce_latency_us(ctx, tr.comm, ring_chunk=a.ring_chunk)
@@ -232,9 +239,13 @@ def run(a) -> int:
             "allreduce_1MiB_us": ar_us,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
+            "replicas_identical": identical,
         }
         print(json.dumps(out), flush=True)
     ctx.destroy()
+    if not identical:
+        print("bench.py: replicas diverged (parameters differ across ranks)", file=sys.stderr)
+        return 3
     return 0
 
 
@@ -269,6 +280,9 @@ def main(argv=None) -> int:
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo process group (RCCL refuses "
                          "two ranks on one GPU); the JSON says rehearsal: true")
+    ap.add_argument("--inject-divergence", type=int, default=None, metavar="RANK",
+                    help="fault injection for tests: perturb RANK's parameters after the timed "
+                         "steps, so the end-of-run replica check must fail (exit 3)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/rank plumbing on CPU (gloo, torch math); rehearsal: true")
     a = ap.parse_args(argv)

@@ -52,6 +52,7 @@ def main() -> int:
     ctx.barrier()
     el = ctx.all_reduce_scalars(t1 - t0, op="max")[0] if ctx.is_distributed else t1 - t0
     n = ctx.world_size
+    identical = ctx.replicas_identical(tr.P, "bench_wide/P") if n > 1 else True
     d = spec.dims
     flops = 6 * a.batch * sum(d[i] * d[i + 1] for i in range(len(d) - 1)) * a.steps * n
     if ctx.rank == 0:
@@ -60,9 +61,13 @@ def main() -> int:
                           "ms_per_step": round(1e3 * el / a.steps, 4), "tflops": round(flops / el / 1e12, 2),
                           "dtype": "bf16 (fp32 master/accum)", "data": "synthetic",
                           "config": {"model": f"MLP {spec}", "global_batch": a.batch * n,
-                                     "parallelism": f"dp{n}", "sync": a.sync if n > 1 else "none"}}),
+                                     "parallelism": f"dp{n}", "sync": a.sync if n > 1 else "none"},
+                          "replicas_identical": identical}),
               flush=True)
     ctx.destroy()
+    if not identical:
+        print("bench_wide.py: replicas diverged (parameters differ across ranks)", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -41,7 +41,8 @@ def cmd_device_server(a) -> int:
     ids = [int(i) for i in a.device_ids.split(",")] if a.device_ids else list(range(1, len(ports) + 1))
     servers = []
     for port, gpu, did in zip(ports, gpus, ids):
-        server, addr, svc = start_device_server(did, a.mem_size, f"{a.host}:{port}", backend=a.backend, gpu=gpu)
+        server, addr, svc = start_device_server(did, a.mem_size, f"{a.host}:{port}", backend=a.backend, gpu=gpu,
+                                              scratch_size=a.scratch_bytes or None)
         if a.fail_after and did == (a.fail_device or did):
             svc.arm_fault(a.fail_after, a.fail_mode)
         print(f"GPU Device server listening on port {addr.rsplit(':', 1)[1]} with device ID {did}", flush=True)
@@ -149,6 +150,9 @@ def main(argv=None) -> int:
     d.add_argument("--device-ids", default="")
     d.add_argument("--backend", default="auto", choices=["auto", "host", "hip"])
     d.add_argument("--mem-size", type=int, default=64 << 20)
+    d.add_argument("--scratch-bytes", type=int, default=0,
+                   help="private ring scratch window per device (0: 64 MiB GPU, 1 MiB host); "
+                        "host data-parallel TrainSteps stages the whole gradient there")
     d.add_argument("--fail-after", type=int, default=0,
                    help="fault injection: die on the N-th data-plane RPC (0 = never)")
     d.add_argument("--fail-device", type=int, default=0, help="only this device id (0 = all)")

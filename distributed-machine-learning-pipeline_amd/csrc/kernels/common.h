@@ -54,6 +54,32 @@ __device__ __forceinline__ void full_barrier() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// ---- Cross-device (xGMI) release / acquire: why no fence instruction -------
+// Every peer-exchange protocol here (pk in mlp_persist.hip, xact, xgmi, the
+// standalone all-reduce in xchg.hip) follows ONE pattern, and it is a complete
+// system-scope release/acquire without buffer_wbl2 / buffer_inv:
+//  * memory: exchange buffers are hipExtMallocWithFlags(hipDeviceMallocUncached)
+//    (runtime/peer_exchange.cpp), i.e. MTYPE UC -- no L1/L2 ever holds a line;
+//  * producer: payload stored with sc0 sc1 (system scope, write-through) ->
+//    `s_waitcnt vmcnt(0)` by EVERY storing wave (a store retires from vmcnt
+//    only when the owning device's memory has acknowledged it, across xGMI
+//    too) -> flag store (system-scope relaxed atomic) by a lane of that wave,
+//    or by one lane behind a workgroup barrier that follows every wave's wait.
+//    A system-scope release fence would add `buffer_wbl2 sc0 sc1`: it writes
+//    back DIRTY L2 lines, and the payload never makes any (UC, write-through),
+//    so the only thing it would order -- the payload before the flag -- is
+//    already ordered by the vmcnt wait (measured cost of the wbl2 instead:
+//    ~1.7 us per issuing wave, MI355X_MICROARCH price list);
+//  * consumer: flag polled with system-scope relaxed loads (sc0 sc1, from
+//    memory), the payload then read with sc0 sc1 loads issued only after the
+//    poll's value returned (control dependency behind its s_waitcnt): nothing
+//    can be served from a stale cache line, so `buffer_inv` (the acquire
+//    fence) would invalidate nothing these loads could hit.
+// What the pattern does NOT cover, and so never appears: plain (cached)
+// payload stores or loads on exchange memory, and flags raised by a lane for
+// other waves without the barrier.  The data-tagged 8-B granules of the
+// on-device hand-offs (one sc1 store carries value + tag) need no ordering.
+//
 // Spin until the peer flag *f reaches `want` (system-scope relaxed polls).
 // Gives up after `timeout` s_memrealtime ticks (100 MHz) and sets *err — and
 // also stops as soon as *err is already set: once any wait of the exchange has

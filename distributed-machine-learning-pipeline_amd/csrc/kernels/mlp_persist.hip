@@ -243,7 +243,9 @@ __device__ __forceinline__ void px_push_wave(const PersistArgs& a, uint64_t s, c
 #pragma unroll
     for (int j = 0; j < NV; ++j) px_st4(r, (lane * (4 * NV) + 4 * j) * 4, v[j]);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot landed before its flag
+  // the slot landed (acknowledged by every peer's memory) before its flag: the
+  // system-scope release of this protocol (common.h, "Cross-device release")
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
     for (int d = 0; d < a.nrep; ++d)
       if (d != a.rep && d % mod == sel)

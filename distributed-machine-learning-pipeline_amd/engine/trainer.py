@@ -110,7 +110,9 @@ class MlpTrainer:
         if capture_collectives is None:  # RCCL collectives recorded into the step graphs
             import os
 
-            capture_collectives = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "1") != "0"
+            # off by default until a multi-GPU run has validated captured RCCL
+            # collectives: eager ncclAllReduce / send-recv per step
+            capture_collectives = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "0") == "1"
         self.capture_collectives = bool(capture_collectives)
         self.xchg_timeout_ms = xchg_timeout_ms
         self.xact_waves = int(xact_waves)  # 0: 8-wave tile blocks from 4 ranks on, else 4
@@ -163,7 +165,11 @@ class MlpTrainer:
                                   follow_torch=self._stream is None)
         self.runner.set_world_size(self.ctx.world_size)
         self._ring_chunk = int(ring_chunk_bytes)
-        self._collective_warm = False  # an eager collective step has run (RCCL connected)
+        # sync modes whose collectives have run one eager step (RCCL connects a
+        # peer pair on its first send/recv, which must never happen inside a
+        # graph capture): 'rccl' warms ncclAllReduce's connections, 'ring' the
+        # send/recv pairs of the in-house ring -- tracked per mode
+        self._warm_modes: set = set()
         if not self.ctx.is_distributed:
             plain = not (self.momentum or self.weight_decay)
             if self._want_persist and plain and C.mlp_persist_supported(self.layout.desc_list()):
@@ -248,8 +254,11 @@ class MlpTrainer:
                                          self.xact_waves)
 
     def _setup_exchange(self, mode: str) -> str:
-        """Collective: build `mode`'s buffers, check one step against a
-        torch.distributed all-reduce.  Returns '' or the (agreed) error."""
+        """Collective: build `mode`'s buffers, check three steps (in two
+        launches: a launch split and a parity wrap) against fp32 torch
+        gradients summed by a torch.distributed all-reduce
+        (parallel/xchg.py verify_against_allreduce).  Returns '' or the
+        (agreed) error."""
         from ..parallel import xchg as X
 
         try:
@@ -421,7 +430,7 @@ class MlpTrainer:
         replay: a run of n = q*G + r steps replays a G-step and an r-step graph."""
         if self.backend != "hip" or not self._graphs_on():
             return
-        if self.sync_active in ("rccl", "ring") and not self._collective_warm:
+        if self.sync_active in ("rccl", "ring") and self.sync_active not in self._warm_modes:
             return  # captured on first use, after an eager step (train_steps)
         for k in self._graph_sizes(n):
             if not self.runner.captured(k):
@@ -445,11 +454,11 @@ class MlpTrainer:
             self._hip_step_torch_sync(n)
         elif self._graphs_on():
             self.steps_done += n
-            if self.sync_active in ("rccl", "ring") and not self._collective_warm:
+            if self.sync_active in ("rccl", "ring") and self.sync_active not in self._warm_modes:
                 # RCCL connects its peers on the first collective it enqueues:
                 # run that step eagerly on every rank before anything is captured
                 self.runner.step(1)
-                self._collective_warm = True
+                self._warm_modes.add(self.sync_active)
                 n -= 1
                 if n == 0:
                     return

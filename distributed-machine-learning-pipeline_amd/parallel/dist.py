@@ -129,6 +129,23 @@ class DistContext:
         with self.guard(f"store.get {key}"):
             return [bytes(store.get(f"{key}/{r}")) for r in range(self.world_size)]
 
+    def replicas_identical(self, t: torch.Tensor, key: str = "replicas") -> bool:
+        """Collective: whether `t` holds the same bytes on every rank (a
+        SHA-256 of each rank's copy, exchanged through the TCP store).  Data
+        parallelism here never broadcasts weights -- every replica applies the
+        same summed gradient -- so this is the end-of-run proof that they did
+        (the reference re-sent the weights to every device each step instead,
+        client.go:642-644)."""
+        import hashlib
+
+        if not self.is_distributed:
+            return True
+        self._hash_calls = getattr(self, "_hash_calls", 0) + 1
+        raw = t.detach().contiguous().reshape(-1).view(torch.uint8).cpu().numpy()
+        h = hashlib.sha256(raw.tobytes()).digest()
+        hs = self.all_gather_bytes(f"hipdsml/{key}/{self._hash_calls}", h)
+        return all(x == hs[0] for x in hs)
+
     def destroy(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()
@@ -141,12 +158,23 @@ class DistContext:
 _uid_counter = 0
 
 
-def make_native_comm(ctx: DistContext, blocking: bool = False):
+def rccl_blocking_default() -> bool:
+    """Blocking RCCL communicators unless HIPDSML_RCCL_NONBLOCKING=1: the
+    non-blocking config has only run with single-rank communicators so far
+    (ADVICE r2), so multi-GPU jobs keep RCCL's default mode until validated."""
+    return os.environ.get("HIPDSML_RCCL_NONBLOCKING", "0") != "1"
+
+
+def make_native_comm(ctx: DistContext, blocking: Optional[bool] = None):
     """Bootstrap a native RCCL communicator over the process group's store.
 
-    Non-blocking by default (``ncclConfig_t.blocking = 0``): no RCCL host call
-    can wait unboundedly on a dead peer, and the context's watchdog polls the
-    communicator's async error and aborts it on a fault (parallel/watchdog.py)."""
+    Blocking by default (:func:`rccl_blocking_default`).  Either way the
+    context's watchdog polls the communicator's async error and, on a fault or a
+    stalled guarded section, aborts it from its own thread (``ncclCommAbort`` is
+    legal on a blocking communicator while another thread waits in RCCL), so a
+    dead peer ends the job instead of hanging it (parallel/watchdog.py)."""
+    if blocking is None:
+        blocking = rccl_blocking_default()
     from ..ops.native import require_native
 
     global _uid_counter

@@ -11,9 +11,10 @@ keep a fault from turning into a hang:
 
 * xGMI exchange kernels bound every flag wait (``kernels/common.h``
   ``poll_flag_ge``) and set an error word the host checks after each sync;
-* RCCL communicators are created non-blocking (``ncclConfig_t.blocking = 0``)
-  so no host call waits unboundedly, and this watchdog thread polls
-  ``ncclCommGetAsyncError`` every ``interval`` seconds;
+* this watchdog thread polls ``ncclCommGetAsyncError`` of every registered
+  RCCL communicator every ``interval`` seconds (communicators are blocking by
+  default, ``HIPDSML_RCCL_NONBLOCKING=1`` makes them non-blocking so no RCCL
+  host call can wait unboundedly either);
 * every blocking host section of the job (stream syncs, collectives on the
   process group) runs under :meth:`Watchdog.guard`.  A section that exceeds
   ``timeout`` seconds — or any RCCL async error — makes the watchdog abort

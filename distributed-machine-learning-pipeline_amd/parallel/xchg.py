@@ -102,6 +102,10 @@ def make_exchange(ctx: DistContext, half_floats: int, ntiles: int, timeout_ms: f
     else:
         try:
             x = C.PeerExchange(ctx.device.index, half_floats, ntiles)
+            if x.memory_kind != "uncached":
+                # the fence-free release/acquire of every exchange protocol
+                # relies on uncached (MTYPE UC) memory (kernels/common.h)
+                raise RuntimeError(f"exchange memory is {x.memory_kind}, not uncached")
             x.set_timeout_ms(timeout_ms)
             h = x.ipc_handle()
         except Exception as e:  # noqa: BLE001
@@ -215,26 +219,45 @@ def check(x, where: str = "") -> None:
                            "a replica stopped or fell behind")
 
 
-def verify_against_allreduce(trainer, tol: float = 1e-6) -> float:
-    """One step through the exchange vs. the same step with a torch.distributed
-    all-reduce; restores the trainer state afterwards.  Returns the max abs
-    difference over all ranks (inf if replicas disagree bit-wise or a peer
-    timed out).  Every rank runs the same collectives whatever happens locally."""
+def verify_against_allreduce(trainer, steps: int = 3) -> float:
+    """`steps` optimizer steps through the active exchange vs. the same steps
+    with fp32 torch gradients summed by a torch.distributed all-reduce; the
+    trainer state is restored afterwards.  Returns the max abs parameter
+    difference over all ranks (inf if replicas disagree bit-wise, a peer timed
+    out or a persistent hand-off gave up).  Every rank runs the same
+    collectives whatever happens locally.
+
+    The exchange runs the steps as TWO launches (1, then steps - 1): for the
+    persistent step (sync='pk') that covers a launch split (the step counter
+    and hand-off tags carried over between launches), and with >= 3 steps the
+    parity halves of every receive buffer are reused (step s and s + 2 share
+    one), so a stale slot or flag from two steps back would show up here."""
     import torch.distributed as dist
+
+    from ..models.mlp import grads_ref
 
     ctx = trainer.ctx
     r = trainer.runner
+    lay = trainer.layout
+    steps = max(2, int(steps))
     P0, ctr0, st0 = trainer.P.clone(), trainer.ctr.clone(), trainer.stats.clone()
-    r.fwd_bwd()
-    r.synchronize()
-    g = trainer.G.clone()
-    dist.all_reduce(g)
-    want = P0 - (trainer.lr / ctx.world_size) * g
-    trainer.ctr.copy_(ctr0)
+    s0 = int(ctr0[1].item())
+    want = P0.clone()
+    d0 = lay.spec.dims[0]
+    for k in range(steps):
+        b = (s0 + k) % trainer.nbatches
+        Xb = trainer.X[b * trainer.batch:(b + 1) * trainer.batch, :d0]
+        yb = trainer.y[b * trainer.batch:(b + 1) * trainer.batch].long()
+        g = grads_ref(lay, want, Xb, yb)[0].contiguous()
+        dist.all_reduce(g)
+        want = want - (trainer.lr / ctx.world_size) * g
     torch.cuda.synchronize(ctx.device)
     r.step(1)
+    r.step(steps - 1)
     r.synchronize()
     timed_out = float(trainer.xchg.error() != 0)
+    if trainer.pk_buf is not None and r.persist_active() and r.persist_failed():
+        timed_out = 1.0  # a hand-off of the persistent step itself gave up
     diff = (trainer.P - want).abs().max().reshape(1)
     ref = trainer.P.clone()
     dist.broadcast(ref, 0)

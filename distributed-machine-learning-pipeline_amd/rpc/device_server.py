@@ -230,10 +230,13 @@ class GPUDeviceServicer:
 
             C = require_native()
             try:
-                # non-blocking: no RCCL host call waits unboundedly on a dead
-                # peer; the coordinator's Abort fan-out (ncclCommAbort) makes
-                # in-flight RCCL kernels return
-                comm = C.RcclComm(request.uniqueId, request.rank, request.nranks, self.dev.gpu, False)
+                # blocking unless HIPDSML_RCCL_NONBLOCKING=1 (parallel/dist.py);
+                # either way the coordinator's Abort fan-out (ncclCommAbort)
+                # makes in-flight RCCL kernels return
+                from ..parallel.dist import rccl_blocking_default
+
+                comm = C.RcclComm(request.uniqueId, request.rank, request.nranks, self.dev.gpu,
+                                  rccl_blocking_default())
             except Exception as e:  # init failure (peer died during bootstrap)
                 context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
             self.comms[cid] = comm
@@ -468,7 +471,10 @@ class GPUDeviceServicer:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION,
                               f"data-parallel TrainSteps on host devices needs comm {request.commId} "
                               f"set up with rank {rank} of {world} (CommInit backend=rpc)")
-            host_ar = self._host_grad_allreduce(request.commId, world, layout.nparams * 4)
+            try:
+                host_ar = self._host_grad_allreduce(request.commId, world, layout.nparams * 4)
+            except ValueError as e:  # the gradient does not fit the ring scratch window
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         try:
             self.trainer = MlpTrainer(spec, ds, batch=batch, lr=request.lr or 0.01, ctx=ctx,
                                       seed=request.seed, momentum=request.momentum,
@@ -493,8 +499,10 @@ class GPUDeviceServicer:
         seg = (-(-(nbytes // 4) // n) + 3) // 4 * 16
         gaddr = self.dev.scratch_addr + (seg + 255) // 256 * 256
         if gaddr + nbytes > self.dev.max_addr + self.dev.scratch_size:
+            need = gaddr + nbytes - self.dev.max_addr
             raise ValueError(f"gradient of {nbytes} B does not fit the {self.dev.scratch_size} B "
-                             "ring scratch window")
+                             f"ring scratch window (needs {need} B: start the device server with "
+                             f"a larger --scratch-bytes)")
 
         def allreduce(g: torch.Tensor) -> None:
             self.dev.write(gaddr, g.detach().float().contiguous().numpy().tobytes(), internal=True,
@@ -601,9 +609,12 @@ def _capture(err, fn, *args):
 
 
 def start_device_server(device_id: int, mem_size: int, address: str = "127.0.0.1:0",
-                        backend: str = "auto", gpu: int = 0, max_workers: int = 32):
-    """Start one device server; returns (grpc_server, address, servicer)."""
-    dev = make_device(device_id, mem_size, backend, gpu=gpu)
+                        backend: str = "auto", gpu: int = 0, max_workers: int = 32,
+                        scratch_size: Optional[int] = None):
+    """Start one device server; returns (grpc_server, address, servicer).
+    `scratch_size` sizes the private ring window above max_addr (None: 64 MiB
+    on a GPU, 1 MiB on the host)."""
+    dev = make_device(device_id, mem_size, backend, gpu=gpu, scratch_size=scratch_size)
     svc = GPUDeviceServicer(dev)
     server, addr = serve("GPUDevice", svc, address, max_workers=max_workers)
     svc.server = server

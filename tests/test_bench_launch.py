@@ -41,6 +41,18 @@ def test_gpus_n_spawns_n_ranks(n):
     assert out["rehearsal"] is True and out["device"] == "cpu"
     assert out["physical_gpus"] == 0
     assert out["steps"] == 3 and out["warmup"] == 1 and out["value"] > 0
+    assert out["replicas_identical"] is True
+
+
+def test_diverged_replica_fails_the_run():
+    """A replica whose parameters drift off (fault injection after the timed
+    steps) must make the run exit non-zero with replicas_identical: false."""
+    p = _run(["--gpus", "2", "--cpu-dry-run", "--steps", "2", "--warmup", "1",
+              "--samples-per-rank", "256", "--inject-divergence", "1"])
+    assert p.returncode != 0, p.stderr[-2000:]  # ranks exit 3; torchrun reports 1
+    assert _json(p.stdout)["replicas_identical"] is False
+    assert "exitcode  : 3" in p.stderr
+    assert "replicas diverged" in p.stderr
 
 
 def test_single_rank_runs_in_process():
