@@ -545,7 +545,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("head_set_stamping", &head_set_stamping);
   m.def("head_set_debug", &head_set_debug);
-  m.def("wgrad_sgd_multi", [bf16p](py::list layers, int variant, int grid) {
+  m.def("wgrad_sgd_multi", [bf16p](py::list layers) {
     // each item: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad); tensors may be None
     std::vector<WgLayer> v;
     auto opt = [](py::handle h) -> c10::optional<torch::Tensor> {
@@ -574,8 +574,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
       v.push_back(a);
     }
-    hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), variant, grid), "wgrad_sgd_multi");
-  }, py::arg("layers"), py::arg("variant") = 0, py::arg("grid") = 0);
+    hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream()), "wgrad_sgd_multi");
+  }, py::arg("layers"));
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

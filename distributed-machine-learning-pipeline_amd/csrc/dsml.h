@@ -276,7 +276,7 @@ struct WgLayer {
 // variant 0: one workgroup per 64 x 64 tile (the production kernel); 20 / 21:
 // roofline probes (tools/wgrad_var.py): the same tiles without operand staging
 // and MFMAs / a `grid`-workgroup linear stream of the same W bytes
-hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int variant = 0, int grid = 0);
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 void head_set_debug(int v);

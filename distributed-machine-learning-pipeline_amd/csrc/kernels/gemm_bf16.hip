@@ -483,13 +483,9 @@ hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, i
   // in flight: twice the bytes in flight per CU of the 4-wave form.
   // Mid K (the 784-wide input layer): 8 waves of 4 K-steps, so every wave's
   // whole K range (<= 128) is ONE load batch instead of two dependent rounds.
-  static const int mid8 = [] {
-    const char* e = getenv("HIPDSML_ROWS64_MID");  // 0: the 4-wave form (A/B)
-    return e ? atoi(e) : 1;
-  }();
   if (K >= 8 * 32 * 8)
     hipLaunchKernelGGL((gemm_rows64_k<8, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
-  else if (K >= 4 * 32 * 4 && K <= 8 * 128 && mid8)
+  else if (K >= 4 * 32 * 4 && K <= 8 * 128)
     hipLaunchKernelGGL((gemm_rows64_k<4, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
   else if (K >= 4 * 32 * 4)
     hipLaunchKernelGGL((gemm_rows64_k<4, 4>), grid, dim3(256), 0, s, A, lda, B, ldb, M, N, K, epi, vec);

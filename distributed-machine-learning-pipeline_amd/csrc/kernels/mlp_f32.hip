@@ -610,8 +610,7 @@ hipError_t mlp_f32_rowchain(const float* P, const float* slab, int nsplit, float
                             const MlpDesc& d, float* stats, int train, float inv_batch,
                             hipStream_t s) {
   if (nsplit < 1 || nsplit > 8) return hipErrorInvalidValue;
-  static const bool no_fast = getenv("HIPDSML_NO_FAST") != nullptr;
-  if (!no_fast) {
+  {
     const hipError_t e = mlp_f32_rowchain_fast(P, slab, nsplit, ws, labels, ctr, row0, d, stats,
                                                train, inv_batch, s);
     if (e != hipErrorNotSupported) return e;

@@ -1028,11 +1028,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     a.xhalf = xa->half;
     a.xerr = xa->err;
   }
-  static const int place = [] {
-    const char* e = getenv("HIPDSML_PK_PLACE");  // 0: the old map (A/B only)
-    return e ? atoi(e) : 1;
-  }();
-  a.place = place;
+  a.place = 1;
   const size_t lds = (size_t)kLdsFloats * sizeof(float);
   static bool attr = false;
   if (!attr) {

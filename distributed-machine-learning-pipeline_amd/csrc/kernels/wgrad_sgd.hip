@@ -252,34 +252,6 @@ __device__ __forceinline__ void wg_pick(const WgMulti& m, int b, WgArgs& a, int&
   nt = t / kts;
 }
 
-// roofline probes (variant 20 / 21): the tile kernel without operand staging
-// and MFMAs, and a plain grid-stride stream of the same bytes (W fp32 RMW +
-// bf16 copy)
-__global__ __launch_bounds__(256) void wgrad_nomma_k(WgMulti m) {
-  __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
-  WgArgs a;
-  int kt, nt;
-  wg_pick(m, blockIdx.x, a, kt, nt);
-  a.M = 0;
-  wgrad_tile(a, kt, nt, lds);
-}
-
-__global__ __launch_bounds__(256) void wgrad_stream_k(WgMulti m) {
-  for (int j = 0; j < m.n; ++j) {
-    const WgArgs a = m.l[j];
-    const int64_t n4 = (int64_t)a.N * a.K / 4;
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-      const int64_t e = 4 * i, r = e / a.K, c = e % a.K;
-      float4 v = *reinterpret_cast<const float4*>(a.W + r * a.ldw + c);
-      v.x -= a.lr; v.y -= a.lr; v.z -= a.lr; v.w -= a.lr;
-      __builtin_nontemporal_store(wg_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<wg_f4*>(a.W + r * a.ldw + c));
-      const uint32_t lo = f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
-      const uint32_t hi = f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
-      __builtin_nontemporal_store(wg_u2{lo, hi}, reinterpret_cast<wg_u2*>(a.Wb + r * a.ldwb + c));
-    }
-  }
-}
-
 bool wg_valid(const WgArgs& a) {
   if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
       a.ldz < ((a.N + 7) & ~7) || a.ldx < ((a.K + 7) & ~7) || (((uintptr_t)a.Z | (uintptr_t)a.X) & 15))
@@ -302,7 +274,7 @@ hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t 
   return hipGetLastError();
 }
 
-hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int variant, int grid) {
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s) {
   if (n < 1 || n > kWgMaxLayers) return hipErrorInvalidValue;
   WgMulti m{};
   m.n = n;
@@ -316,13 +288,7 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int vari
   }
   for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
   for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
-  if (variant == 20) {
-    hipLaunchKernelGGL(wgrad_nomma_k, dim3(t), dim3(256), 0, s, m);
-  } else if (variant == 21) {
-    hipLaunchKernelGGL(wgrad_stream_k, dim3(grid > 0 ? grid : 8192), dim3(256), 0, s, m);
-  } else {
-    hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
-  }
+  hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
   return hipGetLastError();
 }
 

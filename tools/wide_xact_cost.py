@@ -23,7 +23,7 @@ Wb = [torch.zeros(pd[l + 1], pd[l], dtype=torch.bfloat16, device=dev) for l in r
 bias = [torch.zeros(d[l + 1], device=dev) for l in range(3)]
 
 
-def timed(n, variant=0, reps=30):
+def timed(n, reps=30):
     M = B * n
     g = torch.Generator(device=dev).manual_seed(n)
     H = [torch.randn(M, pd[l], device=dev, generator=g).to(torch.bfloat16) for l in range(3)]
@@ -31,12 +31,12 @@ def timed(n, variant=0, reps=30):
     layers = [(Z[l], H[l], M, d[l + 1], d[l], 1.0 / n, 1e-6, W[l], Wb[l], None, bias[l], None)
               for l in range(2, -1, -1)]
     for _ in range(3):
-        C.wgrad_sgd_multi(layers, variant)
+        C.wgrad_sgd_multi(layers)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(reps):
-        C.wgrad_sgd_multi(layers, variant)
+        C.wgrad_sgd_multi(layers)
     e1.record()
     torch.cuda.synchronize()
     return round(1e3 * e0.elapsed_time(e1) / reps, 2)
