@@ -72,7 +72,7 @@ def _launch(a, argv, script: str = "") -> int:
 
 
 def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200,
-                         ring_chunk: int = 1 << 20) -> dict:
+                         ring_chunk: int = 0) -> dict:
     """Device all-reduce latency (µs, max over ranks) of a `nbytes` fp32 buffer
     across the job's GPUs: RCCL's ncclAllReduce ("rccl"), the in-house ring on
     ncclSend/ncclRecv over every directed Hamiltonian ring ("ring") and over a
@@ -83,8 +83,17 @@ def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200,
 
     from hipdsml.parallel.xchg import ExchangeUnavailable, XgmiAllReduce, reset_group
 
-    out = {"bytes": nbytes, "ring_chunk_bytes": ring_chunk}
     t = torch.zeros(nbytes // 4, device=ctx.device)
+    sweep = None
+    if comm is not None and ring_chunk <= 0:  # the in-house ring's chunk, tuned at this size
+        from hipdsml.parallel.ring_tune import tune_ring_chunk
+
+        try:
+            res = tune_ring_chunk(ctx, comm, t)
+            ring_chunk, sweep = int(res["best"]), res["sweep_us"]
+        except Exception as e:  # noqa: BLE001
+            ring_chunk, sweep = 1 << 20, {"error": str(e)[:200]}
+    out = {"bytes": nbytes, "ring_chunk_bytes": ring_chunk, "ring_chunk_sweep_us": sweep}
 
     def timed(name, fn, err=lambda: False):
         ok = 1.0
@@ -162,7 +171,7 @@ def run(a) -> int:
     spec = MlpSpec.parse(a.model)
     ds = synthetic_mnist(a.samples_per_rank, seed=1000 + ctx.rank, dim=spec.dims[0])
     tr = MlpTrainer(spec, ds, batch=a.batch, lr=a.lr, ctx=ctx, seed=0, sync=a.sync,
-                    graph_steps=a.graph_steps,
+                    graph_steps=a.graph_steps, ring_chunk_bytes=a.ring_chunk,
                     auto_fallback="torch" if a.rehearse_one_gpu else "rccl")
     n = ctx.world_size
     sync_us = None
@@ -236,6 +245,8 @@ def run(a) -> int:
             "rehearsal": rehearsal,
             "device": ctx.device.type,
             "sync_us_per_step": sync_us,
+            "ring_chunk_bytes": tr._ring_chunk if tr.comm is not None else None,
+            "ring_chunk_sweep_us": tr.ring_chunk_sweep_us if tr.backend == "hip" else None,
             "allreduce_1MiB_us": ar_us,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
@@ -270,8 +281,9 @@ def main(argv=None) -> int:
     ap.add_argument("--graph-steps", type=int, default=50,
                     help="steps captured per hipGraph (0 = eager C++ launch loop); RCCL "
                          "collectives are captured with the kernels")
-    ap.add_argument("--ring-chunk", type=int, default=1 << 20,
-                    help="chunk bytes of the in-house ring all-reduce")
+    ap.add_argument("--ring-chunk", type=int, default=0,
+                    help="chunk bytes of the in-house ring all-reduce (0: swept at init on the "
+                         "gradient and on the 1 MiB probe, the fastest kept)")
     ap.add_argument("--samples-per-rank", type=int, default=60032)
     ap.add_argument("--no-allreduce-probe", action="store_true",
                     help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")

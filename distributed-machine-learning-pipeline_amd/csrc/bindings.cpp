@@ -275,6 +275,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     hip_ok(reduce_into(dst.data_ptr(), a.data_ptr(), b.data_ptr(), dst.numel(), dtype_of(dst), op,
                        cur_stream()), "reduce_into");
   });
+  m.def("reduce_multi_", [](const std::vector<torch::Tensor>& dsts, const std::vector<torch::Tensor>& srcs,
+                             int op) {
+    TORCH_CHECK(dsts.size() == srcs.size() && !dsts.empty() && dsts.size() <= (size_t)kMaxReduceSegs,
+                "reduce_multi_: 1..", kMaxReduceSegs, " (dst, src) pairs");
+    ReduceSegs m{};
+    const int32_t dt = dtype_of(dsts[0]);
+    for (size_t k = 0; k < dsts.size(); ++k) {
+      TORCH_CHECK(dsts[k].is_cuda() && srcs[k].is_cuda() && dsts[k].is_contiguous() &&
+                  srcs[k].is_contiguous() && dsts[k].numel() == srcs[k].numel() &&
+                  dtype_of(dsts[k]) == dt && dtype_of(srcs[k]) == dt, "reduce_multi_: pair ", k);
+      m.seg[m.count++] = ReduceSeg{dsts[k].data_ptr(), srcs[k].data_ptr(), dsts[k].numel()};
+    }
+    hip_ok(reduce_multi_inplace(m, dt, op, cur_stream()), "reduce_multi_inplace");
+  });
   m.def("scale_", [](torch::Tensor x, double alpha) {
     check_cuda(x, "x");
     hip_ok(scale_inplace(x.data_ptr(), x.numel(), dtype_of(x), (float)alpha, cur_stream()),
@@ -624,7 +638,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("mlp_persist_xbuf_granules", []() { return mlp_persist_xbuf_granules(); });
   m.def("mlp_persist_stamps", []() {
-    std::vector<uint64_t> v(3 * 8 * 8);
+    std::vector<uint64_t> v(4 * 8 * 8);
     hip_ok(mlp_persist_read_stamps(v.data()), "mlp_persist_read_stamps");
     return v;
   });

@@ -84,13 +84,14 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
                          hipStream_t s);
 
 // ---- persistent fused step (kernels/mlp_persist.hip) -------------------------
-// One launch runs `steps` SGD steps of the 784-128-64-10 MLP at batch 64 with
-// the weights resident on chip (36 workgroups: 32 layer-1 tiles + 4 row
-// chains, tagged-granule hand-offs).  `xb` holds mlp_persist_xbuf_granules()
+// One launch runs `steps` SGD steps of the 784-128-64-10 or 784-128-10 MLP at
+// batch <= 64 with the weights resident on chip (64 workgroups: 56 layer-1
+// tiles, 4 row chains, 4 upper-layer gradient blocks; flag / tagged-granule
+// hand-offs).  `xb` holds mlp_persist_xbuf_granules()
 // uint64 granules, zeroed whenever the step counter is rewound; `err` is set
 // when a hand-off timed out (the launch then ends early).
 bool mlp_persist_supported(const MlpDesc& d);
-hipError_t mlp_persist_read_stamps(uint64_t* host_out);  // [3][8][8] (role, step, phase)
+hipError_t mlp_persist_read_stamps(uint64_t* host_out);  // [4][8][8] (role, step, phase)
 void mlp_persist_set_stamping(bool on);
 int64_t mlp_persist_xbuf_granules();
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
@@ -172,6 +173,19 @@ hipError_t sgd_momentum_f32(float* P, const float* G, float* V, int64_t n, float
 // dst = op(dst, src) elementwise; n in elements.
 hipError_t reduce_inplace(void* dst, const void* src, int64_t n, int32_t dtype, int32_t op,
                           hipStream_t s);
+// Up to kMaxReduceSegs in-place reductions dst_k = op(dst_k, src_k) in ONE
+// launch (the in-house ring reduces every directed ring's segment of a step).
+constexpr int kMaxReduceSegs = 8;
+struct ReduceSeg {
+  void* dst;
+  const void* src;
+  int64_t n;  // elements
+};
+struct ReduceSegs {
+  ReduceSeg seg[kMaxReduceSegs];
+  int32_t count;
+};
+hipError_t reduce_multi_inplace(const ReduceSegs& m, int32_t dtype, int32_t op, hipStream_t s);
 // dst = op(a, b)
 hipError_t reduce_into(void* dst, const void* a, const void* b, int64_t n, int32_t dtype,
                        int32_t op, hipStream_t s);

@@ -227,6 +227,81 @@ hipError_t reduce_inplace(void* dst, const void* src, int64_t n, int32_t dtype, 
   return reduce_into(dst, dst, src, n, dtype, op, s);
 }
 
+// ---- several in-place reductions in ONE launch (the in-house ring's step:
+// one receive segment per directed ring, all reduced by a single kernel
+// instead of one launch per ring).  blockIdx.y picks the segment; 16-B vector
+// body when both of its pointers are 16-B aligned, element tail otherwise.
+template <int OP, int DT>
+__device__ __forceinline__ void red_elem(void* dst, const void* src, int64_t e) {
+  if constexpr (DT == kF32) {
+    float* d = static_cast<float*>(dst);
+    d[e] = rop<OP>(d[e], static_cast<const float*>(src)[e]);
+  } else if constexpr (DT == kBF16 || DT == kF16) {
+    uint16_t* d = static_cast<uint16_t*>(dst);
+    d[e] = f2h<OP, DT == kBF16>(rop<OP>(h2f<OP, DT == kBF16>(d[e]),
+                                        h2f<OP, DT == kBF16>(static_cast<const uint16_t*>(src)[e])));
+  } else if constexpr (DT == kU8) {
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    d[e] = ropu8<OP>(d[e], static_cast<const uint8_t*>(src)[e]);
+  } else {
+    int32_t* d = static_cast<int32_t*>(dst);
+    d[e] = ropi<OP>(d[e], static_cast<const int32_t*>(src)[e]);
+  }
+}
+template <int DT>
+constexpr int dt_size() { return DT == kU8 ? 1 : (DT == kBF16 || DT == kF16) ? 2 : 4; }
+
+template <int OP, int DT>
+__global__ __launch_bounds__(256) void reduce_multi_k(ReduceSegs m) {
+  const ReduceSeg sg = m.seg[blockIdx.y];
+  constexpr int per = 16 / dt_size<DT>();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool vec = ((((uintptr_t)sg.dst) | ((uintptr_t)sg.src)) & 15) == 0;
+  const int64_t nv = vec ? sg.n / per : 0;
+  uint4* d4 = static_cast<uint4*>(sg.dst);
+  const uint4* s4 = static_cast<const uint4*>(sg.src);
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    uint4 x = d4[v];
+    const uint4 y = s4[v];
+#pragma unroll
+    for (int j = 0; j < per; ++j) red_elem<OP, DT>(&x, &y, j);
+    d4[v] = x;
+  }
+  for (int64_t e = nv * per + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < sg.n; e += stride)
+    red_elem<OP, DT>(sg.dst, sg.src, e);
+}
+
+template <int OP>
+static hipError_t launch_reduce_multi(const ReduceSegs& m, int32_t dtype, int64_t nmax, hipStream_t s) {
+  const int esz = dtype == kU8 ? 1 : (dtype == kBF16 || dtype == kF16) ? 2 : 4;
+  int gx = grid_for((nmax * esz + 15) / 16);
+  gx = (gx + m.count - 1) / m.count;  // ~ the same total blocks as one launch of the largest
+  const dim3 grid(gx, m.count);
+  switch (dtype) {
+    case kF32: hipLaunchKernelGGL((reduce_multi_k<OP, kF32>), grid, dim3(256), 0, s, m); break;
+    case kBF16: hipLaunchKernelGGL((reduce_multi_k<OP, kBF16>), grid, dim3(256), 0, s, m); break;
+    case kF16: hipLaunchKernelGGL((reduce_multi_k<OP, kF16>), grid, dim3(256), 0, s, m); break;
+    case kU8: hipLaunchKernelGGL((reduce_multi_k<OP, kU8>), grid, dim3(256), 0, s, m); break;
+    case kI32: hipLaunchKernelGGL((reduce_multi_k<OP, kI32>), grid, dim3(256), 0, s, m); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t reduce_multi_inplace(const ReduceSegs& m, int32_t dtype, int32_t op, hipStream_t s) {
+  if (m.count < 1 || m.count > kMaxReduceSegs) return hipErrorInvalidValue;
+  int64_t nmax = 0;
+  for (int k = 0; k < m.count; ++k) nmax = m.seg[k].n > nmax ? m.seg[k].n : nmax;
+  if (nmax <= 0) return hipSuccess;
+  switch (op) {
+    case kSum: return launch_reduce_multi<kSum>(m, dtype, nmax, s);
+    case kProd: return launch_reduce_multi<kProd>(m, dtype, nmax, s);
+    case kMin: return launch_reduce_multi<kMin>(m, dtype, nmax, s);
+    case kMax: return launch_reduce_multi<kMax>(m, dtype, nmax, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // ---- scale / conversions -----------------------------------------------------
 __global__ __launch_bounds__(256) void scale_f32_k(float* x, int64_t n, float alpha) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

@@ -173,10 +173,17 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
       }
     }
     check(ncclGroupEnd(), "ncclGroupEnd");
-    for (const auto& x : g)
-      if (x.reduce && x.recv_len > 0)
-        DSML_HIP_CHECK(reduce_inplace(b + x.recv_off * es, tmp + slot * x.ring, x.recv_len, dtype,
-                                      op, s));
+    // every ring's received segment of this step reduced by ONE launch
+    ReduceSegs m{};
+    for (const auto& x : g) {
+      if (!x.reduce || x.recv_len <= 0) continue;
+      if (m.count == kMaxReduceSegs) {
+        DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, s));
+        m.count = 0;
+      }
+      m.seg[m.count++] = ReduceSeg{b + x.recv_off * es, tmp + slot * x.ring, x.recv_len};
+    }
+    if (m.count > 0) DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, s));
   }
 }
 
@@ -350,7 +357,8 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
     return;
   }
   if (!mlp_persist_supported(d_))
-    throw std::invalid_argument("set_persist: the persistent step covers 784-128-64-10 at batch 64");
+    throw std::invalid_argument("set_persist: the persistent step covers 784-128-64-10 and "
+                                "784-128-10 at batch <= 64");
   if (mom_ != 0.f || wd_ != 0.f) throw std::invalid_argument("set_persist: plain SGD only");
   if (x != nullptr) {
     const int n = x->nranks();

@@ -68,7 +68,7 @@ class MlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "reference",
                  momentum: float = 0.0, weight_decay: float = 0.0, sync: str = "rccl",
-                 ring_chunk_bytes: int = 1 << 20, graph_steps: int = 0,
+                 ring_chunk_bytes: int = 0, graph_steps: int = 0,
                  params: Optional[torch.Tensor] = None, external_comm=None,
                  capture_collectives: Optional[bool] = None, xchg_timeout_ms: float = 10000.0,
                  xact_waves: int = 0, auto_fallback: str = "rccl",
@@ -131,7 +131,7 @@ class MlpTrainer:
         # torch's current stream at every call (no cross-stream edges per step)
         self._stream = stream
         # persistent fused step (kernels/mlp_persist.hip): None = when supported
-        # (single replica, plain SGD, 784-128-64-10 @ 64); HIPDSML_PERSIST=0 disables
+        # (plain SGD, 784-128-64-10 or 784-128-10 at batch <= 64); HIPDSML_PERSIST=0 disables
         if persist is None:
             import os
 
@@ -164,7 +164,9 @@ class MlpTrainer:
                                   stream=self._stream.cuda_stream if self._stream is not None else 0,
                                   follow_torch=self._stream is None)
         self.runner.set_world_size(self.ctx.world_size)
+        # chunk of the in-house ring all-reduce; <= 0: tuned at init (N > 1)
         self._ring_chunk = int(ring_chunk_bytes)
+        self.ring_chunk_sweep_us: Optional[Dict[str, float]] = None
         # sync modes whose collectives have run one eager step (RCCL connects a
         # peer pair on its first send/recv, which must never happen inside a
         # graph capture): 'rccl' warms ncclAllReduce's connections, 'ring' the
@@ -191,9 +193,20 @@ class MlpTrainer:
         elif self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
             if self.comm is None:
                 self.comm = make_native_comm(self.ctx)
-                # the in-house ring's scratch, sized once (never inside a graph capture)
-                self.comm.reserve_ring(self.layout.nparams, self._ring_chunk)
-            self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, ring_chunk_bytes)
+            if self._ring_chunk <= 0:
+                if self.sync in ("auto", "ring") and self.ctx.backend != "none":
+                    # measured, not guessed: every distinct chunk timed on the
+                    # gradient itself, max over ranks (parallel/ring_tune.py)
+                    from ..parallel.ring_tune import tune_ring_chunk
+
+                    res = tune_ring_chunk(self.ctx, self.comm, self.G)
+                    self._ring_chunk = int(res["best"])
+                    self.ring_chunk_sweep_us = res["sweep_us"]
+                else:
+                    self._ring_chunk = 1 << 20
+            # the in-house ring's scratch, sized once (never inside a graph capture)
+            self.comm.reserve_ring(self.layout.nparams, self._ring_chunk)
+            self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, self._ring_chunk)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
         if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain and _xgmi_eligible(
                 self.ctx, need_nccl=not torch_fallback)):
@@ -265,7 +278,8 @@ class MlpTrainer:
             if mode == "pk":
                 C = self.runner_module()
                 if not (self._want_persist and C.mlp_persist_supported(self.layout.desc_list())):
-                    raise X.ExchangeUnavailable("the persistent step covers 784-128-64-10 at batch 64")
+                    raise X.ExchangeUnavailable("the persistent step covers 784-128-64-10 and "
+                                                "784-128-10 at batch <= 64")
                 half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size)
                 x = X.make_exchange(self.ctx, half, ntiles, self.xchg_timeout_ms)
                 if self.pk_buf is None:

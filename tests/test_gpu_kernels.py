@@ -160,6 +160,35 @@ def test_reduce_kernels(dtype, op):
         assert torch.equal(out.cpu(), want)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.uint8, torch.int32])
+@pytest.mark.parametrize("op", ["sum", "max"])
+def test_reduce_multi_matches_per_segment_reduce(dtype, op):
+    """The ring step's merged reduce: up to 8 (dst, src) segments of mixed
+    sizes and alignments in ONE launch == the single-segment kernel on each."""
+    C = require_native()
+    opc = {"sum": 0, "prod": 1, "min": 2, "max": 3}[op]
+    g = torch.Generator().manual_seed(1)
+    sizes, offs = (4099, 17, 65536, 1, 3000, 8, 257, 12345), (0, 1, 4, 3, 0, 2, 5, 7)
+    base_d, base_s, dsts, srcs = [], [], [], []
+    for n, o in zip(sizes, offs):
+        if dtype in (torch.uint8, torch.int32):
+            a = torch.randint(0, 100, (n + o,), generator=g).to(dtype)
+            b = torch.randint(0, 100, (n + o,), generator=g).to(dtype)
+        else:
+            a, b = torch.randn(n + o, generator=g).to(dtype), torch.randn(n + o, generator=g).to(dtype)
+        base_d.append(a.to(DEV))
+        base_s.append(b.to(DEV))
+        dsts.append(base_d[-1][o:])  # odd offsets: the element path
+        srcs.append(base_s[-1][o:])
+    want = [d.clone() for d in dsts]
+    for w, s in zip(want, srcs):
+        C.reduce_into(w, w, s, opc)
+    C.reduce_multi_(dsts, srcs, opc)
+    torch.cuda.synchronize()
+    for d, w in zip(dsts, want):
+        assert torch.equal(d, w)
+
+
 def test_sgd_and_conversion_kernels():
     P = torch.randn(1003, device=DEV)
     G = torch.randn(1003, device=DEV)

@@ -1,7 +1,9 @@
-"""Persistent fused step (kernels/mlp_persist.hip): S SGD steps of the
-flagship MLP 784-128-64-10 per launch, weights resident on chip, tagged-granule
-hand-offs between 32 layer-1 blocks and 4 row-chain blocks.  Checked against
-the fp32 torch reference (models/mlp.py grads_ref) and the three-launch path."""
+"""Persistent fused step (kernels/mlp_persist.hip): S SGD steps per launch,
+weights resident on chip, flag / tagged-granule hand-offs between 56
+layer-1 blocks, 4 row chains and 4 upper-layer gradient blocks.  Covers the
+BASELINE model 784-128-64-10 and the reference client's own 784-128-10
+(client.go:22-33), at batch 64 and below.  Checked against the fp32 torch
+reference (models/mlp.py grads_ref) and the three-launch path."""
 import pytest
 import torch
 
@@ -13,50 +15,59 @@ from hipdsml.parallel.dist import DistContext
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 SPEC = MlpSpec((784, 128, 64, 10))
+REF_SPEC = MlpSpec((784, 128, 10))  # the model client.go codes
 
 
-def _tr(ds, persist, lr=0.05, seed=3):
-    return MlpTrainer(SPEC, ds, batch=64, lr=lr, ctx=DistContext(device=DEV), seed=seed,
+def _tr(ds, persist, lr=0.05, seed=3, spec=SPEC, batch=64):
+    return MlpTrainer(spec, ds, batch=batch, lr=lr, ctx=DistContext(device=DEV), seed=seed,
                       persist=persist)
 
 
-def _ref(ds, steps, lr=0.05, seed=3):
-    nb = len(ds) // 64
-    lay = MlpLayout(SPEC, 64, nb)
+def _ref(ds, steps, lr=0.05, seed=3, spec=SPEC, batch=64):
+    nb = len(ds) // batch
+    lay = MlpLayout(spec, batch, nb)
     P = init_params(lay, seed, "reference")
     loss = 0.0
     for s in range(steps):
         b = s % nb
-        g, ls, _ = grads_ref(lay, P, ds.X[b * 64:(b + 1) * 64], ds.y[b * 64:(b + 1) * 64])
+        g, ls, _ = grads_ref(lay, P, ds.X[b * batch:(b + 1) * batch], ds.y[b * batch:(b + 1) * batch])
         loss += float(ls)
         P = P - lr * g
     return P, loss
 
 
-def test_persistent_step_is_active_for_the_flagship():
-    t = _tr(synthetic_mnist(64 * 4, seed=1), None)
+@pytest.mark.parametrize("spec", [SPEC, REF_SPEC], ids=str)
+def test_persistent_step_is_active_for_both_models(spec):
+    t = _tr(synthetic_mnist(64 * 4, seed=1), None, spec=spec)
     assert t.persistent and t.runner.persist_active()
-    assert not _tr(synthetic_mnist(64 * 4, seed=1), False).persistent
+    assert not _tr(synthetic_mnist(64 * 4, seed=1), False, spec=spec).persistent
+    # outside the family: the three-launch path
+    assert not _tr(synthetic_mnist(64 * 4, seed=1), None, spec=MlpSpec((784, 96, 10))).persistent
 
 
-@pytest.mark.parametrize("steps", [1, 2, 9])
-def test_persistent_matches_fp32_reference(steps):
-    ds = synthetic_mnist(64 * 4, seed=11)
-    t = _tr(ds, True)
+@pytest.mark.parametrize("spec,batch,steps", [(SPEC, 64, 1), (SPEC, 64, 2), (SPEC, 64, 9),
+                                              (REF_SPEC, 64, 1), (REF_SPEC, 64, 9),
+                                              (SPEC, 32, 7), (REF_SPEC, 48, 7), (SPEC, 1, 3)],
+                         ids=lambda v: str(v))
+def test_persistent_matches_fp32_reference(spec, batch, steps):
+    ds = synthetic_mnist(batch * 4, seed=11)
+    t = _tr(ds, True, spec=spec, batch=batch)
+    assert t.persistent
     t.train_steps(steps)
     t.synchronize()
-    want, loss = _ref(ds, steps)
+    want, loss = _ref(ds, steps, spec=spec, batch=batch)
     err = (t.P.cpu() - want).abs().max().item()
     assert err < 2e-5, err
     st = t.read_stats()
-    assert st.count == 64 * steps
+    assert st.count == batch * steps
     assert abs(st.loss_sum - loss) < 1e-3 * max(1.0, loss)
     assert int(t.ctr[0].item()) == steps and int(t.ctr[1].item()) == steps
 
 
-def test_persistent_launch_split_is_bit_exact_and_matches_three_launch_path():
+@pytest.mark.parametrize("spec", [SPEC, REF_SPEC], ids=str)
+def test_persistent_launch_split_is_bit_exact_and_matches_three_launch_path(spec):
     ds = synthetic_mnist(64 * 5, seed=12)
-    a, b, c = _tr(ds, True), _tr(ds, True), _tr(ds, False)
+    a, b, c = _tr(ds, True, spec=spec), _tr(ds, True, spec=spec), _tr(ds, False, spec=spec)
     a.train_steps(23)
     for n in (7, 1, 15):  # epoch wrap-around inside and across launches
         b.train_steps(n)

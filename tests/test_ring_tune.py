@@ -1,0 +1,74 @@
+"""Chunk tuning of the in-house multi-ring all-reduce (parallel/ring_tune.py):
+the selection logic against a fake communicator whose calls advance a fake
+clock by a latency + bandwidth cost model of the ring schedule, and the
+candidate pruning against the schedule's own rounds (ring_plan.h)."""
+import pytest
+
+from hipdsml.parallel import ring_tune as rt
+
+
+class FakeComm:
+    """ring_allreduce_ costs (2(n-1) steps) x rounds x (alpha + beta x bytes per round)."""
+
+    def __init__(self, clock, n, rings, alpha_us, gbps):
+        self.clock, self.n, self.rings = clock, n, rings
+        self.alpha, self.gbps = alpha_us, gbps
+        self.calls = []
+
+    def cost_us(self, nbytes, chunk):
+        r = rt.effective_rounds(nbytes, self.n, self.rings, chunk)
+        per_round = min(chunk, -(-nbytes // (self.rings * self.n)))
+        return 2 * (self.n - 1) * r * (self.alpha + per_round / (self.gbps * 1e3))
+
+    def ring_allreduce_(self, nbytes, chunk):
+        self.calls.append(chunk)
+        self.clock.t += self.cost_us(nbytes, chunk) * 1e-6
+
+
+class Clock:
+    t = 0.0
+
+    def __call__(self):
+        return self.t
+
+
+@pytest.mark.parametrize("nbytes,alpha,gbps", [(437_544, 8.0, 50.0), (1 << 20, 2.0, 5.0),
+                                               (80 << 20, 8.0, 50.0), (80 << 20, 0.5, 400.0)])
+def test_sweep_picks_the_cost_models_fastest_chunk(nbytes, alpha, gbps):
+    clock = Clock()
+    comm = FakeComm(clock, n=8, rings=6, alpha_us=alpha, gbps=gbps)
+    cands = rt.distinct_chunks(nbytes, 8, 6)
+    times = rt.sweep(lambda c: comm.ring_allreduce_(nbytes, c), lambda: None, cands, iters=5,
+                     warmup=1, clock=clock)
+    best = rt.pick_chunk(times)
+    model = {c: comm.cost_us(nbytes, c) for c in cands}
+    fastest = min(model.values())
+    assert model[best] <= fastest * 1.02
+    assert set(comm.calls) == set(cands)
+
+
+def test_distinct_chunks_drop_chunks_past_the_segment():
+    # 437,544 B over 6 rings x 8 ranks: ~9.1 KB segments -> every chunk >= that is one round
+    cands = rt.distinct_chunks(437_544, 8, 6)
+    assert cands == [64 << 10]
+    big = rt.distinct_chunks(80 << 20, 8, 6)
+    assert big == sorted(big) and len(big) == len(set(rt.effective_rounds(80 << 20, 8, 6, c)
+                                                       for c in big))
+    assert len(big) >= 5
+
+
+def test_pick_prefers_larger_chunk_within_tolerance():
+    assert rt.pick_chunk({65536: 100.0, 131072: 101.0, 262144: 150.0}) == 131072
+    assert rt.pick_chunk({65536: 100.0, 131072: 110.0}) == 65536
+    with pytest.raises(ValueError):
+        rt.pick_chunk({})
+
+
+def test_rounds_match_the_native_schedule():
+    """effective_rounds mirrors ring_plan.h: the native schedule has
+    2(n-1) x rounds groups (built without a GPU)."""
+    C = pytest.importorskip("hipdsml.ops.native").require_native()
+    for nbytes, chunk in ((437_544, 16384), (1 << 20, 4096), (80 << 20, 1 << 20)):
+        count = nbytes // 4
+        plan = C.ring_schedule(8, 3, count, 4, chunk // 4, 0)
+        assert len(plan) == 2 * 7 * rt.effective_rounds(nbytes, 8, 6, chunk)
