@@ -728,7 +728,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"), py::arg("waves") = 0,
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def("set_persist", [](PyMlpRunner& s, c10::optional<torch::Tensor> xbuf,
-                             c10::optional<torch::Tensor> err, double timeout_ms, PeerExchange* x) {
+                             c10::optional<torch::Tensor> err, double timeout_ms, PeerExchange* x,
+                             int algo) {
         if (!xbuf) { s.r->set_persist(nullptr, nullptr, 0.0); return; }
         check_cuda(*xbuf, "xbuf");
         TORCH_CHECK(xbuf->scalar_type() == torch::kInt64 &&
@@ -739,11 +740,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         s.keep.push_back(*xbuf);
         s.keep.push_back(*err);
         s.r->set_persist(reinterpret_cast<uint64_t*>(xbuf->data_ptr<int64_t>()),
-                         reinterpret_cast<uint32_t*>(err->data_ptr<int32_t>()), timeout_ms, x);
+                         reinterpret_cast<uint32_t*>(err->data_ptr<int32_t>()), timeout_ms, x, algo);
       }, py::arg("xbuf").none(true), py::arg("err") = py::none(), py::arg("timeout_ms") = 2000.0,
-         py::arg("exchange") = nullptr, py::keep_alive<1, 5>())
-      .def_static("persist_xchg_size", [](int n) { return py::make_tuple(px_half(n), px_ntiles(n)); },
-                  "(half_floats, ntiles) of the persistent step's replica exchange at n ranks")
+         py::arg("exchange") = nullptr, py::arg("algo") = 0, py::keep_alive<1, 5>())
+      .def_static("persist_xchg_size", [](int n, int algo) {
+        return py::make_tuple(px_half(n, algo), px_ntiles(n, algo)); }, py::arg("n"), py::arg("algo") = 0,
+                  "(half_floats, ntiles) of the persistent step's replica exchange at n ranks "
+                  "(algo 0: one-shot, 1: two-shot)")
       .def("persist_active", [](PyMlpRunner& s) { return s.r->persist_active(); })
       .def("persist_failed", [](PyMlpRunner& s) { return s.r->persist_failed(); },
            "a persistent launch gave up on a hand-off (valid after a sync; no device copy)")

@@ -98,12 +98,13 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
                              hipStream_t s, const struct XchgArgs* xa = nullptr,
-                             const struct XchgTab* tab = nullptr);
+                             const struct XchgTab* tab = nullptr, int algo = 0);
 // Data-parallel form (xa->nranks > 1): the receive buffers / flags each replica
-// needs (PeerExchange half >= px_half(n), ntiles >= px_ntiles(n)); lr is passed
-// as lr / n.
-int64_t px_half(int n);
-int px_ntiles(int n);
+// needs (PeerExchange half >= px_half(n, algo), ntiles >= px_ntiles(n, algo));
+// lr is passed as lr / n.  algo 0: one-shot sum (sync 'pk'), 1: two-shot
+// reduce-scatter + all-gather per wave slot (sync 'pk2').
+int64_t px_half(int n, int algo = 0);
+int px_ntiles(int n, int algo = 0);
 
 // ---- peer exchange: gradient all-reduce fused into K_C over xGMI -------------
 // Every replica's K_C publishes each weight-gradient tile into its own

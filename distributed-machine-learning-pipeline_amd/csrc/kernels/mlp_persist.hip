@@ -290,6 +290,7 @@ struct PersistArgs {
   // already lr / nrep.
   XchgTab xt;
   int32_t nrep, rep;
+  int32_t algo;    // 0: one-shot (every slot to every peer), 1: two-shot (reduce-scatter + all-gather)
   int64_t xhalf;   // floats per parity half of a receive buffer (>= px_half)
   uint32_t* xerr;  // the exchange's error word (a peer that did not arrive)
 };
@@ -298,8 +299,10 @@ struct PersistArgs {
 // slots 0..223 = layer-1 block lb, wave w at 4 lb + w, slots 224..239 =
 // gradient block g, wave w at 224 + 4 g + w.  Flags [src][slot].
 constexpr int kPxSlot = 64 * 16, kPxSlots = kNL1 * 4 + kNG * 4;
-int64_t px_half(int n) { return (int64_t)n * kPxSlots * kPxSlot; }
-int px_ntiles(int n) { return n * kPxSlots; }
+// Two-shot adds an all-gather region [slot][64 lanes][16 floats] per parity
+// half and its flags [owner][slot].
+int64_t px_half(int n, int algo) { return (int64_t)(n + (algo ? 1 : 0)) * kPxSlots * kPxSlot; }
+int px_ntiles(int n, int algo) { return (algo ? 2 : 1) * n * kPxSlots; }
 
 // One wave's slot: push v into every peer, raise their flags, wait for every
 // peer's slot of step s here, then v = the rank-ordered sum over all
@@ -347,6 +350,95 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = acc[j];
   return true;
+}
+
+// Two-shot form of the same sum (sync 'pk2'): lane l's values are owned by
+// replica l % n.  Reduce-scatter: each lane sends its values to their owner
+// only; the owner sums all n in rank order.  All-gather: the owner sends the
+// sum to every peer.  Per wave and step 2 (n-1)/n of the slot leaves each
+// replica instead of (n-1) slots (n = 8: 4x fewer bytes per link), for one
+// more flag round trip.  Every replica ends with the owner's bits.
+template <int NV>
+__device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
+                                                   int slot) {
+  const int lane = threadIdx.x & 63;
+  const int n = a.nrep, me = a.rep;
+  const int own = lane % n;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const int64_t per_src = (int64_t)kPxSlots * kPxSlot;
+  const int64_t ag = (int64_t)n * per_src;  // all-gather region of a parity half
+  const uint64_t tag = s + 1;
+  // ---- reduce-scatter: values to their owner ----
+  for (int d = 0; d < n; ++d) {
+    if (d == me) continue;
+    const __amdgpu_buffer_rsrc_t r =
+        rsrc(a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)me * per_src);
+    if (own == d) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) px_st4(r, (lane * 16 + 4 * j) * 4, v[j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // system-scope release (common.h)
+  if (lane == 0)
+    for (int d = 0; d < n; ++d)
+      if (d != me)
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + me * kPxSlots), tag,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = true;
+  if (lane < n && lane != me)
+    ok = poll_flag_ge<1>(a.xt.flags[me] + slot + lane * kPxSlots, tag, a.xerr, a.timeout_ticks);
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  asm volatile("" ::: "memory");
+  if (!ok) return false;
+  if (own == me) {
+    const float* mine = a.xt.buf[me] + poff + (int64_t)slot * kPxSlot;
+    float4 acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int src = 0; src < n; ++src) {
+      const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float4 x = src == me ? v[j] : px_ld4(r, (lane * 16 + 4 * j) * 4);
+        acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = acc[j];
+  }
+  // ---- all-gather: the owner's sums to every peer ----
+  for (int d = 0; d < n; ++d) {
+    if (d == me) continue;
+    const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[d] + poff + ag + (int64_t)slot * kPxSlot);
+    if (own == me) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) px_st4(r, (lane * 16 + 4 * j) * 4, v[j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    for (int d = 0; d < n; ++d)
+      if (d != me)
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + n * kPxSlots + me * kPxSlots + slot), tag,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  ok = true;
+  if (lane < n && lane != me)
+    ok = poll_flag_ge<1>(a.xt.flags[me] + n * kPxSlots + lane * kPxSlots + slot, tag, a.xerr,
+                         a.timeout_ticks);
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  asm volatile("" ::: "memory");
+  if (!ok) return false;
+  if (own != me) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[me] + poff + ag + (int64_t)slot * kPxSlot);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = px_ld4(r, (lane * 16 + 4 * j) * 4);
+  }
+  return true;
+}
+
+template <int NV>
+__device__ __forceinline__ bool px_sum_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV], int slot) {
+  return a.algo ? px_allreduce2_wave<NV>(a, s, v, slot) : px_allreduce_wave<NV>(a, s, v, slot);
 }
 
 // A block that gave up leaves a mark in host memory on its way out, so the
@@ -566,7 +658,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
       float4 v[2];
       v[0] = make_float4(g[0][0], g[0][1], g[0][2], g[0][3]);
       v[1] = w < 3 ? make_float4(g[1][0], g[1][1], g[1][2], g[1][3]) : make_float4(db, 0.f, 0.f, 0.f);
-      const bool xok = px_allreduce_wave<2>(a, s, v, lb * 4 + w);
+      const bool xok = px_sum_wave<2>(a, s, v, lb * 4 + w);
       g[0] = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
       if (w < 3) g[1] = f32x4{v[1].x, v[1].y, v[1].z, v[1].w};
       else db = v[1].x;
@@ -1174,7 +1266,7 @@ __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g,
           float4 v[4] = {make_float4(gw[0][0], gw[0][1], gw[0][2], gw[0][3]),
                          make_float4(gw[1][0], gw[1][1], gw[1][2], gw[1][3]),
                          make_float4(g3[0], g3[1], g3[2], g3[3]), make_float4(sb, sb3, 0.f, 0.f)};
-          xok = px_allreduce_wave<4>(a, s, v, kNL1 * 4 + g * 4 + w);
+          xok = px_sum_wave<4>(a, s, v, kNL1 * 4 + g * 4 + w);
           gw[0] = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
           gw[1] = f32x4{v[1].x, v[1].y, v[1].z, v[1].w};
           g3 = f32x4{v[2].x, v[2].y, v[2].z, v[2].w};
@@ -1183,7 +1275,7 @@ __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g,
         } else {
           float4 v[2] = {make_float4(gw[0][0], gw[0][1], gw[0][2], gw[0][3]),
                          make_float4(gw[1][0], gw[1][1], gw[1][2], gw[1][3])};
-          xok = px_allreduce_wave<2>(a, s, v, kNL1 * 4 + g * 4 + w);
+          xok = px_sum_wave<2>(a, s, v, kNL1 * 4 + g * 4 + w);
           gw[0] = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
           gw[1] = f32x4{v[1].x, v[1].y, v[1].z, v[1].w};
         }
@@ -1246,7 +1338,7 @@ __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g,
         bool xok = true;
         if (w < 3) {
           float4 v[1] = {w < 2 ? make_float4(gw[0], gw[1], gw[2], gw[3]) : make_float4(sb, 0.f, 0.f, 0.f)};
-          xok = px_allreduce_wave<1>(a, s, v, kNL1 * 4 + g * 4 + w);
+          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + g * 4 + w);
           if (w < 2) gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
           else sb = v[0].x;
         }
@@ -1368,7 +1460,7 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
-                             hipStream_t s, const XchgArgs* xa, const XchgTab* tab) {
+                             hipStream_t s, const XchgArgs* xa, const XchgTab* tab, int algo) {
   if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
       (ldx % 4) != 0 || ldx < kD0 || (((uintptr_t)X) & 15) != 0)
     return hipErrorInvalidValue;
@@ -1395,7 +1487,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   a.timeout_ticks = timeout_ticks;
   a.nrep = 1;
   if (xa != nullptr && xa->nranks > 1) {
-    if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks) ||
+    if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks, algo) ||
         xa->err == nullptr)
       return hipErrorInvalidValue;
     a.xt = *tab;
@@ -1403,6 +1495,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     a.rep = xa->rank;
     a.xhalf = xa->half;
     a.xerr = xa->err;
+    a.algo = algo;
   }
   if (d.nlayers == 3) return a.nrep > 1 ? pk_launch<3, true>(a, s) : pk_launch<3, false>(a, s);
   return a.nrep > 1 ? pk_launch<2, true>(a, s) : pk_launch<2, false>(a, s);

@@ -348,7 +348,8 @@ void MlpRunner::enqueue_update(hipStream_t s) {
     DSML_HIP_CHECK(sgd_update_f32(b_.P, b_.G, b_.nparams, lr_ * gscale, s));
 }
 
-void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x) {
+void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x,
+                            int algo) {
   if (xbuf == nullptr) {
     pk_xb_ = nullptr;
     pk_err_ = nullptr;
@@ -364,13 +365,15 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
     const int n = x->nranks();
     if (!x->connected() || n < 2 || n != world_)
       throw std::invalid_argument("set_persist: the replica exchange must connect world_size >= 2 ranks");
-    if (x->ntiles() < px_ntiles(n) || x->half() < px_half(n))
+    if (algo != 0 && algo != 1) throw std::invalid_argument("set_persist: algo must be 0 or 1");
+    if (x->ntiles() < px_ntiles(n, algo) || x->half() < px_half(n, algo))
       throw std::invalid_argument("set_persist: exchange buffers too small for the persistent step");
     xchg_ = nullptr;  // the three-launch exchanges are off while the persistent step runs
   } else if (comm_ != nullptr || xchg_ != nullptr || world_ != 1) {
     throw std::invalid_argument("set_persist: single replica only (or pass the replica exchange)");
   }
   pk_x_ = x;
+  pk_algo_ = x != nullptr ? algo : 0;
   if (err == nullptr) throw std::invalid_argument("set_persist: needs an error word");
   if (pk_herr_ == nullptr) {
     void* h = nullptr;
@@ -390,7 +393,8 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
     if (pk_x_ != nullptr)
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_,
                                        lr_ / (float)pk_x_->nranks(), n, pk_xb_, b_.stats, pk_err_,
-                                       pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table()));
+                                       pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table(),
+                                       pk_algo_));
     else
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
                                        b_.stats, pk_err_, pk_herr_, pk_timeout_, s));

@@ -282,7 +282,8 @@ class MlpRunner {
   // is ONE launch.  Single replica, plain SGD, the flagship shape only.
   // With `x` (>= 2 ranks): the data-parallel persistent step, every weight
   // gradient summed over the replicas inside the launch through x's buffers.
-  void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x = nullptr);
+  void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x = nullptr,
+                   int algo = 0);
   bool persist_active() const { return pk_xb_ != nullptr; }
   // Whether a persistent launch gave up on a hand-off (read from host-mapped
   // memory the kernel marks on the way out: valid after a stream sync, no copy).
@@ -328,6 +329,7 @@ class MlpRunner {
   int xact_waves_ = 0;
   uint64_t* pk_xb_ = nullptr;
   PeerExchange* pk_x_ = nullptr;  // replica exchange of the persistent step (nranks > 1)
+  int pk_algo_ = 0;               // its sum: 0 one-shot, 1 two-shot
   uint32_t* pk_err_ = nullptr;
   uint32_t* pk_herr_ = nullptr;  // hipHostMalloc'd, device-visible
   uint64_t pk_timeout_ = 0;

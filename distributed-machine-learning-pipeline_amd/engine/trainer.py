@@ -26,9 +26,12 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("auto", "pk", "xact", "xgmi", "rccl", "ring", "torch")
-# fused over xGMI peer memory: into K_C (xact, xgmi) or into the persistent step (pk)
-EXCHANGE_MODES = ("pk", "xact", "xgmi")
+SYNC_MODES = ("auto", "pk", "pk2", "xact", "xgmi", "rccl", "ring", "torch")
+# fused over xGMI peer memory: into K_C (xact, xgmi) or into the persistent step
+# (pk: one-shot sum of every wave's gradient slot, pk2: two-shot, i.e.
+# reduce-scatter + all-gather per slot: 2(N-1)/N slots per link instead of N-1)
+EXCHANGE_MODES = ("pk", "pk2", "xact", "xgmi")
+PERSIST_MODES = {"pk": 0, "pk2": 1}
 
 
 @dataclass
@@ -244,12 +247,12 @@ class MlpTrainer:
         """Point the native runner at one gradient-sync mode.  None keeps the
         RCCL communicator as configured; 'rccl' / 'ring' select ncclAllReduce
         or the in-house multi-ring send/recv all-reduce on it."""
-        if mode == "pk":
-            self.xchg = self._exchanges["pk"]
+        if mode in PERSIST_MODES:
+            self.xchg = self._exchanges[mode]
             # waits on peers are bounded like the other exchanges' (ranks can enter
             # a launch seconds apart, e.g. around a checkpoint)
             self.runner.set_persist(self.pk_buf, self.pk_err, max(2000.0, self.xchg_timeout_ms),
-                                    self.xchg)
+                                    self.xchg, PERSIST_MODES[mode])
             return
         if self.pk_buf is not None:
             self.runner.set_persist(None)  # leave the persistent step
@@ -275,12 +278,13 @@ class MlpTrainer:
         from ..parallel import xchg as X
 
         try:
-            if mode == "pk":
+            if mode in PERSIST_MODES:
                 C = self.runner_module()
                 if not (self._want_persist and C.mlp_persist_supported(self.layout.desc_list())):
                     raise X.ExchangeUnavailable("the persistent step covers 784-128-64-10 and "
                                                 "784-128-10 at batch <= 64")
-                half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size)
+                half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size,
+                                                             PERSIST_MODES[mode])
                 x = X.make_exchange(self.ctx, half, ntiles, self.xchg_timeout_ms)
                 if self.pk_buf is None:
                     self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64,
@@ -318,7 +322,10 @@ class MlpTrainer:
         self._exchanges: Dict[str, object] = {}
         self.Xall = None
         strict = self.sync in EXCHANGE_MODES
-        modes = [self.sync] if strict else ["pk", "xact", "xgmi"]
+        # pk2 pays one more flag round trip per slot for fewer bytes: a
+        # candidate from 3 replicas on (at 2 it moves the same bytes as pk)
+        auto = ["pk"] + (["pk2"] if self.ctx.world_size >= 3 else []) + ["xact", "xgmi"]
+        modes = [self.sync] if strict else auto
         ok = []
         for m in modes:
             err = self._setup_exchange(m)

@@ -178,7 +178,7 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
         assert set(tr.sync_times) == {"pk", "xact", "xgmi", "torch"}, tr.sync_times
     else:
         assert tr.sync_active == sync
-    if sync == "pk":  # launches split anywhere: the step counter and tags carry over
+    if sync in ("pk", "pk2"):  # launches split anywhere: the step counter and tags carry over
         assert tr.persistent
         tr.train_steps(2)
         tr.train_steps(4)
@@ -191,7 +191,8 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
 
 @pytest.mark.parametrize("world,graph_steps,sync", [(2, 0, "xgmi"), (2, 3, "xgmi"), (2, 0, "xact"),
                                                     (2, 3, "xact"), (3, 3, "xact"), (3, 3, "xgmi"),
-                                                    (2, 0, "pk"), (3, 0, "pk"), (2, 3, "auto")])
+                                                    (2, 0, "pk"), (3, 0, "pk"), (2, 0, "pk2"),
+                                                    (3, 0, "pk2"), (2, 3, "auto")])
 def test_two_processes_ipc(world, graph_steps, sync):
     """N processes sharing the GPU through IPC handles.  Sharing one GPU, every
     process's spinning weight-gradient launch must be resident at once: the
@@ -200,8 +201,9 @@ def test_two_processes_ipc(world, graph_steps, sync):
     processes — with 4 or more, the hardware scheduler can leave a process's
     queue unmapped while its peers spin (seen as a timed-out self-test).  On a
     node each GPU runs one process and one launch.  sync='pk' runs the
-    persistent step in every process (36 workgroups each, all resident) with
-    the weight gradients summed over the replicas inside the launch."""
+    persistent step in every process (64 workgroups each, all resident) with
+    the weight gradients summed over the replicas inside the launch; 'pk2'
+    sums them two-shot (reduce-scatter + all-gather per wave slot)."""
     with tempfile.TemporaryDirectory() as d:
         spawn_group(_ipc_worker, world, lambda port: (world, port, d, graph_steps, sync,
                                               4 if sync in ("xact", "auto") else 0))

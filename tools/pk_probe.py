@@ -18,14 +18,17 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def pk_bytes_out(n: int, mode: str = "pk") -> int:
+def pk_bytes_out(n: int, algo: int = 0) -> int:
     """Bytes one replica pushes per step at n ranks (kernels/mlp_persist.hip):
-    layer-1 waves move only their real dW1 tiles (wave 0 four 16x16 fp32
-    tiles, waves 1-3 three) to every peer; chain wave slots (40 floats per
-    lane) go from chain c to the peers d with d % 4 == c."""
-    l1 = 32 * (4 + 3 * 3) * 64 * 4 * 4      # per destination
-    ch = 4 * 64 * 40 * 4                     # all 4 chains' slots, per destination
-    return (n - 1) * (l1 + ch)
+    each of the 224 layer-1 waves sums an 8-float-per-lane slot (2 KiB), the
+    16 gradient-block waves 16 / 8 / 4 floats per lane (3 layers: wave 0 four
+    float4, waves 1-3 two).  One-shot (pk): every slot to every peer; two-shot
+    (pk2): (n-1)/n of each slot to its owners, then the owners' (n-1)/n share
+    to every peer."""
+    slot_bytes = 224 * 64 * 8 * 4 + 4 * (64 * 16 * 4 + 3 * 64 * 8 * 4)
+    if algo == 0:
+        return (n - 1) * slot_bytes
+    return 2 * (n - 1) * slot_bytes // n
 
 
 def main() -> int:
@@ -33,6 +36,7 @@ def main() -> int:
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--launch", type=int, default=0, help="steps per launch (0: all in one)")
+    ap.add_argument("--algo", type=int, default=0, help="0: pk (one-shot), 1: pk2 (two-shot)")
     a = ap.parse_args()
     import torch
 
@@ -51,12 +55,12 @@ def main() -> int:
         assert tr.persistent
         xs = []
         if n > 1:
-            half, ntiles = C.MlpRunner.persist_xchg_size(n)
+            half, ntiles = C.MlpRunner.persist_xchg_size(n, a.algo)
             xs = make_local_group(None, [0] * n, 5000.0, half_floats=half, ntiles=ntiles)
             for x in xs:
                 x.fill_flags(1 << 62)
             tr.runner.set_world_size(n)
-            tr.runner.set_persist(tr.pk_buf, tr.pk_err, 5000.0, xs[0])
+            tr.runner.set_persist(tr.pk_buf, tr.pk_err, 5000.0, xs[0], a.algo)
         torch.cuda.synchronize()
 
         def run(k):
@@ -71,10 +75,10 @@ def main() -> int:
         run(a.steps)
         tr.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
-        print(json.dumps({"mode": "pk" if n > 1 else "none", "ranks": n,
+        print(json.dumps({"mode": ("pk2" if a.algo else "pk") if n > 1 else "none", "ranks": n,
                           "us_per_step": round(dt * 1e6, 2),
-                          "bytes_out_per_step": pk_bytes_out(n),
-                          "bytes_per_peer_per_step": pk_bytes_out(n) // max(n - 1, 1)}),
+                          "bytes_out_per_step": pk_bytes_out(n, a.algo),
+                          "bytes_per_peer_per_step": pk_bytes_out(n, a.algo) // max(n - 1, 1)}),
               flush=True)
         del tr, xs
         torch.cuda.synchronize()
