@@ -830,6 +830,10 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     const int par = (int)(s & 1);
     const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * a.batch;
 
+    // this step's labels first: their memory round trip hides under the waits
+    const int srow = w * 4 + (lane >> 4);  // softmax: 16 lanes per row, 4 rows per wave
+    const bool rvalid = rb0 + srow < a.batch;
+    const int y = rvalid ? a.labels[r0 + rb0 + srow] : -1;
     f4v wv[WSlices<NL>::kIt];
     // ---- H1 rows = relu(sum of the 7 k-partials) ----
     // this chain's 16 rows of every partial in one bulk read: thread -> (gn,
@@ -848,6 +852,18 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         v[gk][0] = ld_f4(rb, off);
         v[gk][1] = ld_f4(rb, off + 4);
       }
+      // the previous step's updated upper weights (gradient blocks), in flight
+      // together with the partials: every wave checks their 4 flags itself
+      // (lanes 0-3, then a wave vote), so no workgroup barrier -- which would
+      // drain the partial loads first -- sits between the two load batches
+      if (it > 0) {
+        bool wok = true;
+        if (lane < kNG) wok = wait_flag(rb, kOffWf + (par ^ 1) * kNG + lane, tag - 1, poll);
+        wok = __builtin_amdgcn_ballot_w64(!wok) == 0;
+        asm volatile("" ::: "memory");
+        if (wok) pk_w_fetch<NL>(a, wv, true, par ^ 1);
+        else ok = false;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float z = 0.f;
@@ -856,16 +872,9 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         H1[(8 * half + e) * kS1 + 16 * gn + n] = fmaxf(z, 0.f);
       }
     }
-    const int srow = w * 4 + (lane >> 4);  // softmax: 16 lanes per row, 4 rows per wave
-    const bool rvalid = rb0 + srow < a.batch;
-    const int y = rvalid ? a.labels[r0 + rb0 + srow] : -1;
-    // the previous step's updated upper weights (gradient blocks): in the
-    // steady state they arrive while the partials are loaded and summed
     if (it > 0) {
-      if (tid < kNG && !wait_flag(rb, kOffWf + (par ^ 1) * kNG + tid, tag - 1, poll)) ok = false;
       ok = __syncthreads_and(ok ? 1 : 0) != 0;
       if (!ok) break;
-      pk_w_fetch<NL>(a, wv, true, par ^ 1);
       pk_w_commit<NL>(lds, wv);
     }
     lds_barrier();
