@@ -111,6 +111,10 @@ class WideMlpTrainer:
         self.views = self.layout.views(self.P)
         self.gviews = self.layout.views(self.G)
         self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
+        # the split head's partial logits (two launches of slices x rows
+        # one-wave workgroups instead of one workgroup per row)
+        self.head_ws = (torch.zeros(self.C.head_ws_floats(batch, self.pd[L - 1]), dtype=torch.float32,
+                                    device=dev) if self.fused_head else None)
         # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
         self.plans: Dict[str, tuple] = {}
         for l in range(L):
@@ -135,7 +139,9 @@ class WideMlpTrainer:
         if self.ctx.is_distributed and (sync in ("rccl", "ring") or
                                         (sync == "xact" and self.ctx.backend == "nccl")):
             self.comm = make_native_comm(self.ctx)
-        capture_comm = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "1") != "0"
+        # collectives captured into the epoch graph only on request until a
+        # multi-GPU run has validated it; eager otherwise
+        capture_comm = os.environ.get("HIPDSML_CAPTURE_COLLECTIVES", "0") == "1"
         self.graph_enabled = graph and (not self.ctx.is_distributed or
                                         (self.comm is not None and capture_comm))
         self._graph = None
@@ -275,7 +281,8 @@ class WideMlpTrainer:
             prev = L >= 2
             C.head_softmax_xent(self.H[L - 1], cur[L - 1], b, Bt, self.pd[L - 1], d[L],
                                 self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], None,
-                                self.stats, dzp=self.dZ[L - 1] if prev else None, row_stats=True)
+                                self.stats, dzp=self.dZ[L - 1] if prev else None, row_stats=True,
+                                ws=self.head_ws)
         else:
             C.gemm_bf16_nt_fused(self.H[L - 1], cur[L - 1], Bt, d[L], d[L - 1], bias=b,
                                  of32=self.logits, splits=0)
@@ -480,7 +487,7 @@ class WideMlpTrainer:
                 if self.fused_head:
                     C.head_softmax_xent(self.H[L - 1], self.wb(L - 1), b, m, self.pd[L - 1], d[L],
                                         y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st,
-                                        row_stats=True)
+                                        row_stats=True, ws=self.head_ws)
                 else:
                     C.gemm_bf16_nt_fused(self.H[L - 1], self.wb(L - 1), m, d[L], d[L - 1], bias=b,
                                          of32=self.logits, splits=0)
