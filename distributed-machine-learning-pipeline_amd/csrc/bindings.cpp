@@ -390,10 +390,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                     double inv_batch, c10::optional<torch::Tensor> logits,
                                     torch::Tensor dz, c10::optional<torch::Tensor> dzT,
                                     torch::Tensor stats, c10::optional<torch::Tensor> dzp,
-                                    c10::optional<torch::Tensor> dzpT, bool row_stats,
-                                    c10::optional<torch::Tensor> ws) {
+                                    c10::optional<torch::Tensor> dzpT, bool row_stats) {
     TORCH_CHECK(!row_stats || stats.numel() >= 4 * B, "row_stats needs 4 floats per row");
-    if (ws) check_f32(*ws, "ws");
     TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && H.size(0) >= B && H.size(1) >= K, "H shape");
     TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.size(0) >= C && W.size(1) >= K, "W shape");
     check_cuda(labels, "labels"); check_f32(stats, "stats");
@@ -417,14 +415,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     hip_ok(head_softmax_xent(bf16p(H, "H"), H.stride(0), bf16p(W, "W"), W.stride(0), b, (int)B, (int)K,
                              (int)C, labels.data_ptr<int32_t>(), (float)inv_batch, lg, ldl,
                              bf16p(dz, "dz"), dz.stride(0), t, ldt, (int)Cp, stats.data_ptr<float>(),
-                             cur_stream(), pp, ldp, ppT, ldpT, row_stats ? 1 : 0,
-                             ws ? ws->data_ptr<float>() : nullptr, ws ? ws->numel() : 0),
-           "head_softmax_xent");
+                             cur_stream(), pp, ldp, ppT, ldpT, row_stats ? 1 : 0), "head_softmax_xent");
   }, py::arg("H"), py::arg("W"), py::arg("bias"), py::arg("B"), py::arg("K"), py::arg("C"),
      py::arg("labels"), py::arg("inv_batch"), py::arg("logits"), py::arg("dz"), py::arg("dzT"),
      py::arg("stats"), py::arg("dzp") = py::none(), py::arg("dzpT") = py::none(),
-     py::arg("row_stats") = false, py::arg("ws") = py::none());
-  m.def("head_ws_floats", [](int64_t B, int64_t K) { return (int64_t)head_slices((int)K) * B * 16; });
+     py::arg("row_stats") = false);
   m.def("rowsum_bf16", [bf16p](torch::Tensor X, int64_t N, int64_t cols, c10::optional<torch::Tensor> out,
                               c10::optional<torch::Tensor> bias, double lr) {
     TORCH_CHECK(X.dim() == 2 && X.size(0) >= N && X.size(1) >= cols, "X shape");

@@ -251,11 +251,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp = nullptr, int64_t ldzp = 0, uint16_t* dzpT = nullptr,
-                             int64_t ldpt = 0, int row_stats = 0, float* ws = nullptr,
-                             int64_t ws_floats = 0);
-// Workspace floats of the split head (two launches of head_slices(K) x B
-// one-wave workgroups instead of B workgroups): head_slices(K) * B * 16.
-int head_slices(int K);
+                             int64_t ldpt = 0, int row_stats = 0);
 // Skinny GEMMs (kernels/gemm_skinny.hip): C[M x N] = A[M x K] . B^T for
 // B [N x K] (nn = false) or A . B for B [K x N] (nn = true: W read in its
 // stored layout through transposing LDS reads), 64 x 64 tiles, K split S ways

@@ -817,11 +817,13 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     if (c == y && stats && !(g_head_dbg & 1)) {
       if (row_stats) {
         // this row's own accumulators (stats[4m .. 4m+2]: only this workgroup
-        // writes them): no same-address atomics from 64 workgroups per step
+        // adds to them, so no contention): no-return atomics instead of a
+        // read-modify-write, whose load round trip the dZ_{L-1} phase below
+        // (and every other wave, at its barrier) would wait for
         float* r = stats + 4 * (int64_t)m;
-        r[0] += -logf(p + 1e-10f);
-        r[1] += am == y ? 1.f : 0.f;
-        r[2] += 1.f;
+        __hip_atomic_fetch_add(r + 0, -logf(p + 1e-10f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(r + 1, am == y ? 1.f : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(r + 2, 1.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         atomicAdd(stats + 0, -logf(p + 1e-10f));
         atomicAdd(stats + 1, am == y ? 1.f : 0.f);
@@ -881,139 +883,13 @@ void head_set_stamping(bool on) {
   (void)hipDeviceSynchronize();
 }
 
-// ---- split form of the head (a workspace given): K cut into S <= 16 slices
-// of 512, one 64-lane workgroup per (slice, row) in each of two launches, so
-// S x B workgroups (512 at B = 64, K = 4096) share the work instead of B:
-//  head_part_k:   partial logits of the slice (8 elements per lane, one wave
-//                 reduction per class) -> part[S][B][16]
-//  head_finish_k: every workgroup of a row sums the S partials in slice
-//                 order and runs the softmax-CE itself (identical bits in all
-//                 S), slice 0 stores dZ_L / logits / stats, and each writes
-//                 its slice of dZ_{L-1} = (dZ_L . W) * (H > 0).
-constexpr int kHeadSlice = 512;
-__global__ __launch_bounds__(64) void head_part_k(const uint16_t* __restrict__ H, int64_t ldh,
-                                                  const uint16_t* __restrict__ W, int64_t ldw, int K,
-                                                  int C, int B, float* __restrict__ part) {
-  const int ks = blockIdx.x, m = blockIdx.y, lane = threadIdx.x;
-  const int k = ks * kHeadSlice + 8 * lane;
-  const bool kv = k < K;
-  const uint4 hv = kv ? *reinterpret_cast<const uint4*>(H + (int64_t)m * ldh + k) : make_uint4(0u, 0u, 0u, 0u);
-  uint4 wv[kHeadMaxC];
-#pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c)
-    wv[c] = (kv && c < C) ? *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k) : make_uint4(0u, 0u, 0u, 0u);
-  const float h[8] = {bf16lo(hv.x), bf16hi(hv.x), bf16lo(hv.y), bf16hi(hv.y),
-                      bf16lo(hv.z), bf16hi(hv.z), bf16lo(hv.w), bf16hi(hv.w)};
-  float mine = 0.f;
-#pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c) {
-    if (c >= C) break;
-    const uint4 x = wv[c];
-    const float a = h[0] * bf16lo(x.x) + h[1] * bf16hi(x.x) + h[2] * bf16lo(x.y) + h[3] * bf16hi(x.y) +
-                    h[4] * bf16lo(x.z) + h[5] * bf16hi(x.z) + h[6] * bf16lo(x.w) + h[7] * bf16hi(x.w);
-    const float tot = wave_sum(a);
-    if (lane == c) mine = tot;
-  }
-  if (lane < kHeadMaxC) part[((int64_t)ks * B + m) * kHeadMaxC + lane] = mine;
-}
-
-__global__ __launch_bounds__(64) void head_finish_k(
-    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
-    const float* __restrict__ bias, int K, int C, int B, int S, const int32_t* __restrict__ labels,
-    float inv_batch, const float* __restrict__ part, float* __restrict__ logits, int64_t ldl,
-    uint16_t* __restrict__ dz, int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp,
-    float* __restrict__ stats, uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT,
-    int64_t ldpt, int row_stats) {
-  const int ks = blockIdx.x, m = blockIdx.y, lane = threadIdx.x;
-  const int k = ks * kHeadSlice + 8 * lane;
-  const bool kv = dzp != nullptr && k < K;
-  // the slice's operands of dZ_{L-1} go out first, behind them the partials
-  uint4 hv = make_uint4(0u, 0u, 0u, 0u), wv[kHeadMaxC];
-  if (kv) hv = *reinterpret_cast<const uint4*>(H + (int64_t)m * ldh + k);
-#pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c)
-    wv[c] = (kv && c < C) ? *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k) : make_uint4(0u, 0u, 0u, 0u);
-  const int y = labels[m];
-  const int c = lane & 15;
-  const bool cv = c < C;
-  float z = -3.402823466e38f;
-  if (cv) {
-    z = bias ? bias[c] : 0.f;
-    for (int j = 0; j < S; ++j) z += part[((int64_t)j * B + m) * kHeadMaxC + c];
-  }
-  float mx = z;
-  int am = cv ? c : 0x7fffffff;
-  row16_argmax(mx, am);
-  const float e = cv ? expf(z - mx) : 0.f;
-  const float se = row16_sum(e);
-  const float p = e / se;
-  const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
-  const uint16_t hq = f32_to_bf16(gr);
-  if (ks == 0 && lane < 16) {
-    if (cv && logits) logits[(int64_t)m * ldl + c] = z;
-    if (c < Cp) {
-      dz[(int64_t)m * ldz + c] = hq;
-      if (dzT) dzT[(int64_t)c * ldt + m] = hq;
-    }
-    if (c == y && stats) {
-      if (row_stats) {
-        float* r = stats + 4 * (int64_t)m;
-        r[0] += -logf(p + 1e-10f);
-        r[1] += am == y ? 1.f : 0.f;
-        r[2] += 1.f;
-      } else {
-        atomicAdd(stats + 0, -logf(p + 1e-10f));
-        atomicAdd(stats + 1, am == y ? 1.f : 0.f);
-        atomicAdd(stats + 2, 1.f);
-      }
-    }
-  }
-  if (!kv) return;
-  const float gq = bf16_to_f32(hq);
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc) {
-    if (cc >= C) break;
-    const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gq), cc));
-    const uint4 x = wv[cc];
-    a[0] += g * bf16lo(x.x); a[1] += g * bf16hi(x.x);
-    a[2] += g * bf16lo(x.y); a[3] += g * bf16hi(x.y);
-    a[4] += g * bf16lo(x.z); a[5] += g * bf16hi(x.z);
-    a[6] += g * bf16lo(x.w); a[7] += g * bf16hi(x.w);
-  }
-  const float h[8] = {bf16lo(hv.x), bf16hi(hv.x), bf16lo(hv.y), bf16hi(hv.y),
-                      bf16lo(hv.z), bf16hi(hv.z), bf16lo(hv.w), bf16hi(hv.w)};
-  uint16_t q[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) q[j] = f32_to_bf16(h[j] > 0.f ? a[j] : 0.f);
-  *reinterpret_cast<uint4*>(dzp + (int64_t)m * ldzp + k) =
-      make_uint4(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16),
-                 q[4] | ((uint32_t)q[5] << 16), q[6] | ((uint32_t)q[7] << 16));
-  if (dzpT) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dzpT[(int64_t)(k + j) * ldpt + m] = q[j];
-  }
-}
-
-int head_slices(int K) { return (K + kHeadSlice - 1) / kHeadSlice; }
 
 hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, int64_t ldw,
                              const float* bias, int B, int K, int C, const int32_t* labels,
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt,
-                             int row_stats, float* ws, int64_t ws_floats) {
-  const int S = head_slices(K);
-  if (ws != nullptr && S <= 16 && ws_floats >= (int64_t)S * B * kHeadMaxC && C >= 1 && C <= kHeadMaxC &&
-      Cp <= 64 && (K & 7) == 0 && (ldh & 7) == 0 && (ldw & 7) == 0 &&
-      (((uintptr_t)H | (uintptr_t)W) & 15) == 0 &&
-      (dzp == nullptr || ((ldzp & 7) == 0 && ((uintptr_t)dzp & 15) == 0))) {
-    hipLaunchKernelGGL(head_part_k, dim3(S, B), dim3(64), 0, s, H, ldh, W, ldw, K, C, B, ws);
-    hipLaunchKernelGGL(head_finish_k, dim3(S, B), dim3(64), 0, s, H, ldh, W, ldw, bias, K, C, B, S,
-                       labels, inv_batch, ws, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp,
-                       dzpT, ldpt, row_stats);
-    return hipGetLastError();
-  }
+                             int row_stats) {
   if (dzp && ((ldzp & 7) || ((uintptr_t)dzp & 15))) return hipErrorInvalidValue;
   if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
       (ldw & 7) ||

@@ -111,10 +111,6 @@ class WideMlpTrainer:
         self.views = self.layout.views(self.P)
         self.gviews = self.layout.views(self.G)
         self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
-        # the split head's partial logits (two launches of slices x rows
-        # one-wave workgroups instead of one workgroup per row)
-        self.head_ws = (torch.zeros(self.C.head_ws_floats(batch, self.pd[L - 1]), dtype=torch.float32,
-                                    device=dev) if self.fused_head else None)
         # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
         self.plans: Dict[str, tuple] = {}
         for l in range(L):
@@ -281,8 +277,7 @@ class WideMlpTrainer:
             prev = L >= 2
             C.head_softmax_xent(self.H[L - 1], cur[L - 1], b, Bt, self.pd[L - 1], d[L],
                                 self.y[r0:r0 + Bt], 1.0 / Bt, self.logits, self.dZ[L], None,
-                                self.stats, dzp=self.dZ[L - 1] if prev else None, row_stats=True,
-                                ws=self.head_ws)
+                                self.stats, dzp=self.dZ[L - 1] if prev else None, row_stats=True)
         else:
             C.gemm_bf16_nt_fused(self.H[L - 1], cur[L - 1], Bt, d[L], d[L - 1], bias=b,
                                  of32=self.logits, splits=0)
@@ -487,7 +482,7 @@ class WideMlpTrainer:
                 if self.fused_head:
                     C.head_softmax_xent(self.H[L - 1], self.wb(L - 1), b, m, self.pd[L - 1], d[L],
                                         y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st,
-                                        row_stats=True, ws=self.head_ws)
+                                        row_stats=True)
                 else:
                     C.gemm_bf16_nt_fused(self.H[L - 1], self.wb(L - 1), m, d[L], d[L - 1], bias=b,
                                          of32=self.logits, splits=0)

@@ -104,14 +104,10 @@ def test_gemm_rows64_epilogues(M, N, K):
     assert (o32.cpu() - ref * (mask.float() > 0)).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("split", [False, True], ids=["one_launch", "split"])
 @pytest.mark.parametrize("C_,K", [(10, 4096), (16, 784), (3, 64)])
-def test_head_softmax_xent(C_, K, split):
-    """One workgroup per row, or (split: a workspace given) the two-launch form
-    over K slices of 512 x rows."""
+def test_head_softmax_xent(C_, K):
     C = require_native()
     B = 64
-    ws = torch.zeros(C.head_ws_floats(B, K), device=DEV) if split else None
     g = torch.Generator().manual_seed(C_ * K)
     H = torch.randn(B, K, generator=g).to(torch.bfloat16)
     W = (0.05 * torch.randn(C_, K, generator=g)).to(torch.bfloat16)
@@ -123,7 +119,7 @@ def test_head_softmax_xent(C_, K, split):
     dzT = torch.zeros(Cp, B, dtype=torch.bfloat16, device=DEV)
     stats = torch.zeros(4, device=DEV)
     C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
-                        dzT, stats, ws=ws)
+                        dzT, stats)
     torch.cuda.synchronize()
     z = H.float() @ W.float().t() + b
     assert (logits.cpu() - z).abs().max().item() < 1e-3
@@ -138,7 +134,7 @@ def test_head_softmax_xent(C_, K, split):
     # per-row accumulators (no atomics): the rows' sums equal the atomic totals
     rows = torch.zeros(B * 4, device=DEV)
     C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
-                        dzT, rows, row_stats=True, ws=ws)
+                        dzT, rows, row_stats=True)
     torch.cuda.synchronize()
     tot = rows.view(-1, 4).sum(0)
     assert tot[2].item() == B and torch.all(rows.view(-1, 4)[:, 2] == 1)
@@ -148,7 +144,7 @@ def test_head_softmax_xent(C_, K, split):
     dzp = torch.zeros(B, Kp, dtype=torch.bfloat16, device=DEV)
     dzpT = torch.zeros(Kp, B, dtype=torch.bfloat16, device=DEV)
     C.head_softmax_xent(H.to(DEV), W.to(DEV), b.to(DEV), B, K, C_, y.to(DEV), 1.0 / B, logits, dz,
-                        dzT, stats, dzp=dzp, dzpT=dzpT, ws=ws)
+                        dzT, stats, dzp=dzp, dzpT=dzpT)
     torch.cuda.synchronize()
     dzb = dz.cpu()[:, :C_].float()
     want = (dzb @ W.float()) * (H.float() > 0)

@@ -92,6 +92,17 @@ def test_local_group_matches_reference(world, graph_steps):
     _fresh(_case_local_group, world, graph_steps)
 
 
+def test_local_group_in_the_long_process():
+    """The same 3-replica group run IN this long-lived pytest process (after
+    the tests above have churned the caching allocator), inside a non-null
+    torch stream as _fresh_entry sets up: the replicas' inputs are produced
+    on torch's stream and consumed on the replica queues only behind the
+    PeerExchange constructor's device synchronize, and every runner call
+    joins back into torch's stream before the parameters are read."""
+    with torch.cuda.stream(torch.cuda.Stream(DEV)):
+        _case_local_group(3, 0)
+
+
 def _case_missing_peer():
     trs, xs = _local_group(2, 2, 0, timeout_ms=200.0)
     trs[0].train_steps(1)  # rank 1 never runs
