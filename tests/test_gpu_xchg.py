@@ -25,13 +25,18 @@ DIMS = (784, 128, 64, 10)
 def _fresh(fn, *args):
     """Run `fn(*args)` in a freshly spawned process.
 
-    In-process replica groups are exact in a fresh process but intermittently
-    read stale lines in a long pytest process whose caching allocator hands
-    them memory other kernels (on other queues) touched before: with per-XCD
-    L2s, a replica reading memory another queue wrote is only safe behind a
-    stream-ordered (event) hand-off, and the test groups deliberately run their
-    replicas on independent queues.  Production runs one process per GPU.
-    Exceptions in the child fail the test with the child's traceback."""
+    Round 1 saw in-process replica groups read stale data intermittently in
+    the long pytest process (never in a fresh one) and moved them here.  The
+    suspected cause -- memory the caching allocator recycled from work on
+    another queue, read by a replica queue without a stream-ordered hand-off
+    -- is now excluded by construction: every replica input is produced before
+    the PeerExchange constructor's device synchronize, every exchange payload
+    and flag lives in uncached memory written and read at system scope
+    (kernels/common.h), and test_local_group_in_the_long_process runs one
+    3-replica group in the long process (green in the round-3 full suite,
+    profiles/r3_gpu_suite.txt).  The other cases stay isolated so a fault in
+    one cannot poison the rest of the suite.  Exceptions in the child fail the
+    test with the child's traceback."""
     mp.start_processes(_fresh_entry, args=(fn, args), nprocs=1, start_method="spawn", join=True)
 
 
