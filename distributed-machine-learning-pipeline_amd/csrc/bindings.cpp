@@ -531,7 +531,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_sgd", [bf16p](torch::Tensor Z, torch::Tensor X, int64_t M, int64_t N, int64_t K, double alpha,
                             double lr, c10::optional<torch::Tensor> W, c10::optional<torch::Tensor> Wb,
                             c10::optional<torch::Tensor> G, c10::optional<torch::Tensor> bias,
-                            c10::optional<torch::Tensor> bgrad) {
+                            c10::optional<torch::Tensor> bgrad, c10::optional<torch::Tensor> Wh,
+                            c10::optional<torch::Tensor> Wl) {
     TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
     TORCH_CHECK(Z.size(0) >= M && X.size(0) >= M && Z.size(1) >= ((N + 7) / 8) * 8 &&
                 X.size(1) >= ((K + 7) / 8) * 8, "Z / X too small (rows padded to 8 columns)");
@@ -547,11 +548,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     float* b = nullptr; float* bg = nullptr;
     if (bias) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() >= N, "bias"); b = bias->data_ptr<float>(); }
     if (bgrad) { check_f32(*bgrad, "bgrad"); TORCH_CHECK(bgrad->numel() >= N, "bgrad"); bg = bgrad->data_ptr<float>(); }
-    hip_ok(wgrad_sgd(bf16p(Z, "Z"), Z.stride(0), bf16p(X, "X"), X.stride(0), (int)M, (int)N, (int)K, (float)alpha,
-                     (float)lr, w, ldw, wb, ldwb, g, ldg, b, bg, cur_stream()), "wgrad_sgd");
+    WgLayer a{bf16p(Z, "Z"), Z.stride(0), bf16p(X, "X"), X.stride(0), (int)M, (int)N, (int)K, (float)alpha,
+              (float)lr, w, ldw, wb, ldwb, g, ldg, b, bg};
+    if (Wh) { chk2(*Wh, N, K, "Wh"); a.Wh = bf16p(*Wh, "Wh"); a.ldwh = Wh->stride(0); }
+    if (Wl) {
+      chk2(*Wl, N, K, "Wl");
+      TORCH_CHECK(Wl->scalar_type() == torch::kInt16, "Wl must be int16");
+      a.Wl = reinterpret_cast<uint16_t*>(Wl->data_ptr<int16_t>()); a.ldwl = Wl->stride(0);
+    }
+    hip_ok(wgrad_sgd_multi(&a, 1, cur_stream(), 64), "wgrad_sgd");
   }, py::arg("Z"), py::arg("X"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("alpha") = 1.0,
      py::arg("lr") = 0.0, py::arg("W") = py::none(), py::arg("Wb") = py::none(), py::arg("G") = py::none(),
-     py::arg("bias") = py::none(), py::arg("bgrad") = py::none());
+     py::arg("bias") = py::none(), py::arg("bgrad") = py::none(), py::arg("Wh") = py::none(),
+     py::arg("Wl") = py::none());
+  m.def("hilo_sgd", [bf16p](torch::Tensor hic, torch::Tensor lo, c10::optional<torch::Tensor> G, double lr,
+                           torch::Tensor hin) {
+    // split master step: w = join(hic, lo) - lr * G; hin / lo <- split(w) (G [N x K] fp32)
+    TORCH_CHECK(hic.dim() == 2 && lo.dim() == 2 && hin.dim() == 2 && hic.stride(1) == 1 && lo.stride(1) == 1 &&
+                hin.stride(1) == 1, "hilo_sgd: 2-D rows");
+    TORCH_CHECK(lo.scalar_type() == torch::kInt16, "lo must be int16");
+    int64_t N = hic.size(0), K = hic.size(1);
+    const float* g = nullptr; int64_t ldg = 0;
+    if (G) {
+      check_f32(*G, "G");
+      TORCH_CHECK(G->dim() == 2 && G->stride(1) == 1, "G 2-D rows");
+      N = G->size(0); K = G->size(1); g = G->data_ptr<float>(); ldg = G->stride(0);
+    }
+    TORCH_CHECK(hic.size(0) >= N && hic.size(1) >= K && lo.size(0) >= N && lo.size(1) >= K && hin.size(0) >= N &&
+                hin.size(1) >= K, "hilo_sgd shapes");
+    hip_ok(hilo_sgd(bf16p(hic, "hic"), hic.stride(0), reinterpret_cast<uint16_t*>(lo.data_ptr<int16_t>()),
+                    lo.stride(0), g, ldg, (int)N, (int)K, (float)lr, bf16p(hin, "hin"), hin.stride(0), cur_stream()),
+           "hilo_sgd");
+  }, py::arg("hic"), py::arg("lo"), py::arg("G"), py::arg("lr"), py::arg("hin"));
   m.def("head_stamps", []() {
     std::vector<uint64_t> v(64 * 6);
     hip_ok(head_read_stamps(v.data()), "head_read_stamps");
@@ -559,7 +587,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("head_set_stamping", &head_set_stamping);
   m.def("head_set_debug", &head_set_debug);
-  m.def("wgrad_sgd_multi", [bf16p](py::list layers) {
+  m.def("wgrad_sgd_multi", [bf16p](py::list layers, int tile) {
     // each item: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad); tensors may be None
     std::vector<WgLayer> v;
     auto opt = [](py::handle h) -> c10::optional<torch::Tensor> {
@@ -568,7 +596,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     };
     for (py::handle it : layers) {
       py::tuple t = it.cast<py::tuple>();
-      TORCH_CHECK(t.size() == 12, "wgrad_sgd_multi: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad)");
+      TORCH_CHECK(t.size() == 12 || t.size() == 14,
+                  "wgrad_sgd_multi: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl])");
       torch::Tensor Z = t[0].cast<torch::Tensor>(), X = t[1].cast<torch::Tensor>();
       const int64_t M = t[2].cast<int64_t>(), N = t[3].cast<int64_t>(), K = t[4].cast<int64_t>();
       TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
@@ -586,10 +615,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       if (auto G = opt(t[9])) { chk2(*G, "G"); check_f32(*G, "G"); a.G = G->data_ptr<float>(); a.ldg = G->stride(0); }
       if (auto b = opt(t[10])) { check_f32(*b, "bias"); TORCH_CHECK(b->numel() >= N, "bias"); a.bias = b->data_ptr<float>(); }
       if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
+      if (t.size() == 14) {  // split master: this step's hi words + the int16 remainders
+        if (auto Wh = opt(t[12])) { chk2(*Wh, "Wh"); a.Wh = bf16p(*Wh, "Wh"); a.ldwh = Wh->stride(0); }
+        if (auto Wl = opt(t[13])) {
+          chk2(*Wl, "Wl");
+          TORCH_CHECK(Wl->scalar_type() == torch::kInt16, "Wl must be int16");
+          a.Wl = reinterpret_cast<uint16_t*>(Wl->data_ptr<int16_t>()); a.ldwl = Wl->stride(0);
+        }
+      }
       v.push_back(a);
     }
-    hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream()), "wgrad_sgd_multi");
-  }, py::arg("layers"));
+    hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
+  }, py::arg("layers"), py::arg("tile") = 0);
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");
@@ -598,6 +635,27 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_skinny_set_stamping", &gemm_skinny_set_stamping);
   m.def("gemm_skinny_splits", &gemm_skinny_splits, py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("splits") = 0);
+  m.def("hilo_split", [bf16p](torch::Tensor W, torch::Tensor hi, torch::Tensor lo) {
+    // W [N x K] fp32 (row stride >= K) -> hi (bf16 words) / lo (int16) [>= N x >= K]
+    check_f32(W, "W");
+    TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && hi.dim() == 2 && lo.dim() == 2 && hi.stride(1) == 1 &&
+                lo.stride(1) == 1 && hi.size(0) >= W.size(0) && hi.size(1) >= W.size(1) &&
+                lo.size(0) >= W.size(0) && lo.size(1) >= W.size(1), "hilo_split shapes");
+    TORCH_CHECK(lo.scalar_type() == torch::kInt16, "lo must be int16");
+    hip_ok(hilo_split(W.data_ptr<float>(), (int)W.size(0), (int)W.size(1), W.stride(0), bf16p(hi, "hi"),
+                      hi.stride(0), reinterpret_cast<uint16_t*>(lo.data_ptr<int16_t>()), lo.stride(0),
+                      cur_stream()), "hilo_split");
+  });
+  m.def("hilo_join", [bf16p](torch::Tensor hi, torch::Tensor lo, torch::Tensor W) {
+    check_f32(W, "W");
+    TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && hi.dim() == 2 && lo.dim() == 2 && hi.stride(1) == 1 &&
+                lo.stride(1) == 1 && hi.size(0) >= W.size(0) && hi.size(1) >= W.size(1) &&
+                lo.size(0) >= W.size(0) && lo.size(1) >= W.size(1), "hilo_join shapes");
+    TORCH_CHECK(lo.scalar_type() == torch::kInt16, "lo must be int16");
+    hip_ok(hilo_join(bf16p(hi, "hi"), hi.stride(0), reinterpret_cast<const uint16_t*>(lo.data_ptr<int16_t>()),
+                     lo.stride(0), (int)W.size(0), (int)W.size(1), W.data_ptr<float>(), W.stride(0), cur_stream()),
+           "hilo_join");
+  });
   m.def("sgd_cast", [bf16p](torch::Tensor W, c10::optional<torch::Tensor> G, int64_t N, int64_t K, double lr,
                            torch::Tensor Wb, c10::optional<torch::Tensor> WbT) {
     check_f32(W, "W");

@@ -286,12 +286,28 @@ struct WgLayer {
   int64_t ldg;
   float* bias;   // b -= lr * alpha * colsum(Z) (nullable)
   float* bgrad;  // alpha * colsum(Z) out (nullable)
+  // split fp32 master instead of W (W == nullptr): bits = (hi << 16) + lo.
+  // Wh: this step's hi words (= its bf16 GEMM copy), ldwh; Wl: the int16
+  // remainders, updated in place, ldwl; the updated hi words go to Wb.
+  const uint16_t* Wh;
+  int64_t ldwh;
+  uint16_t* Wl;
+  int64_t ldwl;
 };
-// Up to 4 layers' wgrad_sgd in one launch (one flattened tile grid).
-// variant 0: one workgroup per 64 x 64 tile (the production kernel); 20 / 21:
-// roofline probes (tools/wgrad_var.py): the same tiles without operand staging
-// and MFMAs / a `grid`-workgroup linear stream of the same W bytes
-hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s);
+// fp32 <-> split master (hi: bf16 rounded half away from zero, lo: int16 remainder)
+hipError_t hilo_split(const float* W, int N, int K, int64_t ldw, uint16_t* hi, int64_t ldh, uint16_t* lo,
+                      int64_t ldl, hipStream_t s);
+hipError_t hilo_join(const uint16_t* hi, int64_t ldh, const uint16_t* lo, int64_t ldl, int N, int K, float* W,
+                     int64_t ldw, hipStream_t s);
+// split master SGD step: w = join(hic, lo) - lr * G (G nullable: a re-split);
+// hin <- hi(w) (the next step's bf16 copy), lo <- lo(w) in place
+hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl, const float* G, int64_t ldg,
+                    int N, int K, float lr, uint16_t* hin, int64_t ldn, hipStream_t s);
+// Up to 4 layers' wgrad_sgd in one launch (one flattened tile grid).  tile 128:
+// 128 x 128 tiles for every layer with N, K >= 128, 64 x 64 for the rest; 64:
+// 64 x 64 everywhere; 0 (auto): 128 for fp32-master layers at M >= 512 rows,
+// else 64.
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 void head_set_debug(int v);

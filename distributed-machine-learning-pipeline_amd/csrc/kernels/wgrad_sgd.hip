@@ -25,6 +25,7 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 typedef short wg_i16x4 __attribute__((ext_vector_type(4)));
 typedef float wg_f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t wg_u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t wg_u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) void* wg_gptr;
 typedef __attribute__((address_space(3))) void* wg_lptr;
 typedef __attribute__((address_space(3))) wg_i16x4* wg_lv4;
@@ -35,6 +36,42 @@ constexpr int kWgPitch = 68;      // floats per row of the fp32 epilogue tile
 __device__ __forceinline__ int wg_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
 
 typedef WgLayer WgArgs;  // dsml.h: one layer's operands, targets and step
+
+// Split fp32 master ("hi/lo" form, WgLayer::Wl): w's bit pattern = (hi << 16)
+// + lo, hi = bf16(w) rounded half away from zero in magnitude, lo = the signed
+// 16-bit remainder (in [-0x8000, 0x7fff]: exactly representable, so the split
+// loses nothing).  hi IS the bf16 copy the GEMMs read; the update reads and
+// writes 4 B per weight (hi + lo) instead of fp32 W + the bf16 copy (4 + 4 +
+// 2 B): 20 % fewer bytes in this HBM-bound kernel.
+__device__ __forceinline__ float hl_join(uint32_t h, uint32_t l) {
+  return __uint_as_float((h << 16) + (uint32_t)(int32_t)(int16_t)l);
+}
+__device__ __forceinline__ uint32_t hl_hi(float v) { return (__float_as_uint(v) + 0x8000u) >> 16; }
+__device__ __forceinline__ uint32_t hl_lo(float v, uint32_t h) { return (__float_as_uint(v) - (h << 16)) & 0xffffu; }
+// 8 consecutive weights of the split master: hi and lo as one 16-B word each
+// (a lane's accesses stay 16 B wide: the 8-B form halved the bytes per
+// vector-memory instruction and ran no faster than the fp32 form)
+__device__ __forceinline__ void hl_join8(uint4 h, uint4 l, float (&w)[8]) {
+  const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[2 * i] = hl_join(hw[i] & 0xffffu, lw[i] & 0xffffu);
+    w[2 * i + 1] = hl_join(hw[i] >> 16, lw[i] >> 16);
+  }
+}
+__device__ __forceinline__ void hl_store8(const WgArgs& a, int nr, int kc, const float (&w)[8]) {
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t h0 = hl_hi(w[2 * i]), h1 = hl_hi(w[2 * i + 1]);
+    hw[i] = h0 | (h1 << 16);
+    lw[i] = hl_lo(w[2 * i], h0) | (hl_lo(w[2 * i + 1], h1) << 16);
+  }
+  __builtin_nontemporal_store(wg_u4{hw[0], hw[1], hw[2], hw[3]},
+                              reinterpret_cast<wg_u4*>(a.Wb + (int64_t)nr * a.ldwb + kc));
+  __builtin_nontemporal_store(wg_u4{lw[0], lw[1], lw[2], lw[3]},
+                              reinterpret_cast<wg_u4*>(a.Wl + (int64_t)nr * a.ldwl + kc));
+}
 
 // Several layers' weight gradients in ONE launch (flattened tile grid): the
 // step's last kernel updates every layer, one launch ramp and tail instead of
@@ -77,6 +114,18 @@ __device__ __forceinline__ void wg_load_w(const WgArgs& a, int kt, int nt, float
                           : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
+// 1'. split master: rows (tid >> 3) + 32 j, columns 8 (tid & 7) .. +7 (one 16-B hi
+// and one 16-B lo word per row: 8 lanes cover a tile row's 128 B)
+__device__ __forceinline__ void wg_load_hl(const WgArgs& a, int kt, int nt, uint4 (&w)[4]) {
+  const int tid = threadIdx.x, kc = kt * 64 + 8 * (tid & 7);
+  const bool kv = kc < a.K;  // K % 8 == 0 in this form
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nr = min(nt * 64 + (tid >> 3) + 32 * j, a.N - 1);
+    w[2 * j] = kv ? *reinterpret_cast<const uint4*>(a.Wh + (int64_t)nr * a.ldwh + kc) : make_uint4(0u, 0u, 0u, 0u);
+    w[2 * j + 1] = kv ? *reinterpret_cast<const uint4*>(a.Wl + (int64_t)nr * a.ldwl + kc) : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
 
 // 2. Z[mb.., n0..] and X[mb.., k0..] as row-major images: 2 LDS-DMA pieces per wave each
 __device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb, char* lds) {
@@ -100,7 +149,7 @@ __device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb
 // 2-4. One 64 (n) x 64 (k) tile of layer `a` (k tile kt, n tile nt) whose W
 // loads are already in flight in `wold`.
 __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt, char* lds,
-                                                const float4 (&wold)[4]) {
+                                                const uint4 (&wr)[4]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int k0 = kt * 64, n0 = nt * 64;
   char* imz = lds;
@@ -185,7 +234,7 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
       if (nr >= a.N) continue;
       const float4 gv = *reinterpret_cast<const float4*>(tile + (rl + 16 * j) * kWgPitch + cl);
       if (a.W) {
-        float4 v = wold[j];
+        float4 v = __builtin_bit_cast(float4, wr[j]);
         v.x -= a.lr * gv.x; v.y -= a.lr * gv.y; v.z -= a.lr * gv.z; v.w -= a.lr * gv.w;
         __builtin_nontemporal_store(wg_f4{v.x, v.y, v.z, v.w},
                                     reinterpret_cast<wg_f4*>(a.W + (int64_t)nr * a.ldw + kc));
@@ -200,6 +249,23 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
       }
     }
   }
+  if (a.Wl) {  // split master: 8 consecutive weights per 16-B word
+    const int kc8 = k0 + 8 * (tid & 7);
+    if (kc8 < a.K) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rr = (tid >> 3) + 32 * j, nr = n0 + rr;
+        if (nr >= a.N) continue;
+        const float4 g0 = *reinterpret_cast<const float4*>(tile + rr * kWgPitch + 8 * (tid & 7));
+        const float4 g1 = *reinterpret_cast<const float4*>(tile + rr * kWgPitch + 8 * (tid & 7) + 4);
+        float w[8];
+        hl_join8(wr[2 * j], wr[2 * j + 1], w);
+        w[0] -= a.lr * g0.x; w[1] -= a.lr * g0.y; w[2] -= a.lr * g0.z; w[3] -= a.lr * g0.w;
+        w[4] -= a.lr * g1.x; w[5] -= a.lr * g1.y; w[6] -= a.lr * g1.z; w[7] -= a.lr * g1.w;
+        hl_store8(a, nr, kc8, w);
+      }
+    }
+  }
   if (kt == 0 && tid < 64 && n0 + tid < a.N) {
     const float db = a.alpha * (((bsum[tid] + bsum[64 + tid]) + bsum[128 + tid]) + bsum[192 + tid]);
     if (a.bias) a.bias[n0 + tid] -= a.lr * db;
@@ -208,14 +274,45 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
 }
 
 __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
-  float4 wold[4];
-  wg_load_w(a, kt, nt, wold);
-  wgrad_tile_body(a, kt, nt, lds, wold);
+  // the tile's W words in one register set: fp32 W (4 float4), or for the
+  // split master {hi, lo} of rows (tid >> 3) and (tid >> 3) + 32
+  uint4 wr[4];
+  if (a.Wl) {
+    wg_load_hl(a, kt, nt, wr);
+  } else {
+    float4 wold[4];
+    wg_load_w(a, kt, nt, wold);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wr[j] = __builtin_bit_cast(uint4, wold[j]);
+  }
+  wgrad_tile_body(a, kt, nt, lds, wr);
 }
 
 __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
   wgrad_tile(a, blockIdx.x, blockIdx.y, lds);
+}
+
+// XCD-aware tile order (speed only): blocks b and b + 8 share an XCD under
+// round-robin dispatch, and each XCD has its own 4 MiB L2.  At M = 64 N rows
+// a layer's operands (Z: M x N, X: M x K bf16) outgrow one L2 for N >= 4
+// (8 MB at N = 8 for 4096 x 4096), and every 64 x 64 W tile reads its M-row
+// column blocks of both.  So the 8 XCDs take a 2 (n) x 4 (k) grid of tile
+// blocks: each XCD's tiles read 1/2 of Z's columns and 1/4 of X's (3 MB at
+// N = 8), which its L2 then serves, instead of every XCD cycling through all
+// of both from the shared last-level cache.  Layers whose tile grid does not
+// split that way keep the row-major order.
+__device__ __forceinline__ void wg_tile_xcd(int t, int kts, int nts, int& kt, int& nt) {
+  const int T = kts * nts;
+  if ((T & 7) == 0 && (nts & 1) == 0 && (kts & 3) == 0) {
+    const int x = t & 7, r = t >> 3;
+    const int bn = nts >> 1, bk = kts >> 2;  // tile block of one XCD: bn x bk tiles
+    nt = (x >> 2) * bn + r / bk;
+    kt = (x & 3) * bk + r % bk;
+  } else {
+    kt = t % kts;
+    nt = t / kts;
+  }
 }
 
 __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
@@ -233,30 +330,323 @@ __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
 #pragma unroll
   for (int q = 1; q < kWgMaxLayers; ++q)
     if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
-  wgrad_tile(a, t % kts, t / kts, lds);
+  int kt, nt;
+  // a layer's first block must sit at a multiple of 8 for its XCD map to hold
+  if ((m.start[j] & 7) == 0) wg_tile_xcd(t, kts, (a.N + 63) / 64, kt, nt);
+  else { kt = t % kts; nt = t / kts; }
+  wgrad_tile(a, kt, nt, lds);
 }
 
-// Tile selection of the flattened multi-layer grid (probe kernels below).
-__device__ __forceinline__ void wg_pick(const WgMulti& m, int b, WgArgs& a, int& kt, int& nt) {
+// ---------------------------------------------------------------------------
+// Large-tile form: one 128 (n) x 128 (k) tile per workgroup.  Against the
+// 64 x 64 tiles above it reads the activation operands once per 128 x 128 W
+// elements instead of once per 64 x 64 -- half the operand bytes per W byte,
+// which is what the global-batch update (xact: M = 64 N rows) pays for: 0.4 M
+// / T operand bytes per W byte at tile T.  The batch streams through a 4-slot
+// LDS ring of 32-row blocks (Z and X images, 16 KiB a slot) with three
+// blocks in flight at every wait, so a tile's chain is about one DMA latency
+// plus the MFMAs, not M / 64 dependent rounds; the fp32 W tile's loads are
+// issued right after the first blocks' DMA and retire under the batch loop.
+//
+// The block waits are counted: the wave knows how many vector-memory loads
+// it issued after the block it needs (4 LDS-DMA per block, the 16 (+1) W /
+// bias loads; loads return in order; the tile has no stores before its
+// epilogue) and waits with vmcnt(that).  Every LDS access of the loop is
+// inline asm: the compiler cannot see which LDS bytes a DMA writes, and its
+// own waits before LDS accesses would be vmcnt(0), draining the ring.
+// ---------------------------------------------------------------------------
+constexpr int kBgT = 128;
+constexpr int kBgR = 4;                          // ring slots: 32-row batch blocks
+constexpr int kBgSlot = 2 * 32 * 256;            // Z + X images of one block (256-B rows): 16 KiB
+constexpr int kBgPitch = 132;                    // floats per row of the fp32 epilogue tile
+constexpr int kBgTile = kBgT * kBgPitch * 4;     // 67,584 B, aliasing the ring after the loop
+constexpr int kBgLds = kBgTile + 4 * kBgT * 4;   // + the bias partials [4][128]
+static_assert(kBgTile >= kBgR * kBgSlot, "LDS carve");
+
+// 16-B chunk swizzle of a 256-B image row: the 8 rows one half-wave of a
+// transposing read touches (r & 3 and bit 3 vary) land in 8 different 32-B
+// bank groups.
+__device__ __forceinline__ int bg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+__device__ __forceinline__ wg_u2 bg_dstr(uint32_t addr) {
+  wg_u2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ uint32_t bg_dsr_u16(uint32_t addr) {
+  uint32_t v;
+  asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n, rounded down to a multiple of 4
+// (waiting for more is always safe); n >= 64: nothing to wait for (a wave
+// never has more than 63 vector-memory instructions outstanding).
+__device__ __forceinline__ void bg_vm_wait(int n) {
+  switch (n < 0 ? 0 : n >> 2) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+    default: break;
+  }
+}
+
+// LDS-DMA of batch block s (rows 32 s ..) of the tile: Z[.., n0 ..+127] and
+// X[.., k0 ..+127]; wave w stages rows 8w .. 8w+7 of both (4 instructions).
+__device__ __forceinline__ void bg_stage(const WgArgs& a, int k0, int n0, int s, char* slot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nmax = (int)((a.N + 7) & ~7) - 8, kmax = (int)((a.K + 7) & ~7) - 8;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 8 * w + 4 * j + (lane >> 4), pc = lane & 15;
+    const int m = min(32 * s + r, a.M - 1);
+    const int c = 8 * (pc ^ bg_swz(r));
+    __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + min(n0 + c, nmax)),
+                                     (wg_lptr)(slot + (8 * w + 4 * j) * 256), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + min(k0 + c, kmax)),
+                                     (wg_lptr)(slot + 8192 + (8 * w + 4 * j) * 256), 16, 0, 0);
+  }
+}
+
+// One 32-row block's MFMAs: wave (wn, wk) owns a 64 x 64 quadrant, 4 x 4
+// tiles of 16 x 16, one 32-row reduction step.
+__device__ __forceinline__ void bg_compute(uint32_t iz, int mrow0, int M, int wn, int wk, int lane,
+                                           f32x4 (&acc)[4][4]) {
+  const uint32_t ix = iz + 8192;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  wg_u2 zl[4], zh[4], xl[4], xh[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int ch = ((wn + 16 * x) >> 3) + (p >> 1);
+    zl[x] = bg_dstr(iz + r0 * 256 + 16 * (ch ^ bg_swz(r0)) + 8 * (p & 1));
+    zh[x] = bg_dstr(iz + r1 * 256 + 16 * (ch ^ bg_swz(r1)) + 8 * (p & 1));
+  }
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    const int ch = ((wk + 16 * y) >> 3) + (p >> 1);
+    xl[y] = bg_dstr(ix + r0 * 256 + 16 * (ch ^ bg_swz(r0)) + 8 * (p & 1));
+    xh[y] = bg_dstr(ix + r1 * 256 + 16 * (ch ^ bg_swz(r1)) + 8 * (p & 1));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(zl[0]), "+v"(zl[1]), "+v"(zl[2]), "+v"(zl[3]), "+v"(zh[0]), "+v"(zh[1]),
+                 "+v"(zh[2]), "+v"(zh[3]), "+v"(xl[0]), "+v"(xl[1]), "+v"(xl[2]), "+v"(xl[3]),
+                 "+v"(xh[0]), "+v"(xh[1]), "+v"(xh[2]), "+v"(xh[3])::"memory");
+  uint4 fz[4], fx[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    fz[x] = make_uint4(zl[x].x, zl[x].y, zh[x].x, zh[x].y);
+    fx[x] = make_uint4(xl[x].x, xl[x].y, xh[x].x, xh[x].y);
+  }
+  if (mrow0 + 32 > M) {  // batch tail: rows >= M (clamped copies) contribute 0
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      uint32_t* e = reinterpret_cast<uint32_t*>(&fz[x]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (mrow0 + 8 * g + t >= M) e[t >> 1] &= (t & 1) ? 0x0000ffffu : 0xffff0000u;
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, fz[x]),
+                                                          __builtin_bit_cast(wg_bf16x8, fx[y]),
+                                                          acc[x][y], 0, 0, 0);
+}
+
+__device__ __forceinline__ void wgrad_big_tile(const WgArgs& a, int kt, int nt, char* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k0 = kt * kBgT, n0 = nt * kBgT;
+  const int wn = (w >> 1) * 64, wk = (w & 1) * 64;
+  const int nb = (a.M + 31) / 32;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(wg_lptr)lds;
+  // epilogue map: float4 column group c4, rows r8 + 8j (two full 512-B rows per wave instruction)
+  const int c4 = tid & 31, r8 = tid >> 5;
+  const int kc = k0 + 4 * c4;
+  const bool kv = kc < a.K;  // K % 4 == 0: a 4-column group is whole or absent
+  // blocks 0 .. R-2 first, then the W loads; e[] = loads issued up to each block in flight
+  int issued = 0, e[kBgR - 1];
+#pragma unroll
+  for (int q = 0; q < kBgR - 1; ++q) {
+    if (q < nb) { bg_stage(a, k0, n0, q, lds + q * kBgSlot); issued += 4; }
+    e[q] = issued;
+  }
+  asm volatile("" ::: "memory");  // the W loads follow the DMA in issue order
+  // the W tile's raw words: fp32 W (rows r8 + 8j, 4 columns at kc), or for the
+  // split master 8 hi + 8 lo words (rows (tid >> 4) + 16 j', 8 columns at kc8)
+  uint4 wraw[16];
+  const int kc8 = k0 + 8 * (tid & 15);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (a.W) {
+      const int nr = min(n0 + r8 + 8 * j, a.N - 1);
+      wraw[j] = *reinterpret_cast<const uint4*>(a.W + (int64_t)nr * a.ldw + min(kc, a.K - 4));
+    } else if (a.Wl) {
+      const int nr = min(n0 + (tid >> 4) + 16 * (j >> 1), a.N - 1), k8 = min(kc8, a.K - 8);
+      wraw[j] = (j & 1) ? *reinterpret_cast<const uint4*>(a.Wl + (int64_t)nr * a.ldwl + k8)
+                        : *reinterpret_cast<const uint4*>(a.Wh + (int64_t)nr * a.ldwh + k8);
+    } else {
+      wraw[j] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  if (a.W || a.Wl) issued += 16;
+  asm volatile("" ::: "memory");
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = {0.f, 0.f, 0.f, 0.f};
+  // bias column sums, in the 64 x 64 body's order (16-row groups of every
+  // 64-row block summed over the blocks, then group 0 + 1 + 2 + 3): column
+  // bc; this thread's groups: bh in even 32-row blocks, 2 + bh in odd ones
+  float dA = 0.f, dB = 0.f;
+  const int bc = tid & 127, bh = tid >> 7;
+  for (int s = 0; s < nb; ++s) {
+    bg_vm_wait(issued - e[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // block s landed for every wave; slot (s-1) % R free
+#pragma unroll
+    for (int k = 0; k < kBgR - 2; ++k) e[k] = e[k + 1];
+    if (s + kBgR - 1 < nb) { bg_stage(a, k0, n0, s + kBgR - 1, lds + ((s + kBgR - 1) % kBgR) * kBgSlot); issued += 4; }
+    e[kBgR - 2] = issued;
+    const uint32_t slot = lds0 + (s % kBgR) * kBgSlot;
+    bg_compute(slot, 32 * s, a.M, wn, wk, lane, acc);
+    if (kt == 0) {
+      const int ch = bc >> 3, el = bc & 7;
+      uint32_t v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = 16 * bh + r;
+        v[r] = bg_dsr_u16(slot + rr * 256 + 16 * (ch ^ bg_swz(rr)) + 2 * el);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                     "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]),
+                     "+v"(v[13]), "+v"(v[14]), "+v"(v[15])::"memory");
+      if (s & 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (32 * s + 16 * bh + r < a.M) dB += __uint_as_float(v[r] << 16);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (32 * s + 16 * bh + r < a.M) dA += __uint_as_float(v[r] << 16);
+      }
+    }
+  }
+  // every wave out of the ring (and every load retired) before the tile overwrites it
+  full_barrier();
+  float* tile = reinterpret_cast<float*>(lds);
+  {
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(wn + 16 * x + 4 * g + r) * kBgPitch + wk + 16 * y + i] = acc[x][y][r] * a.alpha;
+  }
+  float* bsum = reinterpret_cast<float*>(lds + kBgTile);
+  if (kt == 0) { bsum[bh * kBgT + bc] = dA; bsum[(2 + bh) * kBgT + bc] = dB; }
+  lds_barrier();
+  if (kv) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int nr = n0 + r8 + 8 * j;
+      if (nr >= a.N) continue;
+      const float4 gv = *reinterpret_cast<const float4*>(tile + (r8 + 8 * j) * kBgPitch + 4 * c4);
+      if (a.W) {
+        float4 v = __builtin_bit_cast(float4, wraw[j]);
+        v.x -= a.lr * gv.x; v.y -= a.lr * gv.y; v.z -= a.lr * gv.z; v.w -= a.lr * gv.w;
+        __builtin_nontemporal_store(wg_f4{v.x, v.y, v.z, v.w},
+                                    reinterpret_cast<wg_f4*>(a.W + (int64_t)nr * a.ldw + kc));
+        if (a.Wb) {
+          const uint32_t lo = f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
+          const uint32_t hi = f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+          __builtin_nontemporal_store(wg_u2{lo, hi},
+                                      reinterpret_cast<wg_u2*>(a.Wb + (int64_t)nr * a.ldwb + kc));
+        }
+      } else if (a.G) {
+        *reinterpret_cast<float4*>(a.G + (int64_t)nr * a.ldg + kc) = gv;
+      }
+    }
+  }
+  if (a.Wl && kc8 < a.K) {  // split master: 8 consecutive weights per 16-B word
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int rr = (tid >> 4) + 16 * j, nr = n0 + rr;
+      if (nr >= a.N) continue;
+      const float4 g0 = *reinterpret_cast<const float4*>(tile + rr * kBgPitch + 8 * (tid & 15));
+      const float4 g1 = *reinterpret_cast<const float4*>(tile + rr * kBgPitch + 8 * (tid & 15) + 4);
+      float w[8];
+      hl_join8(wraw[2 * j], wraw[2 * j + 1], w);
+      w[0] -= a.lr * g0.x; w[1] -= a.lr * g0.y; w[2] -= a.lr * g0.z; w[3] -= a.lr * g0.w;
+      w[4] -= a.lr * g1.x; w[5] -= a.lr * g1.y; w[6] -= a.lr * g1.z; w[7] -= a.lr * g1.w;
+      hl_store8(a, nr, kc8, w);
+    }
+  }
+  if (kt == 0 && tid < kBgT && n0 + tid < a.N) {
+    const float db = a.alpha * (((bsum[tid] + bsum[kBgT + tid]) + bsum[2 * kBgT + tid]) + bsum[3 * kBgT + tid]);
+    if (a.bias) a.bias[n0 + tid] -= a.lr * db;
+    if (a.bgrad) a.bgrad[n0 + tid] = db;
+  }
+}
+
+// Flattened grid over the layers; big[j] selects the 128 x 128 tile for layer j
+// (the 64 x 64 body otherwise: a 10-row classifier layer is one tile row).
+struct WgMultiBig {
+  WgMulti m;
+  int big[kWgMaxLayers];
+};
+
+__global__ __launch_bounds__(256) void wgrad_multi_big_k(WgMultiBig mb) {
+  __shared__ __attribute__((aligned(16))) char lds[kBgLds];
+  const WgMulti& m = mb.m;
+  const int b = blockIdx.x;
   int j = 0;
 #pragma unroll
   for (int q = 1; q < kWgMaxLayers; ++q)
     if (q < m.n && b >= m.start[q]) j = q;
   const int t = b - m.start[j];
-  a = m.l[0];
-  int kts = m.ktiles[0];
+  WgArgs a = m.l[0];
+  int kts = m.ktiles[0], big = mb.big[0];
 #pragma unroll
   for (int q = 1; q < kWgMaxLayers; ++q)
-    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
-  kt = t % kts;
-  nt = t / kts;
+    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; big = mb.big[q]; }
+  const int nts = big ? (a.N + kBgT - 1) / kBgT : (a.N + 63) / 64;
+  int kt, nt;
+  if ((m.start[j] & 7) == 0) wg_tile_xcd(t, kts, nts, kt, nt);
+  else { kt = t % kts; nt = t / kts; }
+  if (big) wgrad_big_tile(a, kt, nt, lds);
+  else wgrad_tile(a, kt, nt, lds);
 }
+
 
 bool wg_valid(const WgArgs& a) {
   if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
       a.ldz < ((a.N + 7) & ~7) || a.ldx < ((a.K + 7) & ~7) || (((uintptr_t)a.Z | (uintptr_t)a.X) & 15))
     return false;
-  if (a.W == nullptr && a.G == nullptr && a.bias == nullptr && a.bgrad == nullptr) return false;
+  if (a.W == nullptr && a.Wl == nullptr && a.G == nullptr && a.bias == nullptr && a.bgrad == nullptr)
+    return false;
+  // split master: the current hi words in, the next step's hi copy and lo (in place) out
+  if (a.Wl && (a.W || a.Wh == nullptr || a.Wb == nullptr || (a.K & 7) ||
+               (((uintptr_t)a.Wh | (uintptr_t)a.Wl | (uintptr_t)a.Wb) & 15) || (a.ldwh & 7) || (a.ldwl & 7) ||
+               (a.ldwb & 7)))
+    return false;
   if ((a.W && (((uintptr_t)a.W & 15) || (a.ldw & 3))) || (a.Wb && (((uintptr_t)a.Wb & 7) || (a.ldwb & 3))) ||
       (a.G && (((uintptr_t)a.G & 15) || (a.ldg & 3))))
     return false;
@@ -274,21 +664,100 @@ hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t 
   return hipGetLastError();
 }
 
-hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s) {
-  if (n < 1 || n > kWgMaxLayers) return hipErrorInvalidValue;
-  WgMulti m{};
+hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile) {
+  if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT)) return hipErrorInvalidValue;
+  WgMultiBig mb{};
+  WgMulti& m = mb.m;
   m.n = n;
-  int t = 0;
+  int t = 0, any_big = 0;
   for (int j = 0; j < n; ++j) {
-    if (!wg_valid(layers[j])) return hipErrorInvalidValue;
-    m.l[j] = layers[j];
+    const WgLayer& L = layers[j];
+    if (!wg_valid(L)) return hipErrorInvalidValue;
+    // 128 x 128 tiles where the layer fills them (a 10-row classifier does
+    // not) and, by default, only for the fp32-master form at a long batch: the
+    // 64 x 64 body's 5 workgroups per CU hide the W round trip better
+    // (MI355X, 784-4096-4096-10 shapes, us at M = 64 / 128 / 256 / 512: fp32
+    // form 34.9 / 40.2 / 54.7 / 78.6 against 39.7 / 45.5 / 55.6 / 74.9; split
+    // master 31.3 / 36.7 / 48.9 / 72.8 against 38.2 / 43.4 / 53.6 / 74.7 --
+    // profiles/r3_wide_xact_cost.json)
+    const int big = L.N >= kBgT && L.K >= kBgT &&
+                    (tile == kBgT || (tile == 0 && L.M >= 512 && L.W != nullptr));
+    const int T = big ? kBgT : 64;
+    mb.big[j] = big;
+    any_big |= big;
+    m.l[j] = L;
     m.start[j] = t;
-    m.ktiles[j] = (layers[j].K + 63) / 64;
-    t += m.ktiles[j] * ((layers[j].N + 63) / 64);
+    m.ktiles[j] = (L.K + T - 1) / T;
+    t += m.ktiles[j] * ((L.N + T - 1) / T);
   }
   for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
-  for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
-  hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
+  for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; mb.big[j] = mb.big[0]; }
+  if (any_big)
+    hipLaunchKernelGGL(wgrad_multi_big_k, dim3(t), dim3(256), 0, s, mb);
+  else
+    hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
+  return hipGetLastError();
+}
+
+
+namespace {
+__global__ void hilo_split_k(const float* __restrict__ W, int N, int K, int64_t ldw, uint16_t* __restrict__ hi,
+                             int64_t ldh, uint16_t* __restrict__ lo, int64_t ldl) {
+  const int64_t total = (int64_t)N * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / K, k = e - n * K;
+    const float v = W[n * ldw + k];
+    const uint32_t h = hl_hi(v);
+    hi[n * ldh + k] = (uint16_t)h;
+    lo[n * ldl + k] = (uint16_t)hl_lo(v, h);
+  }
+}
+__global__ void hilo_join_k(const uint16_t* __restrict__ hi, int64_t ldh, const uint16_t* __restrict__ lo,
+                            int64_t ldl, int N, int K, float* __restrict__ W, int64_t ldw) {
+  const int64_t total = (int64_t)N * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / K, k = e - n * K;
+    W[n * ldw + k] = hl_join(hi[n * ldh + k], lo[n * ldl + k]);
+  }
+}
+__global__ void hilo_sgd_k(const uint16_t* __restrict__ hic, int64_t ldc, uint16_t* __restrict__ lo, int64_t ldl,
+                           const float* __restrict__ G, int64_t ldg, int N, int K, float lr,
+                           uint16_t* __restrict__ hin, int64_t ldn) {
+  const int64_t total = (int64_t)N * K;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / K, k = e - n * K;
+    float w = hl_join(hic[n * ldc + k], lo[n * ldl + k]);
+    if (G) w -= lr * G[n * ldg + k];
+    const uint32_t h = hl_hi(w);
+    hin[n * ldn + k] = (uint16_t)h;
+    lo[n * ldl + k] = (uint16_t)hl_lo(w, h);
+  }
+}
+}  // namespace
+
+hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl, const float* G, int64_t ldg,
+                    int N, int K, float lr, uint16_t* hin, int64_t ldn, hipStream_t s) {
+  if (N <= 0 || K <= 0) return hipSuccess;
+  const int64_t total = (int64_t)N * K;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(hilo_sgd_k, dim3(grid), dim3(256), 0, s, hic, ldc, lo, ldl, G, ldg, N, K, lr, hin, ldn);
+  return hipGetLastError();
+}
+
+hipError_t hilo_split(const float* W, int N, int K, int64_t ldw, uint16_t* hi, int64_t ldh, uint16_t* lo,
+                      int64_t ldl, hipStream_t s) {
+  if (N <= 0 || K <= 0) return hipSuccess;
+  const int64_t total = (int64_t)N * K;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(hilo_split_k, dim3(grid), dim3(256), 0, s, W, N, K, ldw, hi, ldh, lo, ldl);
+  return hipGetLastError();
+}
+hipError_t hilo_join(const uint16_t* hi, int64_t ldh, const uint16_t* lo, int64_t ldl, int N, int K, float* W,
+                     int64_t ldw, hipStream_t s) {
+  if (N <= 0 || K <= 0) return hipSuccess;
+  const int64_t total = (int64_t)N * K;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(hilo_join_k, dim3(grid), dim3(256), 0, s, hi, ldh, lo, ldl, N, K, W, ldw);
   return hipGetLastError();
 }
 

@@ -1,9 +1,14 @@
 """Wide-MLP engine (BASELINE config 4: MLP 784-4096-4096-10, bf16 on MI355X).
 
-Mixed precision: fp32 master weights (flat, same layout as models/mlp.py),
-ONE bf16 copy of each W in its stored [out][in] layout (refreshed by the
-weight-gradient kernel's SGD epilogue), bf16 activations, fp32 accumulation,
-fp32 gradients all-reduced across replicas.  No transposed copy of anything:
+Mixed precision: fp32 master weights, bf16 activations, fp32 accumulation,
+fp32 gradients all-reduced across replicas.  Each fp32 master W is stored
+SPLIT, losslessly: its bf16 high half (rounded half away from zero) IS the
+bf16 copy the GEMMs read, in W's stored [out][in] layout, and an int16
+remainder holds the rest of the bits (kernels/wgrad_sgd.hip hl_*).  The
+update reads and writes 4 B per weight instead of fp32 W + a separate bf16
+copy (10 B): 20 % fewer bytes in the HBM-bound weight-update kernel.  The
+flat fp32 parameter vector (models/mlp.py layout) holds the biases; its
+weight part is rebuilt from the split masters on demand (`params()`).  No transposed copy of anything:
 the products that reduce over a strided dimension read their operand through
 gfx950's transposing LDS read (ds_read_b64_tr_b16).
 
@@ -91,8 +96,8 @@ class WideMlpTrainer:
         self.Xb = torch.zeros(self.nbatches * batch, _rup(spec.dims[0], 16), dtype=torch.bfloat16,
                               device=dev)
         self.C.cast_transpose(self.X, self.nbatches * batch, spec.dims[0], self.Xb, None)
-        self.P = init_params(self.layout, seed, init).to(dev)
-        self.G = torch.zeros_like(self.P)
+        self._P = init_params(self.layout, seed, init).to(dev)
+        self.G = torch.zeros_like(self._P)
         bf = dict(dtype=torch.bfloat16, device=dev)
         # bf16 W_l with rows padded to 16 (zeros: the dgrad reads a whole K tile of
         # rows), double-buffered by step parity: step s reads Wb[l][s % 2] (forward,
@@ -101,6 +106,9 @@ class WideMlpTrainer:
         # concurrently with the dgrad chain that still reads the old weights.
         self.Wb = [[torch.zeros(self.pd[l + 1], self.pd[l], **bf) for _ in range(2)]
                    for l in range(L)]
+        # the int16 remainders of the split fp32 masters (updated in place)
+        self.Wlo = [torch.zeros(self.pd[l + 1], self.pd[l], dtype=torch.int16, device=dev)
+                    for l in range(L)]
         self.H = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L)]
         self.dZ = [None] + [torch.zeros(batch, self.pd[l], **bf) for l in range(1, L + 1)]
         self.xact = self.ctx.is_distributed and sync == "xact"
@@ -108,7 +116,7 @@ class WideMlpTrainer:
         # per-row loss / correct / count accumulators (the head kernel's row_stats
         # form: no same-address atomics), summed by read_stats
         self.stats = torch.zeros(batch * 4, dtype=torch.float32, device=dev)
-        self.views = self.layout.views(self.P)
+        self.views = self.layout.views(self._P)
         self.gviews = self.layout.views(self.G)
         self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
         # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
@@ -231,12 +239,24 @@ class WideMlpTrainer:
         return self.Xb[b * self.batch:(b + 1) * self.batch]
 
     def _refresh_bf16(self) -> None:
-        """Both bf16 copies of every W_l from the fp32 masters."""
-        d = self.spec.dims
+        """Split masters (both hi copies + the remainders) from the fp32 W in P."""
         for l in range(self.L):
             W, _ = self.views[l]
-            for buf in self.Wb[l]:
-                self.C.sgd_cast(W, None, d[l + 1], d[l], 0.0, buf, None)
+            self.C.hilo_split(W, self.Wb[l][0], self.Wlo[l])
+            self.Wb[l][1].copy_(self.Wb[l][0])
+
+    def params(self) -> torch.Tensor:
+        """The flat fp32 parameter vector, its weights rebuilt from the split
+        masters (exact: the split is lossless)."""
+        with torch.cuda.device(self.device):
+            for l in range(self.L):
+                W, _ = self.views[l]
+                self.C.hilo_join(self.wb(l), self.Wlo[l], W)
+        return self._P
+
+    @property
+    def P(self) -> torch.Tensor:
+        return self.params()
 
     def wb(self, l: int) -> torch.Tensor:
         """The bf16 copy of W_l the next step reads."""
@@ -303,7 +323,7 @@ class WideMlpTrainer:
             for l in range(L - 1, -1, -1):
                 W, b = self.views[l]
                 layers.append((self.dZall[l + 1], Hall0 if l == 0 else self.Hall[l], M, d[l + 1], d[l],
-                               1.0 / n, self.lr, W, nxt[l], None, b, None))
+                               1.0 / n, self.lr, None, nxt[l], None, b, None, cur[l], self.Wlo[l]))
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1
@@ -317,8 +337,8 @@ class WideMlpTrainer:
             layers = []
             for l in range(L - 1, -1, -1):
                 W, b = self.views[l]
-                layers.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, W, nxt[l],
-                               None, b, None))
+                layers.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l],
+                               None, b, None, cur[l], self.Wlo[l]))
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1
@@ -334,17 +354,17 @@ class WideMlpTrainer:
                 if l > 0 and self._ss is not None:
                     self._ss.wait_stream(main)
                     with torch.cuda.stream(self._ss):
-                        C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale, W=W,
-                                    Wb=nxt[l], bias=b)
+                        C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale,
+                                    Wb=nxt[l], bias=b, Wh=cur[l], Wl=self.Wlo[l])
                 else:
-                    C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale, W=W,
-                                Wb=nxt[l], bias=b)
+                    C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale,
+                                Wb=nxt[l], bias=b, Wh=cur[l], Wl=self.Wlo[l])
             if l > 0 and not (self.fused_head and l == L - 1):
                 # activation gradient (reads this step's W_l copy, not the one being written)
                 self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
             if not fused_sgd:
                 C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], G=gW, bgrad=gb)
-                self._sync_layer(l, scale, nxt[l])
+                self._sync_layer(l, scale, cur[l], nxt[l])
         # join: the next step's forward reads every updated layer (and overwrites
         # the activations the side-stream kernels read)
         side = self._ss if fused_sgd else self._cs
@@ -352,7 +372,7 @@ class WideMlpTrainer:
             main.wait_stream(side)
         self.steps_done += 1
 
-    def _sync_layer(self, l: int, scale: float, wb_next: torch.Tensor) -> None:
+    def _sync_layer(self, l: int, scale: float, wb_cur: torch.Tensor, wb_next: torch.Tensor) -> None:
         """Per-layer gradient bucket: as soon as layer l's weight gradient is
         written, its all-reduce and its SGD + bf16 refresh run on the comm stream
         while the backward of layers < l continues on the compute stream (none of
@@ -377,7 +397,7 @@ class WideMlpTrainer:
                 import torch.distributed as dist
 
                 dist.all_reduce(g)
-            C.sgd_cast(W, gW, d[l + 1], d[l], scale, wb_next, None)
+            C.hilo_sgd(wb_cur, self.Wlo[l], gW, scale, wb_next)
             C.sgd_update_(b, gb, scale)
 
     def _warm_comm(self) -> None:
@@ -444,7 +464,7 @@ class WideMlpTrainer:
 
     def state_dict(self) -> Dict[str, object]:
         self.synchronize()
-        return {"spec": list(self.spec.dims), "params": self.P.detach().cpu().clone(),
+        return {"spec": list(self.spec.dims), "params": self.params().detach().cpu().clone(),
                 "velocity": torch.empty(0), "steps_done": self.steps_done, "lr": self.lr,
                 "batch": self.batch}
 
@@ -452,9 +472,9 @@ class WideMlpTrainer:
         if list(sd["spec"]) != list(self.spec.dims):
             raise ValueError("checkpoint is for a different model")
         self.synchronize()
-        self.P.copy_(sd["params"].to(self.device))
+        self._P.copy_(sd["params"].to(self.device))
         self.steps_done = int(sd["steps_done"])
-        self._refresh_bf16()  # both bf16 GEMM copies from the fp32 masters
+        self._refresh_bf16()  # the split masters from the fp32 weights
         self.synchronize()
 
     @torch.no_grad()

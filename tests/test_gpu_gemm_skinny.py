@@ -116,12 +116,17 @@ def test_wgrad_sgd_matches_fp32(M, N, K):
     assert (db - alpha * Z[:, :N].float().sum(0)).abs().max().item() < 1e-4
 
 
-def test_wgrad_sgd_multi_matches_per_layer_launches():
-    """Three layers' updates in one flattened launch == one launch per layer, bit for bit."""
+@pytest.mark.parametrize("tile,M", [(64, 64), (0, 64), (128, 64), (0, 512), (128, 48), (128, 200),
+                                    (128, 8), (64, 512)])
+def test_wgrad_sgd_multi_matches_per_layer_launches(tile, M):
+    """Three layers' updates in one flattened launch == one launch per layer
+    (64 x 64 tiles), bit for bit -- also with the 128 x 128 tiles (tile 128) of
+    the big layers, whose 32-row batch blocks stream through a 4-slot LDS
+    ring: the same MFMA order per element, the same bias-sum order.  M = 512 is the global batch
+    of the activation-exchange sync at 8 replicas; 48 / 200 have a batch tail."""
     C = require_native()
-    g = torch.Generator(device="cpu").manual_seed(77)
+    g = torch.Generator(device="cpu").manual_seed(77 + M)
     shapes = [(10, 4096), (4096, 4096), (4096, 784)]  # (N, K) of the wide MLP's layers, top down
-    M = 64
     args_a, args_b = [], []
     for N, K in shapes:
         pn, pk = (N + 15) // 16 * 16, (K + 15) // 16 * 16
@@ -134,9 +139,27 @@ def test_wgrad_sgd_multi_matches_per_layer_launches():
         for lst in (args_a, args_b):
             lst.append((Z.to(DEV), X.to(DEV), M, N, K, 1.0, 0.01, W.to(DEV),
                         torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV), None, b.to(DEV), None))
-    C.wgrad_sgd_multi(args_a)
+    C.wgrad_sgd_multi(args_a, tile=tile)
     for (Z, X, M_, N, K, al, lr, W, Wb, G, b, bg) in args_b:
         C.wgrad_sgd(Z, X, M_, N, K, alpha=al, lr=lr, W=W, Wb=Wb, bias=b)
     torch.cuda.synchronize()
     for a, b in zip(args_a, args_b):
         assert torch.equal(a[7], b[7]) and torch.equal(a[8], b[8]) and torch.equal(a[10], b[10])
+
+
+@pytest.mark.parametrize("M", [64, 512])
+def test_wgrad_sgd_multi_big_tiles_gradient_form(M):
+    """The 128 x 128 tiles in the gradient-out form (W = None: G and db written
+    for an all-reduce) against fp32."""
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(5 + M)
+    N, K = 512, 784
+    Z = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    X = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    G = torch.full((N, K), float("nan"), device=DEV)
+    db = torch.zeros(N, device=DEV)
+    C.wgrad_sgd_multi([(Z, X, M, N, K, 0.5, 0.0, None, None, G, None, db)], tile=128)
+    torch.cuda.synchronize()
+    Gref = 0.5 * Z.float().t() @ X.float()
+    assert (G - Gref).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
+    assert (db - 0.5 * Z.float().sum(0)).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)

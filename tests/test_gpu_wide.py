@@ -57,9 +57,19 @@ def test_wide_step_matches_fp32_reference():
     assert rel < 0.05, rel  # bf16 activations / dZ: ~0.4 % per element, compounded over layers
     st = tr.read_stats()
     assert st.count == 64 and abs(st.loss_sum - float(loss_sum)) / float(loss_sum) < 0.02
-    # the bf16 GEMM copies match the updated fp32 master weights
+    # the bf16 GEMM copy IS the high half of the split fp32 master: the
+    # master's bits rounded half away from zero (RNE but at exact ties), and
+    # high half + int16 remainder rebuild the master exactly
     W0, _ = tr.views[0]
-    assert torch.equal(tr.wb(0)[:256, :784].cpu(), W0.cpu().to(torch.bfloat16))
+    bits = W0.cpu().contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    hi = ((bits + 0x8000) >> 16) & 0xFFFF
+    got = tr.wb(0)[:256, :784].cpu().contiguous().view(torch.int16).to(torch.int64) & 0xFFFF
+    assert torch.equal(got, hi)
+    lo = tr.Wlo[0][:256, :784].cpu().to(torch.int64)
+    assert torch.equal(((hi << 16) + lo) & 0xFFFFFFFF, bits)
+    rne = W0.cpu().to(torch.bfloat16).view(torch.int16).to(torch.int64) & 0xFFFF
+    ties = (bits & 0xFFFF) == 0x8000
+    assert torch.equal(got[~ties], rne[~ties])
 
 
 @pytest.mark.parametrize("graph", [False, True])

@@ -20,7 +20,16 @@ pd = [784, 4096, 4096, 16]
 B = 64
 W = [torch.randn(d[l + 1], d[l], device=dev) * 0.01 for l in range(3)]
 Wb = [torch.zeros(pd[l + 1], pd[l], dtype=torch.bfloat16, device=dev) for l in range(3)]
+# the engine's split masters (hi = the bf16 copy, lo = int16 remainder); HILO=0: fp32 W form
+HILO = os.environ.get("HILO", "1") == "1"
+Wh = [torch.zeros(pd[l + 1], pd[l], dtype=torch.bfloat16, device=dev) for l in range(3)]
+Wl = [torch.zeros(pd[l + 1], pd[l], dtype=torch.int16, device=dev) for l in range(3)]
+for l in range(3):
+    C.hilo_split(W[l], Wh[l], Wl[l])
 bias = [torch.zeros(d[l + 1], device=dev) for l in range(3)]
+
+
+TILE = int(os.environ.get("WG_TILE", "0"))
 
 
 def timed(n, reps=30):
@@ -28,15 +37,19 @@ def timed(n, reps=30):
     g = torch.Generator(device=dev).manual_seed(n)
     H = [torch.randn(M, pd[l], device=dev, generator=g).to(torch.bfloat16) for l in range(3)]
     Z = [torch.randn(M, pd[l + 1], device=dev, generator=g).mul(1e-3).to(torch.bfloat16) for l in range(3)]
-    layers = [(Z[l], H[l], M, d[l + 1], d[l], 1.0 / n, 1e-6, W[l], Wb[l], None, bias[l], None)
-              for l in range(2, -1, -1)]
+    if HILO:
+        layers = [(Z[l], H[l], M, d[l + 1], d[l], 1.0 / n, 1e-6, None, Wb[l], None, bias[l], None, Wh[l], Wl[l])
+                  for l in range(2, -1, -1)]
+    else:
+        layers = [(Z[l], H[l], M, d[l + 1], d[l], 1.0 / n, 1e-6, W[l], Wb[l], None, bias[l], None)
+                  for l in range(2, -1, -1)]
     for _ in range(3):
-        C.wgrad_sgd_multi(layers)
+        C.wgrad_sgd_multi(layers, tile=TILE)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(reps):
-        C.wgrad_sgd_multi(layers)
+        C.wgrad_sgd_multi(layers, tile=TILE)
     e1.record()
     torch.cuda.synchronize()
     return round(1e3 * e0.elapsed_time(e1) / reps, 2)
