@@ -816,6 +816,8 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     for (int e = tid; e < 16 * kS3; e += kThreads) DZ2[e] = 0.f;
   }
   float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
+  __shared__ uint32_t s_fail;  // a wave saw a wait give up (set once: the loop then ends)
+  if (tid == 0) s_fail = 0u;
   __syncthreads();
   bool ok = true;
   const bool local = pk_upper_local(a, s0, poll, ok);
@@ -835,12 +837,35 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     const bool rvalid = rb0 + srow < a.batch;
     const int y = rvalid ? a.labels[r0 + rb0 + srow] : -1;
     f4v wv[WSlices<NL>::kIt];
+    // The previous step's updated upper weights (gradient blocks): every wave
+    // checks their 4 flags itself (lanes 0-3, then a wave vote), so no
+    // workgroup barrier -- which would drain the first load batch -- sits
+    // between the two load batches.  Order, measured (r3 stamps): 2 layers,
+    // whose 5 KB of weights are published ~1.8 us before the partials
+    // complete, fetch them FIRST, in flight during the partials wait (step
+    // 7.24 -> 6.96 us); 3 layers, whose 37 KB arrive about when the last
+    // partial does, fetch them after the partials (weights first: 9.56 ->
+    // 10.04 us).
+    auto fetch_w = [&]() {
+      if (it > 0) {
+        bool wok = true;
+        if (lane < kNG) wok = wait_flag(rb, kOffWf + (par ^ 1) * kNG + lane, tag - 1, poll);
+        wok = __builtin_amdgcn_ballot_w64(!wok) == 0;
+        asm volatile("" ::: "memory");
+        if (wok) pk_w_fetch<NL>(a, wv, true, par ^ 1);
+        else ok = false;
+      }
+    };
+    constexpr bool kWFirst = NL == 2;
+    if (kWFirst) fetch_w();
     // ---- H1 rows = relu(sum of the 7 k-partials) ----
     // this chain's 16 rows of every partial in one bulk read: thread -> (gn,
     // column n, 8 rows), 7 gk
     {
       if (tid < kNL1 && !wait_flag(rb, kOffPf + tid, tag, poll)) ok = false;
-      ok = __syncthreads_and(ok ? 1 : 0) != 0;
+      if (!ok) s_fail = 1u;
+      lds_barrier();
+      ok = s_fail == 0u;
       if (!ok) break;
       PK_STAMP(1, 1);
       const int gn = tid >> 5, n = (tid >> 1) & 15, half = tid & 1;
@@ -852,18 +877,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         v[gk][0] = ld_f4(rb, off);
         v[gk][1] = ld_f4(rb, off + 4);
       }
-      // the previous step's updated upper weights (gradient blocks), in flight
-      // together with the partials: every wave checks their 4 flags itself
-      // (lanes 0-3, then a wave vote), so no workgroup barrier -- which would
-      // drain the partial loads first -- sits between the two load batches
-      if (it > 0) {
-        bool wok = true;
-        if (lane < kNG) wok = wait_flag(rb, kOffWf + (par ^ 1) * kNG + lane, tag - 1, poll);
-        wok = __builtin_amdgcn_ballot_w64(!wok) == 0;
-        asm volatile("" ::: "memory");
-        if (wok) pk_w_fetch<NL>(a, wv, true, par ^ 1);
-        else ok = false;
-      }
+      if (!kWFirst) fetch_w();
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float z = 0.f;

@@ -4,7 +4,7 @@ gemm_one.py rows64|splitk4|dwsgd|skinny_nt|skinny_nn|wgrad [N K iters]."""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main() -> int:

@@ -14,7 +14,7 @@ import tempfile
 import torch
 import torch.multiprocessing as mp
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def _worker(rank, world, port, out):

@@ -7,7 +7,7 @@ import time
 
 import torch
 
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
 from hipdsml.data.mnist import synthetic_mnist  # noqa: E402
 from hipdsml.engine.trainer import MlpTrainer  # noqa: E402
 from hipdsml.models.mlp import MlpSpec  # noqa: E402

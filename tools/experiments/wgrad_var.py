@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from hipdsml.data.mnist import synthetic_mnist  # noqa: E402
 from hipdsml.engine.wide import WideMlpTrainer  # noqa: E402
 from hipdsml.models.mlp import MlpSpec  # noqa: E402
