@@ -747,6 +747,13 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   HEAD_STAMP(0);
   const int y = labels[m];
   const float bc = (bias && lane < C) ? bias[lane] : 0.f;
+  // this row's own loss / correct / count accumulators (row_stats: only this
+  // workgroup touches them): read now, under the operand loads, and written
+  // back with one plain store after the softmax -- a read-modify-write with
+  // no round trip of its own (device atomics there kept the kernel's tail
+  // waiting 1.8 us for their completion: head_bench dbg1)
+  const bool rst = row_stats && stats && w == 0 && !(g_head_dbg & 1);
+  float4 racc = rst ? *reinterpret_cast<const float4*>(stats + 4 * (int64_t)m) : make_float4(0.f, 0.f, 0.f, 0.f);
   // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
   uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][kHeadMaxC];
 #pragma unroll
@@ -816,14 +823,10 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     if (c < kHeadMaxC) gz[c] = bf16_to_f32(hq);
     if (c == y && stats && !(g_head_dbg & 1)) {
       if (row_stats) {
-        // this row's own accumulators (stats[4m .. 4m+2]: only this workgroup
-        // adds to them, so no contention): no-return atomics instead of a
-        // read-modify-write, whose load round trip the dZ_{L-1} phase below
-        // (and every other wave, at its barrier) would wait for
-        float* r = stats + 4 * (int64_t)m;
-        __hip_atomic_fetch_add(r + 0, -logf(p + 1e-10f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(r + 1, am == y ? 1.f : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(r + 2, 1.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        racc.x += -logf(p + 1e-10f);
+        racc.y += am == y ? 1.f : 0.f;
+        racc.z += 1.f;
+        *reinterpret_cast<float4*>(stats + 4 * (int64_t)m) = racc;
       } else {
         atomicAdd(stats + 0, -logf(p + 1e-10f));
         atomicAdd(stats + 1, am == y ? 1.f : 0.f);
@@ -891,6 +894,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt,
                              int row_stats) {
   if (dzp && ((ldzp & 7) || ((uintptr_t)dzp & 15))) return hipErrorInvalidValue;
+  if (row_stats && stats && ((uintptr_t)stats & 15)) return hipErrorInvalidValue;  // float4 per row
   if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
       (ldw & 7) ||
       (((uintptr_t)H | (uintptr_t)W) & 15))

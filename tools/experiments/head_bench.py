@@ -18,7 +18,9 @@ logits = torch.empty(B, Cn, device=dev)
 dz = torch.zeros(B, 16, dtype=torch.bfloat16, device=dev)
 dzp = torch.zeros(B, K, dtype=torch.bfloat16, device=dev)
 stats = torch.zeros(4, device=dev)
+rstats = torch.zeros(4 * B, device=dev)  # per-row accumulators, as the wide engine runs it
 nostats = torch.zeros(4, device=dev)
+rstats = torch.zeros(4 * B, device=dev)  # per-row accumulators, as the wide engine runs it
 
 
 def t(fn, iters=50):
@@ -37,6 +39,10 @@ def t(fn, iters=50):
 
 
 out = {
+    "full_row_stats": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, logits, dz, None, rstats,
+                                                    dzp=dzp, row_stats=True)),
+    "no_dzp_row_stats": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, logits, dz, None, rstats,
+                                                      row_stats=True)),
     "full": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, logits, dz, None, stats, dzp=dzp)),
     "no_dzp": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, logits, dz, None, stats)),
     "no_logits_no_dzp": t(lambda: C.head_softmax_xent(H, W, b, B, K, Cn, y, 1.0 / B, None, dz, None, stats)),
