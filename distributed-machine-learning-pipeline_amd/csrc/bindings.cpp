@@ -809,6 +809,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("persist_failed", [](PyMlpRunner& s) { return s.r->persist_failed(); },
            "a persistent launch gave up on a hand-off (valid after a sync; no device copy)")
       .def("clear_persist_error", [](PyMlpRunner& s) { s.r->clear_persist_error(); })
+      .def("set_persist_gram", [](PyMlpRunner& s, torch::Tensor g) {
+        check_f32(g, "gram");
+        TORCH_CHECK(g.is_contiguous() && g.numel() >= (int64_t)s.r->desc().nbatches * 64 * 64,
+                    "gram: contiguous float[nbatches][64][64]");
+        TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr<float>()) & 15) == 0, "gram: 16-B aligned");
+        s.keep.push_back(g);
+        s.r->set_persist_gram(g.data_ptr<float>());
+      }, py::arg("gram"),
+           "single-replica persistent step: the per-batch Gram table G1T[b][m'][m] = "
+           "X_{b-1}[m'] . X_b[m] + 1 (trainer._gram_table)")
+      .def("set_persist_carry", [](PyMlpRunner& s, bool c) { s.r->set_persist_carry(c); }, py::arg("carry"))
+      .def("persist_carry", [](PyMlpRunner& s) { return s.r->persist_carry(); },
+           "the hand-off buffer holds the last launch's pipeline state (next partials + correction)")
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })
       .def("exchange_mode", [](PyMlpRunner& s) { return s.r->exchange_mode(); })
       .def("plan", [](PyMlpRunner& s) {

@@ -98,7 +98,12 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
                              hipStream_t s, const struct XchgArgs* xa = nullptr,
-                             const struct XchgTab* tab = nullptr, int algo = 0);
+                             const struct XchgTab* tab = nullptr, int algo = 0,
+                             const float* gram = nullptr, int carry = 0);
+// Single replica: the Gram table the persistent step reads, float[nbatches][64][64]
+// with G1T[b][m'][m] = X_{b-1}[m'] . X_b[m] + 1 (rows past the batch repeat its
+// last row; b - 1 wraps), and `carry` = 1 when the hand-off buffer still holds
+// the state the previous launch left (nothing rewound or rewrote P since).
 // Data-parallel form (xa->nranks > 1): the receive buffers / flags each replica
 // needs (PeerExchange half >= px_half(n, algo), ntiles >= px_ntiles(n, algo));
 // lr is passed as lr / n.  algo 0: one-shot sum (sync 'pk'), 1: two-shot

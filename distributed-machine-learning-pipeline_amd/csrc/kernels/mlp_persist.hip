@@ -62,6 +62,7 @@ constexpr int kGN = 8, kGK = 7, kKC = kD0 / kGK;        // 112 k per layer-1 blo
 constexpr int kNL1 = kGN * kGK;                         // 56 layer-1 blocks
 constexpr int kNCH = 4, kNG = 4;                        // chains (16 rows each), gradient blocks
 constexpr int kNBlk = kNL1 + kNCH + kNG;                // 64
+constexpr int kNPart = kNL1 + kGN;                      // partial slots: 56 layer-1 + 8 corrections
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
 
@@ -123,14 +124,31 @@ template <> struct GLay<2> {
   static constexpr int B2 = W2 + 16 * kSW;           // [16]
   static constexpr int TOTAL = B2 + 16;
 };
+// Layer-1 block of the single-replica (Gram-corrected) step: three X tiles
+// (X(s) for the backward, X(s+1) for the next forward, X(s+2) in flight), and
+// in the gk == 0 blocks the Gram block G1^T(s+1) = (X(s) X(s+1)^T + 1) [64][64].
+struct L1GLay {
+  static constexpr int X0 = 0;
+  static constexpr int W = X0 + 3 * kB * kKC;         // W1 tile [16][kXS]
+  static constexpr int DZ = W + 16 * kXS;             // dZ1 tile [64][17]
+  static constexpr int B1 = DZ + kB * 17;             // b1 slice [16]
+  static constexpr int G = B1 + 16;                   // G1^T [64 m'][64 m] (LDS-DMA image)
+  static constexpr int TOTAL = G + kB * kB;
+};
+static_assert(L1GLay::G % 4 == 0, "LDS-DMA image must be 16-B aligned");
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int NL>
-constexpr int lds_floats() { return cmax(L1Lay::TOTAL, cmax(ChLay<NL>::TOTAL, GLay<NL>::TOTAL)); }
+constexpr int lds_floats() {
+  return cmax(cmax(L1Lay::TOTAL, L1GLay::TOTAL), cmax(ChLay<NL>::TOTAL, GLay<NL>::TOTAL));
+}
 static_assert(lds_floats<3>() * 4 <= 160 * 1024 && lds_floats<2>() * 4 <= 160 * 1024, "LDS budget");
 
 // ---- hand-off buffer layout (8-byte granules) --------------------------------
-// PART[56][4][16][16] layer-1 partials [block][chain][n][row], plain fp32 (b1
-//                   added by gk == 0), one flag per block and step (PF)
+// PART[2][64][4][16][16] partials [parity][slot][chain][n][row], plain fp32:
+//                   slots 0-55 the layer-1 blocks' k-partials of Z1 (b1 added by
+//                   gk == 0), slots 56-63 (single replica) the Gram corrections
+//                   of the 8 column tiles; one flag per slot, parity and step
+//                   (PF[2][64]).  The data-parallel form uses parity 0, slots < 56.
 // SF[64]            started flags (tag = first step + 1): the step counter is
 //                   handed on only once every block has read it
 // DZ1[64][128]      activation gradient of layer 1, tagged granules
@@ -145,8 +163,8 @@ static_assert(lds_floats<3>() * 4 <= 160 * 1024 && lds_floats<2>() * 4 <= 160 * 
 constexpr int kCX = 16 * kD1 + 16 * kH2 + 16 * kH2 + 16 * 16;  // 4352 floats
 constexpr int kWX = 16 * kD1 + 16 * 16 + 16 + 16;              // 2336 floats
 constexpr int64_t kOffPart = 0;
-constexpr int64_t kOffPf = kOffPart + kNL1 * 16 * kB / 2;
-constexpr int64_t kOffSf = kOffPf + 64;
+constexpr int64_t kOffPf = kOffPart + 2 * kNPart * 16 * kB / 2;
+constexpr int64_t kOffSf = kOffPf + 2 * 64;
 constexpr int64_t kOffDz1 = kOffSf + 64;
 constexpr int64_t kOffCx = kOffDz1 + kB * kD1;
 constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCX / 2;
@@ -282,6 +300,12 @@ struct PersistArgs {
   uint32_t* err;
   uint32_t* herr;  // host-mapped mirror of err (nullable): read without a copy
   uint64_t timeout_ticks;
+  // Single replica: G1^T of every batch, [nbatches][64 m'][64 m] =
+  // X_{b-1}[m'] . X_b[m] + 1 (padding rows repeat the batch's last row), and
+  // whether the hand-off buffer carries the pipeline state of the previous
+  // launch (its last step's next partials and correction, step tags s0 + 1).
+  const float* gram;
+  int32_t carry;
   // Data parallelism over nrep replicas (nrep > 1): every step, each wave's
   // weight-gradient slot is pushed into every peer's receive buffer (xt.buf[d],
   // this replica's slot; parity by step), flagged (xt.flags[d]), and summed
@@ -691,6 +715,254 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   if (lb == 0) PK_EDGE(2);
 }
 
+
+// ---- single replica: the layer-1 blocks off the critical path (Gram form) ----
+// W1(s+1) = W1(s) - lr dZ1(s)^T X(s) and b1(s+1) = b1(s) - lr colsum dZ1(s), so
+//   Z1(s+1) = X(s+1) W1(s+1)^T + b1(s+1)
+//           = [X(s+1) W1(s)^T + b1(s)] - lr (X(s+1) X(s)^T + 1) dZ1(s)
+//           = P(s+1) + C(s+1).
+// P(s+1) needs only W1(s): the layer-1 blocks compute and publish it BEFORE
+// dZ1(s) exists, while the chains still work on step s.  The correction
+// C(s+1) is a [64 x 64] . [64 x 128] product over the Gram block G1 (data
+// only: precomputed per batch on the host): once dZ1(s) arrives, the gk == 0
+// block of each column tile computes its [64 x 16] part (16 MFMAs a wave) and
+// publishes it as an 8th partial.  The chain's critical path becomes chain ->
+// dZ1 -> correction -> chain, instead of chain -> dZ1 -> dW1 + update ->
+// forward -> 57 KB of partials -> chain (r3: 6.3 us of the 9.2 us step).
+// Replicas of a data-parallel job keep the direct form (their W1 update sums
+// every replica's dZ1^T X).
+
+__device__ __forceinline__ int64_t pk_part_off(int par, int slot, int c) {  // floats
+  return kOffPart * 2 + (((int64_t)par * kNPart + slot) * kNCH + c) * 256;
+}
+__device__ __forceinline__ int64_t pk_pf(int par, int slot) { return kOffPf + par * 64 + slot; }
+
+// X tile of step s -> the LDS image at xl (LDS-DMA, as pk_glds_x).
+__device__ __forceinline__ void pk_glds_x_to(const PersistArgs& a, float* xl, uint64_t s, int lane,
+                                             int w, int k0) {
+  const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * a.batch;
+#pragma unroll
+  for (int ch = w; ch < kXF4 / 64; ch += 4) {
+    const int e = ch * 64 + lane;
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    const int64_t row = r0 + min(r, a.batch - 1);
+    __builtin_amdgcn_global_load_lds((pk_gptr)(a.X + row * a.ldx + k0 + 4 * c4),
+                                     (pk_lptr)(xl + ch * 256), 16, 0, 0);
+  }
+}
+// G1^T of the batch of step s -> LDS (16 KiB, 4 LDS-DMA chunks per wave).
+__device__ __forceinline__ void pk_glds_gram(const PersistArgs& a, float* gl, uint64_t s, int lane, int w) {
+  const float* src = a.gram + (int64_t)(s % (uint64_t)a.nbatches) * (kB * kB);
+#pragma unroll
+  for (int ch = w; ch < kB * kB / 256; ch += 4)
+    __builtin_amdgcn_global_load_lds((pk_gptr)(src + ch * 256 + lane * 4), (pk_lptr)(gl + ch * 256), 16, 0, 0);
+}
+// One wave's [16 rows x 16 n] of X . W1_tile^T (+ b1), stored (write-through) to
+// its chain's run of partial slot `slot`, parity `par`; drained by this wave.
+__device__ __forceinline__ void pk_l1_partial(__amdgpu_buffer_rsrc_t rb, const float* Xl, const float* Wl,
+                                              const float* B1, int par, int slot, int w, int i, int q) {
+  f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f},
+                  {0.f, 0.f, 0.f, 0.f}};
+  const float* xa = Xl + (16 * w + i) * kKC + 4 * q;
+  const float* wa = Wl + i * kXS + 4 * q;
+#pragma unroll
+  for (int gq = 0; gq < kKC / 16; ++gq) {
+    const float4 xv = *reinterpret_cast<const float4*>(xa + 16 * gq);
+    const float4 wv = *reinterpret_cast<const float4*>(wa + 16 * gq);
+    acc[0] = mfma_f32_16x16x4(xv.x, wv.x, acc[0]);
+    acc[1] = mfma_f32_16x16x4(xv.y, wv.y, acc[1]);
+    acc[2] = mfma_f32_16x16x4(xv.z, wv.z, acc[2]);
+    acc[3] = mfma_f32_16x16x4(xv.w, wv.w, acc[3]);
+  }
+  const float bn = B1[i];
+  f4v z;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) z[r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]) + bn;
+  st_f4(rb, pk_part_off(par, slot, w) + i * 16 + 4 * q, z);
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
+  const int gn = lb % kGN, gk = lb / kGN;
+  const int n0 = gn * 16, k0 = gk * kKC;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  pk_started(a, blk, s0);
+  float* Wl = lds + L1GLay::W;
+  float* Dz = lds + L1GLay::DZ;
+  float* B1 = lds + L1GLay::B1;
+  float* Gl = lds + L1GLay::G;
+  auto xbuf = [&](uint64_t s) { return lds + L1GLay::X0 + (int)(s % 3u) * (kB * kKC); };
+
+  if (lb == 0) PK_EDGE(0);
+  // ---- prologue: W1 tile, b1 slice, X of the first two steps ----
+  const float* W1g = a.P + a.w_off[0];
+  constexpr int kW1F4 = 16 * (kKC / 4), kW1Per = (kW1F4 + kThreads - 1) / kThreads;
+  float4 w1v[kW1Per];
+#pragma unroll
+  for (int j = 0; j < kW1Per; ++j) {
+    const int e = min(tid + j * kThreads, kW1F4 - 1);
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    w1v[j] = *reinterpret_cast<const float4*>(W1g + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4);
+  }
+  const float b1v = (tid < 16 && gk == 0) ? a.P[a.b_off[0] + n0 + tid] : 0.f;
+#pragma unroll
+  for (int j = 0; j < kW1Per; ++j) {
+    const int e = tid + j * kThreads;
+    if (e < kW1F4) {
+      const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+      *reinterpret_cast<float4*>(Wl + r * kXS + 4 * c4) = w1v[j];
+    }
+  }
+  if (tid < 16) B1[tid] = b1v;
+  pk_glds_x_to(a, xbuf(s0), s0, lane, w, k0);
+  pk_glds_x_to(a, xbuf(s0 + 1), s0 + 1, lane, w, k0);
+  __syncthreads();  // W1 / b1 stores and both X tiles (LDS-DMA, vmcnt) landed
+  if (lb == 0) PK_EDGE(1);
+  if (!a.carry) {
+    // no state from a previous launch: step s0's Z1 directly, correction 0
+    const uint32_t t0 = (uint32_t)(s0 + 1);
+    const int par0 = (int)(s0 & 1);
+    pk_l1_partial(rb, xbuf(s0), Wl, B1, par0, lb, w, i, q);
+    if (gk == 0) {
+      st_f4(rb, pk_part_off(par0, kNL1 + gn, w) + i * 16 + 4 * q, f4v{0.f, 0.f, 0.f, 0.f});
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {
+      st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
+      if (gk == 0) st_gran(rb, pk_pf(par0, kNL1 + gn), __uint_as_float(t0), t0);
+    }
+  }
+
+  bool ok = true;
+  const int stamp_on = g_pk_stamp_on && lb == 0;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    PK_STAMP(0, 0);
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);       // step s
+    const uint32_t tagn = tag + 1;                 // step s + 1
+    const int parn = (int)((s + 1) & 1);
+
+    // ---- P(s+1) = X(s+1) W1(s)^T + b1(s): published before dZ1(s) exists ----
+    pk_l1_partial(rb, xbuf(s + 1), Wl, B1, parn, lb, w, i, q);
+    __syncthreads();
+    if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
+    PK_STAMP(0, 1);
+    // X(s+2) into the third buffer (its last reader, step s-1's backward,
+    // finished before the barrier that ended that step); the column tile's
+    // Gram block of step s+1 for the correction
+    pk_glds_x_to(a, xbuf(s + 2), s + 2, lane, w, k0);
+    if (gk == 0) pk_glds_gram(a, Gl, s + 1, lane, w);
+
+    // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
+    {
+      const int m = tid >> 2, qq = tid & 3;
+      const int64_t g = kOffDz1 + (int64_t)m * kD1 + n0 + 4 * qq;
+      uint4 v0, v1;
+      poll.start();
+      for (;;) {
+        v0 = ld_gran2(rb, g);
+        v1 = ld_gran2(rb, g + 2);
+        if (v0.y == tag && v0.w == tag && v1.y == tag && v1.w == tag) break;
+        if (!poll.again()) { ok = false; break; }
+      }
+      Dz[m * 17 + 4 * qq + 0] = __uint_as_float(v0.x);
+      Dz[m * 17 + 4 * qq + 1] = __uint_as_float(v0.z);
+      Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
+      Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
+    }
+    if (lb == 0 && it + 1 == a.steps && tid < kNBlk && ok) {
+      // hand the step counter on once every block has read it (SF tags)
+      const uint32_t t0 = (uint32_t)(s0 + 1);
+      poll.start();
+      while (flag_tag(rb, kOffSf + tid) != t0)
+        if (!poll.again()) { ok = false; break; }
+    }
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;  // also retires the X / G LDS-DMA
+    if (!ok) break;
+    if (lb == 0 && it + 1 == a.steps && tid == 0) {
+      const uint64_t e = s0 + (uint64_t)a.steps;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr + 1), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    PK_STAMP(0, 2);
+
+    // ---- gk == 0: C(s+1)[64 x 16] = -lr G1(s+1) dZ1(s)[:, tile]; wave w: rows
+    // 16 w .. +15 (chain w's rows), K = 64 batch rows ----
+    if (gk == 0) {
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < kB / 4; ks += 2) {
+        c0 = mfma_f32_16x16x4(Gl[(4 * ks + q) * kB + 16 * w + i], Dz[(4 * ks + q) * 17 + i], c0);
+        c1 = mfma_f32_16x16x4(Gl[(4 * ks + 4 + q) * kB + 16 * w + i], Dz[(4 * ks + 4 + q) * 17 + i], c1);
+      }
+      const f4v cz = {-a.lr * (c0[0] + c1[0]), -a.lr * (c0[1] + c1[1]), -a.lr * (c0[2] + c1[2]),
+                      -a.lr * (c0[3] + c1[3])};
+      st_f4(rb, pk_part_off(parn, kNL1 + gn, w) + i * 16 + 4 * q, cz);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      if (tid == 0) st_gran(rb, pk_pf(parn, kNL1 + gn), __uint_as_float(tagn), tagn);
+    }
+
+    // ---- backward: dW1 tile [16 n][112 k] = dZ1^T . X(s), SGD in LDS ----
+    const float* Xl = xbuf(s);
+    float dv[kB / 4];
+#pragma unroll
+    for (int ms = 0; ms < kB / 4; ++ms) dv[ms] = Dz[(4 * ms + q) * 17 + i];
+    f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float db = 0.f;
+    if (w < 3) {
+      const float* xb0 = Xl + q * kKC + 16 * w + i;
+      const float* xb1 = xb0 + 64;
+#pragma unroll
+      for (int ms = 0; ms < kB / 4; ++ms) {
+        g[0] = mfma_f32_16x16x4(dv[ms], xb0[4 * ms * kKC], g[0]);
+        g[1] = mfma_f32_16x16x4(dv[ms], xb1[4 * ms * kKC], g[1]);
+      }
+    } else {
+      const float* xb0 = Xl + q * kKC + 48 + i;
+#pragma unroll
+      for (int ms = 0; ms < kB / 4; ms += 2) {
+        g[0] = mfma_f32_16x16x4(dv[ms], xb0[4 * ms * kKC], g[0]);
+        g[1] = mfma_f32_16x16x4(dv[ms + 1], xb0[4 * (ms + 1) * kKC], g[1]);
+      }
+      g[0] = g[0] + g[1];
+#pragma unroll
+      for (int ms = 0; ms < kB / 4; ++ms) db += dv[ms];
+      db += __shfl_xor(db, 16, 64);
+      db += __shfl_xor(db, 32, 64);
+    }
+    // every wave read this step's W1 tile in the P(s+1) forward, before the
+    // barrier that followed it
+    const int kc0 = 16 * w + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Wl[(4 * q + r) * kXS + kc0] -= a.lr * g[0][r];
+    if (w < 3) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Wl[(4 * q + r) * kXS + kc0 + 64] -= a.lr * g[1][r];
+    } else if (gk == 0 && q == 0) {
+      B1[i] -= a.lr * db;
+    }
+    __syncthreads();
+    PK_STAMP(0, 3);
+  }
+
+  // ---- epilogue: the resident weights back to HBM ----
+  float* W1w = a.P + a.w_off[0];
+  for (int e = tid; e < kW1F4; e += kThreads) {
+    const int r = e / (kKC / 4), c4 = e - r * (kKC / 4);
+    *reinterpret_cast<float4*>(W1w + (int64_t)(n0 + r) * kD0 + k0 + 4 * c4) =
+        *reinterpret_cast<const float4*>(Wl + r * kXS + 4 * c4);
+  }
+  if (gk == 0 && tid < 16) a.P[a.b_off[0] + n0 + tid] = B1[tid];
+  pk_report(a, ok);
+  if (lb == 0) PK_EDGE(2);
+}
+
 // -----------------------------------------------------------------------------
 // Chain block: the critical path of the upper layers for 16 batch rows
 // -----------------------------------------------------------------------------
@@ -787,7 +1059,21 @@ __device__ __forceinline__ void pk_chain_rows_out(__amdgpu_buffer_rsrc_t rb, con
   }
 }
 
-template <int NL>
+// Per-wave wait for partial-slot flags: lane j < nflags polls slot slot_of(j)
+// of parity `par` for `tag`, then a wave vote -- no workgroup barrier, so the
+// wave's loads already in flight are not drained.  false: a wait gave up.
+template <typename F>
+__device__ __forceinline__ bool pk_wave_wait(__amdgpu_buffer_rsrc_t rb, int par, int nflags, F slot_of,
+                                             uint32_t tag, Poll& poll) {
+  const int lane = threadIdx.x & 63;
+  bool ok = true;
+  if (lane < nflags) ok = wait_flag(rb, pk_pf(par, slot_of(lane)), tag, poll);
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  asm volatile("" ::: "memory");
+  return ok;
+}
+
+template <int NL, bool DP>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c, int blk) {
   using L = ChLay<NL>;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -825,7 +1111,25 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (c == 0 && g_pk_stamp_on && tid == 0) g_pk_stamps[3][1][0] = local ? 1u : 0u;
 
   const int stamp_on = g_pk_stamp_on && c == 0;
-  for (int it = 0; it < a.steps && ok; ++it) {
+  // thread -> (column tile gn, column n, 8 rows) of this chain's H1 block
+  const int pgn = tid >> 5, pn = (tid >> 1) & 15, phalf = tid & 1;
+  // wave w's partial slots: gn = 2 w, 2 w + 1 of every gk (lane j -> slot)
+  auto l1_slot = [&](int j) { return 2 * w + (j & 1) + kGN * (j >> 1); };
+  f4v pv[kGK][2];  // single replica: P(s) of the next step, loaded a step ahead
+  bool pok = true;  // this wave's P loads are valid (agreed at the next block vote)
+  auto load_p = [&](int pr) {
+#pragma unroll
+    for (int gk = 0; gk < kGK; ++gk) {
+      const int64_t off = pk_part_off(pr, pgn + kGN * gk, c) + pn * 16 + 8 * phalf;
+      pv[gk][0] = ld_f4(rb, off);
+      pv[gk][1] = ld_f4(rb, off + 4);
+    }
+  };
+  if constexpr (!DP) {
+    pok = ok && pk_wave_wait(rb, (int)(s0 & 1), 2 * kGK, l1_slot, (uint32_t)(s0 + 1), poll);
+    if (pok) load_p((int)(s0 & 1));
+  }
+  for (int it = 0; ok && it < a.steps; ++it) {
     PK_STAMP(1, 0);
     const uint64_t s = s0 + (uint64_t)it;
     const uint32_t tag = (uint32_t)(s + 1);
@@ -858,38 +1162,62 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     };
     constexpr bool kWFirst = NL == 2;
     if (kWFirst) fetch_w();
-    // ---- H1 rows = relu(sum of the 7 k-partials) ----
-    // this chain's 16 rows of every partial in one bulk read: thread -> (gn,
-    // column n, 8 rows), 7 gk
-    {
-      if (tid < kNL1 && !wait_flag(rb, kOffPf + tid, tag, poll)) ok = false;
-      if (!ok) s_fail = 1u;
-      lds_barrier();
-      ok = s_fail == 0u;
-      if (!ok) break;
-      PK_STAMP(1, 1);
-      const int gn = tid >> 5, n = (tid >> 1) & 15, half = tid & 1;
-      f4v v[kGK][2];
+    if constexpr (!DP) {
+      // ---- H1 rows = relu(P(s) + C(s)): P(s) came in a step ahead; the
+      // correction of this wave's two column tiles is the last thing to wait for ----
+      if (pok && pk_wave_wait(rb, par, 2, [&](int j) { return kNL1 + 2 * w + j; }, tag, poll)) {
+        PK_STAMP(1, 1);
+        const int64_t off = pk_part_off(par, kNL1 + pgn, c) + pn * 16 + 8 * phalf;
+        const f4v c0 = ld_f4(rb, off), c1 = ld_f4(rb, off + 4);
+        if (!kWFirst) fetch_w();
 #pragma unroll
-      for (int gk = 0; gk < kGK; ++gk) {
-        const int lb = gn + kGN * gk;
-        const int64_t off = kOffPart * 2 + (((int64_t)lb * kNCH + c) * 16 + n) * 16 + 8 * half;
-        v[gk][0] = ld_f4(rb, off);
-        v[gk][1] = ld_f4(rb, off + 4);
+        for (int e = 0; e < 8; ++e) {
+          float z = 0.f;
+#pragma unroll
+          for (int gk = 0; gk < kGK; ++gk) z += pv[gk][e >> 2][e & 3];
+          z += (e < 4 ? c0 : c1)[e & 3];
+          H1[(8 * phalf + e) * kS1 + 16 * pgn + pn] = fmaxf(z, 0.f);
+        }
+      } else {
+        ok = false;
       }
-      if (!kWFirst) fetch_w();
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float z = 0.f;
-#pragma unroll
-        for (int gk = 0; gk < kGK; ++gk) z += v[gk][e >> 2][e & 3];
-        H1[(8 * half + e) * kS1 + 16 * gn + n] = fmaxf(z, 0.f);
-      }
-    }
-    if (it > 0) {
+      // every wave's waits agreed on (drains the weight loads, consumed next)
       ok = __syncthreads_and(ok ? 1 : 0) != 0;
       if (!ok) break;
-      pk_w_commit<NL>(lds, wv);
+      if (it > 0) pk_w_commit<NL>(lds, wv);
+    } else {
+      // ---- H1 rows = relu(sum of the 7 k-partials) ----
+      // this chain's 16 rows of every partial in one bulk read: thread -> (gn,
+      // column n, 8 rows), 7 gk
+      {
+        if (tid < kNL1 && !wait_flag(rb, kOffPf + tid, tag, poll)) ok = false;
+        if (!ok) s_fail = 1u;
+        lds_barrier();
+        ok = s_fail == 0u;
+        if (!ok) break;
+        PK_STAMP(1, 1);
+        f4v v[kGK][2];
+#pragma unroll
+        for (int gk = 0; gk < kGK; ++gk) {
+          const int lb = pgn + kGN * gk;
+          const int64_t off = kOffPart * 2 + (((int64_t)lb * kNCH + c) * 16 + pn) * 16 + 8 * phalf;
+          v[gk][0] = ld_f4(rb, off);
+          v[gk][1] = ld_f4(rb, off + 4);
+        }
+        if (!kWFirst) fetch_w();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float z = 0.f;
+#pragma unroll
+          for (int gk = 0; gk < kGK; ++gk) z += v[gk][e >> 2][e & 3];
+          H1[(8 * phalf + e) * kS1 + 16 * pgn + pn] = fmaxf(z, 0.f);
+        }
+      }
+      if (it > 0) {
+        ok = __syncthreads_and(ok ? 1 : 0) != 0;
+        if (!ok) break;
+        pk_w_commit<NL>(lds, wv);
+      }
     }
     lds_barrier();
     // the H1 rows go to the gradient blocks now; drained and flagged after the
@@ -1098,6 +1426,16 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     lds_barrier();
     if (tid == 0) st_gran(rb, kOffCxf + 8 + par * kNCH + c, __uint_as_float(tag), tag);
     PK_STAMP(1, 5);
+    // single replica: the next step's P(s+1) partials, published by the
+    // layer-1 blocks while this step ran, come in now (consumed after the next
+    // correction arrives)
+    if constexpr (!DP) {
+      if (it + 1 < a.steps) {
+        const int pn1 = (int)((s + 1) & 1);
+        pok = pk_wave_wait(rb, pn1, 2 * kGK, l1_slot, tag + 1, poll);
+        if (pok) load_p(pn1);
+      }
+    }
   }
 
   // ---- epilogue: stats (the gradient blocks write the upper weights back) ----
@@ -1429,10 +1767,11 @@ void mlp_persist_k(PersistArgs a) {
   const int b = blockIdx.x;
   const int x = b & 7, y = b >> 3;
   if (x == 0) {
-    if (y < kNCH) pk_chain<NL>(a, lds, y, b);
+    if (y < kNCH) pk_chain<NL, DP>(a, lds, y, b);
     else pk_grad<NL, DP>(a, lds, y - kNCH, b);
   } else {
-    pk_layer1<DP>(a, lds, y + kGN * (x - 1), b);
+    if constexpr (DP) pk_layer1<true>(a, lds, y + kGN * (x - 1), b);
+    else pk_layer1_gram(a, lds, y + kGN * (x - 1), b);
   }
 }
 
@@ -1483,7 +1822,8 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
-                             hipStream_t s, const XchgArgs* xa, const XchgTab* tab, int algo) {
+                             hipStream_t s, const XchgArgs* xa, const XchgTab* tab, int algo,
+                             const float* gram, int carry) {
   if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
       (ldx % 4) != 0 || ldx < kD0 || (((uintptr_t)X) & 15) != 0)
     return hipErrorInvalidValue;
@@ -1509,6 +1849,8 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
   a.herr = herr;
   a.timeout_ticks = timeout_ticks;
   a.nrep = 1;
+  a.gram = gram;
+  a.carry = carry ? 1 : 0;
   if (xa != nullptr && xa->nranks > 1) {
     if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks, algo) ||
         xa->err == nullptr)
@@ -1520,6 +1862,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     a.xerr = xa->err;
     a.algo = algo;
   }
+  if (a.nrep == 1 && (gram == nullptr || ((uintptr_t)gram & 15) != 0)) return hipErrorInvalidValue;
   if (d.nlayers == 3) return a.nrep > 1 ? pk_launch<3, true>(a, s) : pk_launch<3, false>(a, s);
   return a.nrep > 1 ? pk_launch<2, true>(a, s) : pk_launch<2, false>(a, s);
 }

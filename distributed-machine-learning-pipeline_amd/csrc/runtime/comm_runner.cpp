@@ -254,6 +254,7 @@ bool MlpRunner::persist_failed() const {
 
 void MlpRunner::clear_persist_error() {
   if (pk_herr_ != nullptr) __atomic_store_n(pk_herr_, 0u, __ATOMIC_RELEASE);
+  pk_carry_ = false;  // called when the buffer is rewound: nothing carries over
 }
 
 void MlpRunner::reset_graph() {
@@ -384,6 +385,7 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
   pk_xb_ = xbuf;
   pk_err_ = err;
   pk_timeout_ = (uint64_t)(timeout_ms * 1e5);  // s_memrealtime: 100 MHz
+  pk_carry_ = false;
   reset_graph();
 }
 
@@ -395,9 +397,14 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
                                        lr_ / (float)pk_x_->nranks(), n, pk_xb_, b_.stats, pk_err_,
                                        pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table(),
                                        pk_algo_));
-    else
+    else {
+      if (pk_gram_ == nullptr)
+        throw std::invalid_argument("persistent step: set_persist_gram first (single replica)");
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
-                                       b_.stats, pk_err_, pk_herr_, pk_timeout_, s));
+                                       b_.stats, pk_err_, pk_herr_, pk_timeout_, s, nullptr, nullptr,
+                                       0, pk_gram_, pk_carry_ ? 1 : 0));
+      pk_carry_ = true;  // the next launch, in stream order, finds this one's state
+    }
     return;
   }
   for (int i = 0; i < n; ++i) enqueue_step(s);

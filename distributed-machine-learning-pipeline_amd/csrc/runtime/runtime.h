@@ -285,6 +285,14 @@ class MlpRunner {
   void set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, PeerExchange* x = nullptr,
                    int algo = 0);
   bool persist_active() const { return pk_xb_ != nullptr; }
+  // Single replica: the Gram table of the batches (float[nbatches][64][64],
+  // kernels/mlp_persist.hip), set once; and whether the hand-off buffer carries
+  // the previous launch's pipeline state -- set by every single-replica
+  // launch, cleared by set_persist / clear_persist_error and by the owner
+  // whenever it rewrites the parameters or the buffer.
+  void set_persist_gram(const float* g) { pk_gram_ = g; pk_carry_ = false; }
+  void set_persist_carry(bool c) { pk_carry_ = c; }
+  bool persist_carry() const { return pk_carry_; }
   // Whether a persistent launch gave up on a hand-off (read from host-mapped
   // memory the kernel marks on the way out: valid after a stream sync, no copy).
   bool persist_failed() const;
@@ -333,6 +341,8 @@ class MlpRunner {
   uint32_t* pk_err_ = nullptr;
   uint32_t* pk_herr_ = nullptr;  // hipHostMalloc'd, device-visible
   uint64_t pk_timeout_ = 0;
+  const float* pk_gram_ = nullptr;
+  bool pk_carry_ = false;
   int algo_ = 0;
   int world_ = 1;
   int64_t chunk_bytes_ = 1 << 20;

@@ -180,6 +180,8 @@ class MlpTrainer:
             if self._want_persist and plain and C.mlp_persist_supported(self.layout.desc_list()):
                 self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64, device=d)
                 self.pk_err = torch.zeros(1, dtype=torch.int32, device=d)
+                self.pk_gram = self._gram_table()
+                self.runner.set_persist_gram(self.pk_gram)
                 self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0)
                 self.sync_active = "none"
             return
@@ -424,11 +426,36 @@ class MlpTrainer:
         return self.runner is not None and self.pk_buf is not None and self.runner.persist_active()
 
     def _rewound(self) -> None:
-        """The step counter went back: stale hand-off tags could match again."""
+        """The step counter went back: stale hand-off tags could match again
+        (and the pipeline state a launch carries over to the next is gone)."""
         if self.pk_buf is not None:
             self.pk_buf.zero_()
             self.pk_err.zero_()
             self.runner.clear_persist_error()
+
+    def _gram_table(self) -> torch.Tensor:
+        """Per-batch Gram blocks of the single-replica persistent step
+        (kernels/mlp_persist.hip, "Gram form"): G1T[b][m'][m] = X_{b-1}[m'] .
+        X_b[m] + 1, b - 1 wrapping, rows past the batch repeating its last row
+        as the kernel's X tiles do.  float[nbatches][64][64] (16 KB a batch)."""
+        nb, B, d0 = self.nbatches, self.batch, self.spec.dims[0]
+        Xb = self.X[: nb * B, :d0].reshape(nb, B, d0)
+        if B < 64:
+            Xb = Xb[:, torch.clamp(torch.arange(64, device=Xb.device), max=B - 1), :]
+        G = torch.empty((nb, 64, 64), dtype=torch.float32, device=self.device)
+        step = 256  # bounded temporaries for large shards
+        for b0 in range(0, nb, step):
+            b1 = min(nb, b0 + step)
+            prev = Xb[torch.arange(b0 - 1, b1 - 1, device=Xb.device) % nb]
+            torch.bmm(prev, Xb[b0:b1].transpose(1, 2), out=G[b0:b1])
+        G += 1.0
+        return G.contiguous()
+
+    def _params_rewritten(self) -> None:
+        """P changed outside the persistent launches: the partials the last
+        launch computed from the old weights must not be carried over."""
+        if self.pk_buf is not None and self.runner is not None:
+            self.runner.set_persist_carry(False)
 
     def _graphs_on(self) -> bool:
         """Whether train_steps replays hipGraphs for the active sync mode."""
@@ -616,6 +643,7 @@ class MlpTrainer:
 
         self.synchronize()
         sgd_update_(self.P, g.to(self.P.device).contiguous(), self.lr * scale)
+        self._params_rewritten()
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
@@ -647,9 +675,18 @@ class MlpTrainer:
     # --------------------------------------------------------- state / ckpt --
     def state_dict(self) -> Dict[str, object]:
         self.synchronize()
-        return {"spec": list(self.spec.dims), "params": self.P.detach().cpu().clone(),
-                "velocity": self.V.detach().cpu().clone(), "steps_done": self.steps_done,
-                "lr": self.lr, "batch": self.batch}
+        sd = {"spec": list(self.spec.dims), "params": self.P.detach().cpu().clone(),
+              "velocity": self.V.detach().cpu().clone(), "steps_done": self.steps_done,
+              "lr": self.lr, "batch": self.batch}
+        if self._carries_state():
+            # the single-replica persistent step's pipeline state (the next step's
+            # partials and correction), so a resume is bit-identical to running on
+            sd["persist_carry"] = self.pk_buf.detach().cpu().clone()
+        return sd
+
+    def _carries_state(self) -> bool:
+        return (self.pk_buf is not None and not self.ctx.is_distributed and self.runner is not None
+                and self.runner.persist_active() and self.runner.persist_carry())
 
     def load_state_dict(self, sd: Dict[str, object]) -> None:
         if list(sd["spec"]) != list(self.spec.dims):
@@ -663,6 +700,11 @@ class MlpTrainer:
             # A = B = s at the start of step s (dsml.h step-counter protocol)
             self.ctr.fill_(self.steps_done)
             self._rewound()
+            carry = sd.get("persist_carry")
+            if (carry is not None and self.pk_buf is not None and not self.ctx.is_distributed
+                    and self.runner.persist_active() and carry.numel() == self.pk_buf.numel()):
+                self.pk_buf.copy_(carry.to(self.device))
+                self.runner.set_persist_carry(True)
             torch.cuda.synchronize(self.device)
             if self.xchg is not None:  # flags may be ahead of the restored step
                 from ..parallel.xchg import reset_group
