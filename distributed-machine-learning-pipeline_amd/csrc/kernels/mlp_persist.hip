@@ -170,7 +170,11 @@ constexpr int64_t kOffCx = kOffDz1 + kB * kD1;
 constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCX / 2;
 constexpr int64_t kOffWx = kOffCxf + 16;  // CXF: [part 0 = H1, part 1 = the rest][2][4]
 constexpr int64_t kOffWf = kOffWx + 2 * kNG * kWX / 2;
-constexpr int64_t kTotalG = kOffWf + 8;
+// CG[64][128]: single replica, the layer-1 correction C(s) of step s as tagged
+// granules (tag s + 1), written by the gk == 0 layer-1 blocks, polled directly
+// by the chains (no drain, no flag: one hop).
+constexpr int64_t kOffCg = kOffWf + 8;
+constexpr int64_t kTotalG = kOffCg + kB * kD1;
 static_assert(kCX % 4 == 0 && kWX % 4 == 0 && (kOffCx % 2) == 0 && (kOffWx % 2) == 0,
               "exchange rows travel as 16-B vectors");
 
@@ -757,10 +761,10 @@ __device__ __forceinline__ void pk_glds_gram(const PersistArgs& a, float* gl, ui
   for (int ch = w; ch < kB * kB / 256; ch += 4)
     __builtin_amdgcn_global_load_lds((pk_gptr)(src + ch * 256 + lane * 4), (pk_lptr)(gl + ch * 256), 16, 0, 0);
 }
-// One wave's [16 rows x 16 n] of X . W1_tile^T (+ b1), stored (write-through) to
-// its chain's run of partial slot `slot`, parity `par`; drained by this wave.
-__device__ __forceinline__ void pk_l1_partial(__amdgpu_buffer_rsrc_t rb, const float* Xl, const float* Wl,
-                                              const float* B1, int par, int slot, int w, int i, int q) {
+// One wave's [16 rows x 16 n] of X . W1_tile^T (+ b1): lane (i, q) holds rows
+// 16 w + 4 q .. +3 of column i.
+__device__ __forceinline__ f4v pk_l1_fwd(const float* Xl, const float* Wl, const float* B1, int w, int i,
+                                         int q) {
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f},
                   {0.f, 0.f, 0.f, 0.f}};
   const float* xa = Xl + (16 * w + i) * kKC + 4 * q;
@@ -778,8 +782,31 @@ __device__ __forceinline__ void pk_l1_partial(__amdgpu_buffer_rsrc_t rb, const f
   f4v z;
 #pragma unroll
   for (int r = 0; r < 4; ++r) z[r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]) + bn;
-  st_f4(rb, pk_part_off(par, slot, w) + i * 16 + 4 * q, z);
+  return z;
+}
+// ... stored (write-through) to its chain's run of partial slot `slot`, parity
+// `par`; drained by this wave.
+__device__ __forceinline__ void pk_l1_partial(__amdgpu_buffer_rsrc_t rb, const float* Xl, const float* Wl,
+                                              const float* B1, int par, int slot, int w, int i, int q) {
+  st_f4(rb, pk_part_off(par, slot, w) + i * 16 + 4 * q, pk_l1_fwd(Xl, Wl, B1, w, i, q));
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// gk == 0 block: its own k-partial plus the 6 other k-partials of its column
+// tile (slots gn + 8 gk), summed in gk order -- the partial sum of Z1 the
+// correction completes.  false: a wait gave up.  Block-wide (barrier inside).
+__device__ __forceinline__ bool pk_l1_gather(__amdgpu_buffer_rsrc_t rb, f4v& z, int par, int gn, uint32_t tag,
+                                             Poll& poll, int w, int i, int q) {
+  const int tid = threadIdx.x;
+  bool ok = true;
+  if (tid >= 1 && tid < kGK) ok = wait_flag(rb, pk_pf(par, gn + kGN * tid), tag, poll);
+  ok = __syncthreads_and(ok ? 1 : 0) != 0;
+  if (!ok) return false;
+  f4v v[kGK - 1];
+#pragma unroll
+  for (int gk = 1; gk < kGK; ++gk) v[gk - 1] = ld_f4(rb, pk_part_off(par, gn + kGN * gk, w) + i * 16 + 4 * q);
+#pragma unroll
+  for (int gk = 1; gk < kGK; ++gk) z += v[gk - 1];
+  return true;
 }
 
 __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
@@ -826,15 +853,18 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     // no state from a previous launch: step s0's Z1 directly, correction 0
     const uint32_t t0 = (uint32_t)(s0 + 1);
     const int par0 = (int)(s0 & 1);
-    pk_l1_partial(rb, xbuf(s0), Wl, B1, par0, lb, w, i, q);
-    if (gk == 0) {
-      st_f4(rb, pk_part_off(par0, kNL1 + gn, w) + i * 16 + 4 * q, f4v{0.f, 0.f, 0.f, 0.f});
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (tid == 0) {
-      st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
-      if (gk == 0) st_gran(rb, pk_pf(par0, kNL1 + gn), __uint_as_float(t0), t0);
+    if (gk != 0) {
+      pk_l1_partial(rb, xbuf(s0), Wl, B1, par0, lb, w, i, q);
+      __syncthreads();
+      if (tid == 0) st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
+    } else {
+      f4v z = pk_l1_fwd(xbuf(s0), Wl, B1, w, i, q);
+      if (!pk_l1_gather(rb, z, par0, gn, t0, poll, w, i, q)) {
+        pk_report(a, false);
+        return;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st_gran(rb, kOffCg + (int64_t)(16 * w + 4 * q + r) * kD1 + n0 + i, z[r], t0);
     }
   }
 
@@ -847,10 +877,17 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     const uint32_t tagn = tag + 1;                 // step s + 1
     const int parn = (int)((s + 1) & 1);
 
-    // ---- P(s+1) = X(s+1) W1(s)^T + b1(s): published before dZ1(s) exists ----
-    pk_l1_partial(rb, xbuf(s + 1), Wl, B1, parn, lb, w, i, q);
-    __syncthreads();
-    if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
+    // ---- P(s+1) = X(s+1) W1(s)^T + b1(s), before dZ1(s) exists: published
+    // by gk >= 1; the gk == 0 block keeps its own and gathers the other six ----
+    f4v zs;
+    if (gk != 0) {
+      pk_l1_partial(rb, xbuf(s + 1), Wl, B1, parn, lb, w, i, q);
+      __syncthreads();
+      if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
+    } else {
+      zs = pk_l1_fwd(xbuf(s + 1), Wl, B1, w, i, q);
+      if (!pk_l1_gather(rb, zs, parn, gn, tagn, poll, w, i, q)) { ok = false; break; }
+    }
     PK_STAMP(0, 1);
     // X(s+2) into the third buffer (its last reader, step s-1's backward,
     // finished before the barrier that ended that step); the column tile's
@@ -900,12 +937,13 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
         c0 = mfma_f32_16x16x4(Gl[(4 * ks + q) * kB + 16 * w + i], Dz[(4 * ks + q) * 17 + i], c0);
         c1 = mfma_f32_16x16x4(Gl[(4 * ks + 4 + q) * kB + 16 * w + i], Dz[(4 * ks + 4 + q) * 17 + i], c1);
       }
-      const f4v cz = {-a.lr * (c0[0] + c1[0]), -a.lr * (c0[1] + c1[1]), -a.lr * (c0[2] + c1[2]),
-                      -a.lr * (c0[3] + c1[3])};
-      st_f4(rb, pk_part_off(parn, kNL1 + gn, w) + i * 16 + 4 * q, cz);
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      if (tid == 0) st_gran(rb, pk_pf(parn, kNL1 + gn), __uint_as_float(tagn), tagn);
+      // Z1(s+1) = P(s+1) + C(s+1), one tagged granule per value: the chains
+      // poll the data itself
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        st_gran(rb, kOffCg + (int64_t)(16 * w + 4 * q + r) * kD1 + n0 + i, zs[r] + -a.lr * (c0[r] + c1[r]),
+                tagn);
+      PK_STAMP(0, 4);
     }
 
     // ---- backward: dW1 tile [16 n][112 k] = dZ1^T . X(s), SGD in LDS ----
@@ -1115,20 +1153,6 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   const int pgn = tid >> 5, pn = (tid >> 1) & 15, phalf = tid & 1;
   // wave w's partial slots: gn = 2 w, 2 w + 1 of every gk (lane j -> slot)
   auto l1_slot = [&](int j) { return 2 * w + (j & 1) + kGN * (j >> 1); };
-  f4v pv[kGK][2];  // single replica: P(s) of the next step, loaded a step ahead
-  bool pok = true;  // this wave's P loads are valid (agreed at the next block vote)
-  auto load_p = [&](int pr) {
-#pragma unroll
-    for (int gk = 0; gk < kGK; ++gk) {
-      const int64_t off = pk_part_off(pr, pgn + kGN * gk, c) + pn * 16 + 8 * phalf;
-      pv[gk][0] = ld_f4(rb, off);
-      pv[gk][1] = ld_f4(rb, off + 4);
-    }
-  };
-  if constexpr (!DP) {
-    pok = ok && pk_wave_wait(rb, (int)(s0 & 1), 2 * kGK, l1_slot, (uint32_t)(s0 + 1), poll);
-    if (pok) load_p((int)(s0 & 1));
-  }
   for (int it = 0; ok && it < a.steps; ++it) {
     PK_STAMP(1, 0);
     const uint64_t s = s0 + (uint64_t)it;
@@ -1160,27 +1184,52 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
         else ok = false;
       }
     };
-    constexpr bool kWFirst = NL == 2;
+    constexpr bool kWFirst = DP && NL == 2;  // single replica: Z1 (one hop) comes before the weights
     if (kWFirst) fetch_w();
     if constexpr (!DP) {
-      // ---- H1 rows = relu(P(s) + C(s)): P(s) came in a step ahead; the
-      // correction of this wave's two column tiles is the last thing to wait for ----
-      if (pok && pk_wave_wait(rb, par, 2, [&](int j) { return kNL1 + 2 * w + j; }, tag, poll)) {
-        PK_STAMP(1, 1);
-        const int64_t off = pk_part_off(par, kNL1 + pgn, c) + pn * 16 + 8 * phalf;
-        const f4v c0 = ld_f4(rb, off), c1 = ld_f4(rb, off + 4);
-        if (!kWFirst) fetch_w();
+      // ---- H1 rows = relu(Z1(s)): the gk == 0 layer-1 blocks publish Z1 =
+      // P + C as tagged granules; polled directly (one hop, no flag) ----
+      bool cok = true;
+      PK_STAMP(1, 6);
+      {
+        // thread -> row rr, columns cc .. cc + 7 (four 16-B granule pairs)
+        const int rr = tid >> 4, cc = 8 * (tid & 15);
+        const int64_t g0 = kOffCg + (int64_t)(rb0 + rr) * kD1 + cc;
+        uint4 cv[4];
+        // light polling: one lane per row spins on one 16-B pair (the payload
+        // lines stay quiet while their writers store them); once all four rows
+        // of the wave show it, every lane reads its four pairs and every tag
+        // is checked (the writing lanes are unordered)
+        poll.start();
+        for (;;) {
+          bool ready = true;
+          if ((tid & 15) == 0) {
+            const uint4 f = ld_gran2(rb, g0 + 6);
+            ready = f.y == tag && f.w == tag;
+          }
+          if (__builtin_amdgcn_ballot_w64(!ready) == 0) {
+            bool all = true;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float z = 0.f;
-#pragma unroll
-          for (int gk = 0; gk < kGK; ++gk) z += pv[gk][e >> 2][e & 3];
-          z += (e < 4 ? c0 : c1)[e & 3];
-          H1[(8 * phalf + e) * kS1 + 16 * pgn + pn] = fmaxf(z, 0.f);
+            for (int j = 0; j < 4; ++j) {
+              cv[j] = ld_gran2(rb, g0 + 2 * j);
+              all = all && cv[j].y == tag && cv[j].w == tag;
+            }
+            if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
+          }
+          if (!poll.again()) { cok = false; break; }
         }
-      } else {
-        ok = false;
+        PK_STAMP(1, 1);
+        if (cok) {
+          float* hr = H1 + rr * kS1 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hr[2 * j] = fmaxf(__uint_as_float(cv[j].x), 0.f);
+            hr[2 * j + 1] = fmaxf(__uint_as_float(cv[j].z), 0.f);
+          }
+        }
       }
+      if (!cok) ok = false;
+      if (!kWFirst) fetch_w();
       // every wave's waits agreed on (drains the weight loads, consumed next)
       ok = __syncthreads_and(ok ? 1 : 0) != 0;
       if (!ok) break;
@@ -1426,16 +1475,6 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     lds_barrier();
     if (tid == 0) st_gran(rb, kOffCxf + 8 + par * kNCH + c, __uint_as_float(tag), tag);
     PK_STAMP(1, 5);
-    // single replica: the next step's P(s+1) partials, published by the
-    // layer-1 blocks while this step ran, come in now (consumed after the next
-    // correction arrives)
-    if constexpr (!DP) {
-      if (it + 1 < a.steps) {
-        const int pn1 = (int)((s + 1) & 1);
-        pok = pk_wave_wait(rb, pn1, 2 * kGK, l1_slot, tag + 1, poll);
-        if (pok) load_p(pn1);
-      }
-    }
   }
 
   // ---- epilogue: stats (the gradient blocks write the upper weights back) ----

@@ -49,6 +49,16 @@ out["chain_dz1_publish_to_l1_ready_us"] = med([(st[0][s][2] - st[1][s][4]) / 100
 out["chain_rows_to_grad_ready_us"] = med([(st[2][s][1] - st[1][s][5]) / 100.0 for s in range(8)])
 out["grad_publish_to_chain_w_ready_us"] = med([(st[1][s + 1][1] - st[2][s][4]) / 100.0 for s in range(7)])
 out["chain_flag_wait_us"] = med([(st[1][s][1] - st[1][s][0]) / 100.0 for s in range(8)])
+if spec.dims and all(st[1][s][6] for s in range(8)):
+    # single-replica Gram form: chain step start -> Z1 poll begins (weights
+    # fetched first for 2 layers) -> Z1 seen; layer-1 gk = 0 block: dZ1 ready ->
+    # Z1 = P + C stored; Z1 stored (step s) -> chain sees it (step s+1)
+    out["gram"] = {
+        "chain_start_to_z1_poll_us": med([(st[1][s][6] - st[1][s][0]) / 100.0 for s in range(8)]),
+        "chain_z1_poll_us": med([(st[1][s][1] - st[1][s][6]) / 100.0 for s in range(8)]),
+        "l1_dz1_ready_to_z1_stored_us": med([(st[0][s][4] - st[0][s][2]) / 100.0 for s in range(8)]),
+        "z1_stored_to_chain_seen_us": med([(st[1][s + 1][1] - st[0][s][4]) / 100.0 for s in range(7)]),
+    }
 out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
 print(json.dumps(out, indent=1))
 if len(sys.argv) > 1:
