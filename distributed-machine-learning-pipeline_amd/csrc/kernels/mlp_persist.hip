@@ -63,6 +63,18 @@ constexpr int kNL1 = kGN * kGK;                         // 56 layer-1 blocks
 constexpr int kNCH = 4, kNG = 4;                        // chains (16 rows each), gradient blocks
 constexpr int kNBlk = kNL1 + kNCH + kNG;                // 64
 constexpr int kNPart = kNL1 + kGN;                      // partial slots: 56 layer-1 + 8 corrections
+// Single replica: the upper weights' full-batch gradients + SGD run in
+// gradient TILES (W2 [16 h x 32 n] tiles of the 3-layer model, [16 o x 16 n]
+// tiles of the 2-layer one) -- each loads only its operand columns and
+// publishes only its tile, so the weights the chains wait for come back after
+// ~16 MFMAs instead of a quarter of the update.  All upper blocks (chains +
+// tiles) sit at blockIdx 8 k; layer-1 block (gn, gk) at blockIdx 8 gn + gk + 1.
+template <int NL> struct GTile { static constexpr int kN = NL == 3 ? 16 : 8; };
+template <int NL> constexpr int pk_grid(bool dp) { return dp ? kNBlk : 8 * (kNCH + GTile<NL>::kN); }
+// Whether blockIdx b does work in the single-replica grid (the rest exit).
+template <int NL> __device__ __forceinline__ bool pk_sr_active(int b) {
+  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < kGN;
+}
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
 
@@ -139,7 +151,7 @@ static_assert(L1GLay::G % 4 == 0, "LDS-DMA image must be 16-B aligned");
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int NL>
 constexpr int lds_floats() {
-  return cmax(cmax(L1Lay::TOTAL, L1GLay::TOTAL), cmax(ChLay<NL>::TOTAL, GLay<NL>::TOTAL));
+  return cmax(cmax(L1Lay::TOTAL, L1GLay::TOTAL), cmax(ChLay<NL>::TOTAL, GLay<NL>::TOTAL));  // >= GTLay
 }
 static_assert(lds_floats<3>() * 4 <= 160 * 1024 && lds_floats<2>() * 4 <= 160 * 1024, "LDS budget");
 
@@ -165,7 +177,7 @@ constexpr int kWX = 16 * kD1 + 16 * 16 + 16 + 16;              // 2336 floats
 constexpr int64_t kOffPart = 0;
 constexpr int64_t kOffPf = kOffPart + 2 * kNPart * 16 * kB / 2;
 constexpr int64_t kOffSf = kOffPf + 2 * 64;
-constexpr int64_t kOffDz1 = kOffSf + 64;
+constexpr int64_t kOffDz1 = kOffSf + 256;  // SF[256]: indexed by blockIdx
 constexpr int64_t kOffCx = kOffDz1 + kB * kD1;
 constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCX / 2;
 constexpr int64_t kOffWx = kOffCxf + 16;  // CXF: [part 0 = H1, part 1 = the rest][2][4]
@@ -174,7 +186,14 @@ constexpr int64_t kOffWf = kOffWx + 2 * kNG * kWX / 2;
 // granules (tag s + 1), written by the gk == 0 layer-1 blocks, polled directly
 // by the chains (no drain, no flag: one hop).
 constexpr int64_t kOffCg = kOffWf + 8;
-constexpr int64_t kTotalG = kOffCg + kB * kD1;
+// WXS[2][kWXS]: single replica, the gradient tiles' updated upper weights,
+// parity by step, in the chains' order: 3 layers W2 [64][128], W3 [16 o][64]
+// (o >= 10 zero), b2 [64], b3 [16]; 2 layers W2 [16 o][128], b2 [16].  WFS[2][16]
+// flags, one per tile.
+constexpr int kWXS = kH2 * kD1 + 16 * kH2 + kH2 + 16;   // 9296 floats
+constexpr int64_t kOffWxs = kOffCg + kB * kD1;
+constexpr int64_t kOffWfs = kOffWxs + 2 * kWXS / 2;
+constexpr int64_t kTotalG = kOffWfs + 32;
 static_assert(kCX % 4 == 0 && kWX % 4 == 0 && (kOffCx % 2) == 0 && (kOffWx % 2) == 0,
               "exchange rows travel as 16-B vectors");
 
@@ -489,11 +508,12 @@ __device__ __forceinline__ void pk_started(const PersistArgs& a, int blk, uint64
 // The upper group (4 chains + 4 gradient blocks, blocks 8 k): whether all of
 // it runs on ONE XCD, read from their SF granules (same answer in every
 // member).  false on a timeout (the caller's ok flag is cleared).
-__device__ __forceinline__ bool pk_upper_local(const PersistArgs& a, uint64_t s0, Poll& poll, bool& ok) {
-  __shared__ uint32_t xs[kNCH + kNG];
+__device__ __forceinline__ bool pk_upper_local(const PersistArgs& a, uint64_t s0, Poll& poll, bool& ok,
+                                               int count = kNCH + kNG) {
+  __shared__ uint32_t xs[32];
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   const int tid = threadIdx.x;
-  if (tid < kNCH + kNG) {
+  if (tid < count) {
     const int64_t g = kOffSf + 8 * tid;
     poll.start();
     uint4 f;
@@ -506,7 +526,7 @@ __device__ __forceinline__ bool pk_upper_local(const PersistArgs& a, uint64_t s0
   }
   ok = __syncthreads_and(ok ? 1 : 0) != 0;
   bool same = true;
-  for (int k = 1; k < kNCH + kNG; ++k) same = same && xs[k] == xs[0];
+  for (int k = 1; k < count; ++k) same = same && xs[k] == xs[0];
   return ok && same;
 }
 
@@ -809,6 +829,7 @@ __device__ __forceinline__ bool pk_l1_gather(__amdgpu_buffer_rsrc_t rb, f4v& z, 
   return true;
 }
 
+template <int NL>
 __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
@@ -912,7 +933,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
       Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
       Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
     }
-    if (lb == 0 && it + 1 == a.steps && tid < kNBlk && ok) {
+    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false) && pk_sr_active<NL>(tid) && ok) {
       // hand the step counter on once every block has read it (SF tags)
       const uint32_t t0 = (uint32_t)(s0 + 1);
       poll.start();
@@ -1076,6 +1097,76 @@ __device__ __forceinline__ void pk_w_commit(float* lds, const f4v (&v)[WSlices<N
   }
 }
 
+
+// Single replica: the upper weights in the chains' order (WXS layout) from the
+// gradient tiles' parity-`par` publication (from_wx) or, at the launch start,
+// from P; pk_w_commit_sr writes them into the chain's LDS.
+template <int NL> struct WSr { static constexpr int kTot = NL == 3 ? 2324 : 516,
+                                                    kIt = (kTot + kThreads - 1) / kThreads; };
+static_assert(WSr<3>::kIt == WSlices<3>::kIt && WSr<2>::kIt == WSlices<2>::kIt, "register budget");
+template <int NL>
+__device__ __forceinline__ void pk_w_fetch_sr(const PersistArgs& a, f4v (&v)[WSr<NL>::kIt], bool from_wx,
+                                              int par) {
+  const int tid = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  const int64_t base = kOffWxs * 2 + (int64_t)par * kWXS;
+  auto bias = [&](int boff, int o0) {
+    const float* bp = a.P + a.b_off[boff];
+    return f4v{o0 < kNC ? bp[o0] : 0.f, o0 + 1 < kNC ? bp[o0 + 1] : 0.f, o0 + 2 < kNC ? bp[o0 + 2] : 0.f,
+               o0 + 3 < kNC ? bp[o0 + 3] : 0.f};
+  };
+#pragma unroll
+  for (int j = 0; j < WSr<NL>::kIt; ++j) {
+    const int e = min(tid + j * kThreads, WSr<NL>::kTot - 1);
+    if (from_wx) {
+      v[j] = ld_f4(rb, base + 4 * e);  // the WXS order IS the fetch order
+      continue;
+    }
+    if constexpr (NL == 3) {
+      if (e < 2048) {
+        v[j] = *reinterpret_cast<const f4v*>(a.P + a.w_off[1] + 4 * e);
+      } else if (e < 2304) {
+        const int o = (e - 2048) >> 4, c4 = (e - 2048) & 15;
+        v[j] = o < kNC ? *reinterpret_cast<const f4v*>(a.P + a.w_off[2] + o * kH2 + 4 * c4)
+                       : f4v{0.f, 0.f, 0.f, 0.f};
+      } else if (e < 2320) {
+        v[j] = *reinterpret_cast<const f4v*>(a.P + a.b_off[1] + 4 * (e - 2304));
+      } else {
+        v[j] = bias(2, 4 * (e - 2320));
+      }
+    } else {
+      if (e < 512) {
+        const int o = e >> 5, c4 = e & 31;
+        v[j] = o < kNC ? *reinterpret_cast<const f4v*>(a.P + a.w_off[1] + o * kD1 + 4 * c4)
+                       : f4v{0.f, 0.f, 0.f, 0.f};
+      } else {
+        v[j] = bias(1, 4 * (e - 512));
+      }
+    }
+  }
+}
+template <int NL>
+__device__ __forceinline__ void pk_w_commit_sr(float* lds, const f4v (&v)[WSr<NL>::kIt]) {
+  using L = ChLay<NL>;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < WSr<NL>::kIt; ++j) {
+    const int e = tid + j * kThreads;
+    if (e >= WSr<NL>::kTot) continue;
+    float* dst;
+    if constexpr (NL == 3) {
+      if (e < 2048) dst = lds + L::W2 + (e >> 5) * kS1 + 4 * (e & 31);
+      else if (e < 2304) dst = lds + ChLay<3>::W3 + ((e - 2048) >> 4) * kS2 + 4 * ((e - 2048) & 15);
+      else if (e < 2320) dst = lds + L::B2 + 4 * (e - 2304);
+      else dst = lds + ChLay<3>::B3 + 4 * (e - 2320);
+    } else {
+      if (e < 512) dst = lds + L::W2 + (e >> 5) * kS1 + 4 * (e & 31);
+      else dst = lds + L::B2 + 4 * (e - 512);
+    }
+    dst[0] = v[j][0]; dst[1] = v[j][1]; dst[2] = v[j][2]; dst[3] = v[j][3];
+  }
+}
+
 // The chain's rows after H1 -> CX (3 layers: H2 [16][64], dZ2 [16][64], dZ3
 // [16][16]; 2 layers: dZ2 [16][16]), stored but not drained.
 template <int NL>
@@ -1130,8 +1221,13 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (c == 0) PK_EDGE(3);
   {
     f4v wv[WSlices<NL>::kIt];
-    pk_w_fetch<NL>(a, wv, false, 0);
-    pk_w_commit<NL>(lds, wv);
+    if constexpr (DP) {
+      pk_w_fetch<NL>(a, wv, false, 0);
+      pk_w_commit<NL>(lds, wv);
+    } else {
+      pk_w_fetch_sr<NL>(a, wv, false, 0);
+      pk_w_commit_sr<NL>(lds, wv);
+    }
   }
   if constexpr (NL == 3) {
     float* DZ3 = lds + L::DZ3;
@@ -1144,7 +1240,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (tid == 0) s_fail = 0u;
   __syncthreads();
   bool ok = true;
-  const bool local = pk_upper_local(a, s0, poll, ok);
+  const bool local = pk_upper_local(a, s0, poll, ok, DP ? kNCH + kNG : kNCH + GTile<NL>::kN);
   if (c == 0) PK_EDGE(4);
   if (c == 0 && g_pk_stamp_on && tid == 0) g_pk_stamps[3][1][0] = local ? 1u : 0u;
 
@@ -1177,14 +1273,19 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     auto fetch_w = [&]() {
       if (it > 0) {
         bool wok = true;
-        if (lane < kNG) wok = wait_flag(rb, kOffWf + (par ^ 1) * kNG + lane, tag - 1, poll);
+        if constexpr (DP) {
+          if (lane < kNG) wok = wait_flag(rb, kOffWf + (par ^ 1) * kNG + lane, tag - 1, poll);
+        } else {
+          if (lane < GTile<NL>::kN) wok = wait_flag(rb, kOffWfs + (par ^ 1) * 16 + lane, tag - 1, poll);
+        }
         wok = __builtin_amdgcn_ballot_w64(!wok) == 0;
         asm volatile("" ::: "memory");
-        if (wok) pk_w_fetch<NL>(a, wv, true, par ^ 1);
-        else ok = false;
+        if (!wok) ok = false;
+        else if constexpr (DP) pk_w_fetch<NL>(a, wv, true, par ^ 1);
+        else pk_w_fetch_sr<NL>(a, wv, true, par ^ 1);
       }
     };
-    constexpr bool kWFirst = DP && NL == 2;  // single replica: Z1 (one hop) comes before the weights
+    constexpr bool kWFirst = DP && NL == 2;  // single replica: Z1 before the weights (weights first: 7.16 -> 9.0 us)
     if (kWFirst) fetch_w();
     if constexpr (!DP) {
       // ---- H1 rows = relu(Z1(s)): the gk == 0 layer-1 blocks publish Z1 =
@@ -1233,7 +1334,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       // every wave's waits agreed on (drains the weight loads, consumed next)
       ok = __syncthreads_and(ok ? 1 : 0) != 0;
       if (!ok) break;
-      if (it > 0) pk_w_commit<NL>(lds, wv);
+      if (it > 0) pk_w_commit_sr<NL>(lds, wv);
     } else {
       // ---- H1 rows = relu(sum of the 7 k-partials) ----
       // this chain's 16 rows of every partial in one bulk read: thread -> (gn,
@@ -1792,6 +1893,228 @@ __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g,
   pk_report(a, ok);
 }
 
+
+// -----------------------------------------------------------------------------
+// Gradient tile (single replica): full-batch dW / db + SGD of one tile of the
+// upper weights.  3 layers, tile g: W2 rows 16 gh .. +15 x columns 32 gn .. +31
+// (gh = g / 4, gn = g % 4); the gn == 0 tiles also own W3 columns 16 gh .. +15
+// and b2[16 gh ..], tile 0 b3.  2 layers, tile g: W2 columns 16 g .. +15 (all
+// class rows); tile 0 b2.
+// -----------------------------------------------------------------------------
+struct GTLay {
+  static constexpr int H1T = 0;                 // [32 n][kST] (rows contiguous)
+  static constexpr int DZ2T = H1T + 32 * kST;   // [16][kST]
+  static constexpr int H2T = DZ2T + 16 * kST;   // [16][kST]
+  static constexpr int DZ3T = H2T + 16 * kST;   // [16][kST]
+  static constexpr int W2 = DZ3T + 16 * kST;    // tile [16][33]
+  static constexpr int W3 = W2 + 16 * 33;       // [16 o][17]
+  static constexpr int B = W3 + 16 * 17;        // b2 slice [16], b3 [16]
+  static constexpr int TOTAL = B + 32;
+};
+
+template <int NL>
+__device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  pk_started(a, blk, s0);
+  float* H1T = lds + GTLay::H1T;
+  float* DZ2T = lds + GTLay::DZ2T;
+  float* H2T = lds + GTLay::H2T;
+  float* DZ3T = lds + GTLay::DZ3T;
+  float* W2 = lds + GTLay::W2;
+  float* W3 = lds + GTLay::W3;
+  float* Bs = lds + GTLay::B;
+  // tile geometry: W2 rows r0 .. r0 + 15 (3 layers: h; 2 layers: class o),
+  // columns n0 .. n0 + nw - 1
+  constexpr int nw = NL == 3 ? 32 : 16;
+  const int gh = NL == 3 ? g >> 2 : 0;
+  const int n0 = NL == 3 ? 32 * (g & 3) : 16 * g;
+  const bool own3 = NL == 3 && (g & 3) == 0;  // W3 columns + b2 slice (3 layers)
+  const int r0 = 16 * gh;
+
+  // ---- prologue: the tile (and its extras) from P ----
+  for (int e = tid; e < 16 * nw; e += kThreads) {
+    const int r = e / nw, c = e - r * nw;
+    W2[r * 33 + c] = (NL == 3 || r < kNC) ? a.P[a.w_off[1] + (int64_t)(r0 + r) * kD1 + n0 + c] : 0.f;
+  }
+  if (own3) {
+    const int o = tid >> 4, j = tid & 15;
+    W3[o * 17 + j] = o < kNC ? a.P[a.w_off[2] + (int64_t)o * kH2 + r0 + j] : 0.f;
+    if (tid < 16) Bs[tid] = a.P[a.b_off[1] + r0 + tid];
+  }
+  if (g == 0 && tid < 16) {
+    if constexpr (NL == 3) Bs[16 + tid] = tid < kNC ? a.P[a.b_off[2] + tid] : 0.f;
+    else Bs[tid] = tid < kNC ? a.P[a.b_off[1] + tid] : 0.f;
+  }
+  __syncthreads();
+  bool ok = true;
+  const bool local = pk_upper_local(a, s0, poll, ok, kNCH + GTile<NL>::kN);
+  const int stamp_on = g_pk_stamp_on && g == 0;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    PK_STAMP(2, 0);
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);
+    const int par = (int)(s & 1);
+    // ---- part 0: the tile's H1 columns of the 64 rows (flagged in the chains' forward) ----
+    if (tid < kNCH && !wait_flag(rb, kOffCxf + par * kNCH + tid, tag, poll)) ok = false;
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (!ok) break;
+    {
+      constexpr int kC4 = nw / 4, kIt = 64 * kC4 / kThreads;  // f4 per row, per thread
+      f4v v[kIt];
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int x = tid + j * kThreads, r = x / kC4, c4 = x - r * kC4;
+        v[j] = ld_f4(rb, kOffCx * 2 + ((int64_t)par * kNCH + (r >> 4)) * kCX + (r & 15) * kD1 + n0 + 4 * c4);
+      }
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int x = tid + j * kThreads, r = x / kC4, c4 = x - r * kC4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) H1T[(4 * c4 + e) * kST + r] = v[j][e];
+      }
+    }
+    // ---- part 1: the rest of the rows (flagged at the end of the chains' step) ----
+    if (tid < kNCH && !wait_flag(rb, kOffCxf + 8 + par * kNCH + tid, tag, poll)) ok = false;
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (!ok) break;
+    {
+      // thread -> row r = tid / 4, 4 columns 4 (tid % 4); 3 layers: dZ2 slice
+      // (and H2 slice + dZ3 for the W3 owners); 2 layers: the logits' gradient
+      const int r = tid >> 2, c4 = tid & 3;
+      const int64_t rowb = kOffCx * 2 + ((int64_t)par * kNCH + (r >> 4)) * kCX + (r & 15) * (NL == 3 ? kH2 : 16);
+      f4v vd, vh = {0.f, 0.f, 0.f, 0.f}, v3 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (NL == 3) {
+        vd = ld_f4(rb, rowb + 3072 + r0 + 4 * c4);    // dZ2 [16][64] at 3072 of the chain's run
+        if (own3) {
+          vh = ld_f4(rb, rowb + 2048 + r0 + 4 * c4);  // H2 [16][64] at 2048
+          v3 = ld_f4(rb, kOffCx * 2 + ((int64_t)par * kNCH + (r >> 4)) * kCX + 4096 + (r & 15) * 16 + 4 * c4);
+        }
+      } else {
+        vd = ld_f4(rb, rowb + 2048 + 4 * c4);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        DZ2T[(4 * c4 + e) * kST + r] = vd[e];
+        if (own3) {
+          H2T[(4 * c4 + e) * kST + r] = vh[e];
+          DZ3T[(4 * c4 + e) * kST + r] = v3[e];
+        }
+      }
+    }
+    __syncthreads();
+    PK_STAMP(2, 1);
+
+    // ---- gradients: 16 MFMAs per 16 x 16 output tile (K = the 64 rows), each
+    // lane's 16-B LDS reads feeding 4 MFMAs (k = 16 gq + 4 q + j) ----
+    f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+    float sb = 0.f;
+    auto tile16 = [&](const float* A, const float* Bm) {
+      f32x4 c[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 av = *reinterpret_cast<const float4*>(A + i * kST + 16 * gq + 4 * q);
+        const float4 bv = *reinterpret_cast<const float4*>(Bm + i * kST + 16 * gq + 4 * q);
+        c[0] = mfma_f32_16x16x4(av.x, bv.x, c[0]);
+        c[1] = mfma_f32_16x16x4(av.y, bv.y, c[1]);
+        c[2] = mfma_f32_16x16x4(av.z, bv.z, c[2]);
+        c[3] = mfma_f32_16x16x4(av.w, bv.w, c[3]);
+      }
+      return (c[0] + c[1]) + (c[2] + c[3]);
+    };
+    auto rowsum = [&](const float* A) {  // sum over the 64 rows of feature i (16 lanes x 4 q)
+      float t = 0.f;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 x = *reinterpret_cast<const float4*>(A + i * kST + 16 * gq + 4 * q);
+        t += (x.x + x.y) + (x.z + x.w);
+      }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      return t;
+    };
+    if constexpr (NL == 3) {
+      if (w < 2) gw = tile16(DZ2T, H1T + 16 * w * kST);          // dW2 [16 h][16 n]
+      else if (w == 2 && own3) gw = tile16(DZ3T, H2T);           // dW3 [16 o][16 h]
+      else if (w == 3 && own3) sb = rowsum(DZ2T);                // db2 slice
+      float sb3 = 0.f;
+      if (w == 3 && g == 0) sb3 = rowsum(DZ3T);                  // db3
+      PK_STAMP(2, 2);
+      // ---- SGD on the resident tile ----
+      if (w < 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W2[(4 * q + r) * 33 + 16 * w + i] -= a.lr * gw[r];
+      } else if (w == 2 && own3) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * q + r < kNC) W3[(4 * q + r) * 17 + i] -= a.lr * gw[r];
+      } else if (w == 3 && q == 0) {
+        if (own3) Bs[i] -= a.lr * sb;
+        if (g == 0 && i < kNC) Bs[16 + i] -= a.lr * sb3;
+      }
+    } else {
+      if (w == 0) gw = tile16(DZ2T, H1T);                         // dW2 [16 o][16 n]
+      else if (w == 1 && g == 0) sb = rowsum(DZ2T);               // db2
+      PK_STAMP(2, 2);
+      if (w == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * q + r < kNC) W2[(4 * q + r) * 33 + i] -= a.lr * gw[r];
+      } else if (w == 1 && g == 0 && q == 0 && i < kNC) {
+        Bs[i] -= a.lr * sb;
+      }
+    }
+    __syncthreads();
+    PK_STAMP(2, 3);
+    // ---- publish the tile into WXS[par] (the chains' order) ----
+    {
+      const int64_t base = kOffWxs * 2 + (int64_t)par * kWXS;
+      constexpr int kT4 = 16 * nw / 4;  // f4 of the W2 tile
+      if (tid < kT4) {
+        const int r = tid / (nw / 4), c4 = tid - r * (nw / 4);
+        const float* src = W2 + r * 33 + 4 * c4;
+        st_up4(rb, base + (int64_t)(r0 + r) * kD1 + n0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
+      } else if (NL == 3 && own3 && tid < kT4 + 64) {
+        const int x = tid - kT4, o = x >> 2, c4 = x & 3;
+        const float* src = W3 + o * 17 + 4 * c4;
+        st_up4(rb, base + kH2 * kD1 + o * kH2 + r0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
+      } else if (NL == 3 && own3 && tid < kT4 + 68) {
+        const int c4 = tid - kT4 - 64;
+        st_up4(rb, base + kH2 * kD1 + 16 * kH2 + r0 + 4 * c4,
+               f4v{Bs[4 * c4], Bs[4 * c4 + 1], Bs[4 * c4 + 2], Bs[4 * c4 + 3]}, local);
+      } else if (g == 0 && tid >= 200 && tid < 204) {
+        const int c4 = tid - 200;
+        const float* src = Bs + (NL == 3 ? 16 : 0) + 4 * c4;
+        st_up4(rb, base + (NL == 3 ? kH2 * kD1 + 16 * kH2 + kH2 : 16 * kD1) + 4 * c4,
+               f4v{src[0], src[1], src[2], src[3]}, local);
+      }
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_gran(rb, kOffWfs + par * 16 + g, __uint_as_float(tag), tag);
+    PK_STAMP(2, 4);
+  }
+
+  // ---- epilogue: the tile back to HBM ----
+  for (int e = tid; e < 16 * nw; e += kThreads) {
+    const int r = e / nw, c = e - r * nw;
+    if (NL == 3 || r < kNC) a.P[a.w_off[1] + (int64_t)(r0 + r) * kD1 + n0 + c] = W2[r * 33 + c];
+  }
+  if (own3) {
+    const int o = tid >> 4, j = tid & 15;
+    if (o < kNC) a.P[a.w_off[2] + (int64_t)o * kH2 + r0 + j] = W3[o * 17 + j];
+    if (tid < 16) a.P[a.b_off[1] + r0 + tid] = Bs[tid];
+  }
+  if (g == 0 && tid < kNC) {
+    if constexpr (NL == 3) a.P[a.b_off[2] + tid] = Bs[16 + tid];
+    else a.P[a.b_off[1] + tid] = Bs[tid];
+  }
+  pk_report(a, ok);
+}
+
 // DP: the data-parallel form (replica exchange compiled in); the single-replica
 // launch runs the exchange-free code.  Placement (speed only, every hand-off is
 // placement-independent): under round-robin dispatch blocks b and b + 8 share
@@ -1805,12 +2128,24 @@ void mlp_persist_k(PersistArgs a) {
   float* lds = reinterpret_cast<float*>(lds4);
   const int b = blockIdx.x;
   const int x = b & 7, y = b >> 3;
-  if (x == 0) {
-    if (y < kNCH) pk_chain<NL, DP>(a, lds, y, b);
-    else pk_grad<NL, DP>(a, lds, y - kNCH, b);
+  if constexpr (DP) {
+    if (x == 0) {
+      if (y < kNCH) pk_chain<NL, true>(a, lds, y, b);
+      else pk_grad<NL, true>(a, lds, y - kNCH, b);
+    } else {
+      pk_layer1<true>(a, lds, y + kGN * (x - 1), b);
+    }
   } else {
-    if constexpr (DP) pk_layer1<true>(a, lds, y + kGN * (x - 1), b);
-    else pk_layer1_gram(a, lds, y + kGN * (x - 1), b);
+    // 4 chains + the gradient tiles at blockIdx 8 k (one XCD under
+    // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
+    // grid's other blocks exit at once
+    if (!pk_sr_active<NL>(b)) return;
+    if (x == 0) {
+      if (y < kNCH) pk_chain<NL, false>(a, lds, y, b);
+      else pk_gtile<NL>(a, lds, y - kNCH, b);
+    } else {
+      pk_layer1_gram<NL>(a, lds, y + kGN * (x - 1), b);
+    }
   }
 }
 
@@ -1851,10 +2186,10 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return e;
-    if (per_cu < 1 || per_cu * cus < kNBlk) return hipErrorCooperativeLaunchTooLarge;
+    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(DP)) return hipErrorCooperativeLaunchTooLarge;
     attr = true;
   }
-  hipLaunchKernelGGL((mlp_persist_k<NL, DP>), dim3(kNBlk), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((mlp_persist_k<NL, DP>), dim3(pk_grid<NL>(DP)), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
