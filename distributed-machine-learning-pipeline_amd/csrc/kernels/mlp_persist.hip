@@ -62,7 +62,7 @@ constexpr int kGN = 8, kGK = 7, kKC = kD0 / kGK;        // 112 k per layer-1 blo
 constexpr int kNL1 = kGN * kGK;                         // 56 layer-1 blocks
 constexpr int kNCH = 4, kNG = 4;                        // chains (16 rows each), gradient blocks
 constexpr int kNBlk = kNL1 + kNCH + kNG;                // 64
-constexpr int kNPart = kNL1 + kGN;                      // partial slots: 56 layer-1 + 8 corrections
+constexpr int kNPart = kNL1;                            // partial slots per parity
 // Single replica: the upper weights' full-batch gradients + SGD run in
 // gradient TILES (W2 [16 h x 32 n] tiles of the 3-layer model, [16 o x 16 n]
 // tiles of the 2-layer one) -- each loads only its operand columns and
@@ -156,11 +156,11 @@ constexpr int lds_floats() {
 static_assert(lds_floats<3>() * 4 <= 160 * 1024 && lds_floats<2>() * 4 <= 160 * 1024, "LDS budget");
 
 // ---- hand-off buffer layout (8-byte granules) --------------------------------
-// PART[2][64][4][16][16] partials [parity][slot][chain][n][row], plain fp32:
-//                   slots 0-55 the layer-1 blocks' k-partials of Z1 (b1 added by
-//                   gk == 0), slots 56-63 (single replica) the Gram corrections
-//                   of the 8 column tiles; one flag per slot, parity and step
-//                   (PF[2][64]).  The data-parallel form uses parity 0, slots < 56.
+// PART[2][56][4][16][16] partials [parity][slot][chain][n][row], plain fp32:
+//                   the layer-1 blocks' k-partials of Z1 (b1 added by gk == 0);
+//                   one flag per slot, parity and step (PF[2][64]).  The
+//                   data-parallel form uses parity 0 (read by the chains); the
+//                   single replica both parities (read by the gk == 0 blocks).
 // SF[64]            started flags (tag = first step + 1): the step counter is
 //                   handed on only once every block has read it
 // DZ1[64][128]      activation gradient of layer 1, tagged granules
@@ -1188,20 +1188,6 @@ __device__ __forceinline__ void pk_chain_rows_out(__amdgpu_buffer_rsrc_t rb, con
   }
 }
 
-// Per-wave wait for partial-slot flags: lane j < nflags polls slot slot_of(j)
-// of parity `par` for `tag`, then a wave vote -- no workgroup barrier, so the
-// wave's loads already in flight are not drained.  false: a wait gave up.
-template <typename F>
-__device__ __forceinline__ bool pk_wave_wait(__amdgpu_buffer_rsrc_t rb, int par, int nflags, F slot_of,
-                                             uint32_t tag, Poll& poll) {
-  const int lane = threadIdx.x & 63;
-  bool ok = true;
-  if (lane < nflags) ok = wait_flag(rb, pk_pf(par, slot_of(lane)), tag, poll);
-  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
-  asm volatile("" ::: "memory");
-  return ok;
-}
-
 template <int NL, bool DP>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c, int blk) {
   using L = ChLay<NL>;
@@ -1247,8 +1233,6 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   const int stamp_on = g_pk_stamp_on && c == 0;
   // thread -> (column tile gn, column n, 8 rows) of this chain's H1 block
   const int pgn = tid >> 5, pn = (tid >> 1) & 15, phalf = tid & 1;
-  // wave w's partial slots: gn = 2 w, 2 w + 1 of every gk (lane j -> slot)
-  auto l1_slot = [&](int j) { return 2 * w + (j & 1) + kGN * (j >> 1); };
   for (int it = 0; ok && it < a.steps; ++it) {
     PK_STAMP(1, 0);
     const uint64_t s = s0 + (uint64_t)it;
