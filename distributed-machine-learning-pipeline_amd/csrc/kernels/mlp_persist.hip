@@ -178,7 +178,11 @@ constexpr int64_t kOffPart = 0;
 constexpr int64_t kOffPf = kOffPart + 2 * kNPart * 16 * kB / 2;
 constexpr int64_t kOffSf = kOffPf + 2 * 64;
 constexpr int64_t kOffDz1 = kOffSf + 256;  // SF[256]: indexed by blockIdx
-constexpr int64_t kOffCx = kOffDz1 + kB * kD1;
+// DZ1[2][64][128]: parity by step in the single-replica step (there the
+// chains' next step does not wait for the gk >= 1 layer-1 blocks to have read
+// this step's dZ1, so it must not overwrite it); the data-parallel step (where
+// it does wait, through every block's partials) uses parity 0
+constexpr int64_t kOffCx = kOffDz1 + 2 * kB * kD1;
 constexpr int64_t kOffCxf = kOffCx + 2 * kNCH * kCX / 2;
 constexpr int64_t kOffWx = kOffCxf + 16;  // CXF: [part 0 = H1, part 1 = the rest][2][4]
 constexpr int64_t kOffWf = kOffWx + 2 * kNG * kWX / 2;
@@ -919,7 +923,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
     {
       const int m = tid >> 2, qq = tid & 3;
-      const int64_t g = kOffDz1 + (int64_t)m * kD1 + n0 + 4 * qq;
+      const int64_t g = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
       uint4 v0, v1;
       poll.start();
       for (;;) {
@@ -1477,7 +1481,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           for (int r = 0; r < 4; ++r) {
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? a0[tt][r] + a1[tt][r] : 0.f;
-            st_gran(rb, kOffDz1 + (int64_t)(rb0 + m) * kD1 + n, v, tag);
+            st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
           }
         }
       }
@@ -1547,7 +1551,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           for (int r = 0; r < 4; ++r) {
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? acc[tt][r] : 0.f;
-            st_gran(rb, kOffDz1 + (int64_t)(rb0 + m) * kD1 + n, v, tag);
+            st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
           }
         }
       }
