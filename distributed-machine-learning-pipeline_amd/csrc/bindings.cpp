@@ -701,6 +701,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
+  m.def("mlp_persist_set_jitter", [](int ticks) { mlp_persist_set_jitter(ticks); },
+        "testing only: every block of the single-replica persistent step sleeps a pseudo-random "
+        "0..ticks x 64 cycles before its hand-offs (0 = off)");
   m.def("mlp_plan", [](const std::vector<int64_t>& desc) {
     const MlpDesc d = desc_from_list(desc);
     const MlpLaunchCfg c = mlp_plan_first_layer(d);

@@ -299,6 +299,21 @@ __device__ __forceinline__ float4 px_ld4(const __amdgpu_buffer_rsrc_t& r, int of
 // [5] exit).
 __device__ uint64_t g_pk_stamps[4][8][8];
 __device__ int g_pk_stamp_on;
+// Testing only: uneven-load injection.  With g_pk_jitter = J > 0 every block
+// of the single-replica step sleeps a pseudo-random 0..J x 64 cycles before
+// its hand-off waits and publications, so producers and consumers drift
+// apart by microseconds -- the results must stay bit-identical
+// (tests/test_gpu_persist.py).  0 in production: one scalar load per block.
+__device__ int g_pk_jitter;
+__device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
+  if (jit <= 0) return;
+  uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
+  h ^= h >> 13;
+  h *= 0x5bd1e995u;
+  h ^= h >> 15;
+  const int n = (int)(h % (uint32_t)(jit + 1));
+  for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);
+}
 #define PK_EDGE(ph)                                                                   \
   do {                                                                                \
     if (g_pk_stamp_on && threadIdx.x == 0)                                            \
@@ -848,6 +863,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
   float* B1 = lds + L1GLay::B1;
   float* Gl = lds + L1GLay::G;
   auto xbuf = [&](uint64_t s) { return lds + L1GLay::X0 + (int)(s % 3u) * (kB * kKC); };
+  const int jit = g_pk_jitter;
 
   if (lb == 0) PK_EDGE(0);
   // ---- prologue: W1 tile, b1 slice, X of the first two steps ----
@@ -901,6 +917,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     const uint32_t tag = (uint32_t)(s + 1);       // step s
     const uint32_t tagn = tag + 1;                 // step s + 1
     const int parn = (int)((s + 1) & 1);
+    pk_jit(jit, blk, s, 1);
 
     // ---- P(s+1) = X(s+1) W1(s)^T + b1(s), before dZ1(s) exists: published
     // by gk >= 1; the gk == 0 block keeps its own and gathers the other six ----
@@ -919,6 +936,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     // Gram block of step s+1 for the correction
     pk_glds_x_to(a, xbuf(s + 2), s + 2, lane, w, k0);
     if (gk == 0) pk_glds_gram(a, Gl, s + 1, lane, w);
+    pk_jit(jit, blk, s, 2);
 
     // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
     {
@@ -1235,6 +1253,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (c == 0 && g_pk_stamp_on && tid == 0) g_pk_stamps[3][1][0] = local ? 1u : 0u;
 
   const int stamp_on = g_pk_stamp_on && c == 0;
+  const int jit = DP ? 0 : g_pk_jitter;
   // thread -> (column tile gn, column n, 8 rows) of this chain's H1 block
   const int pgn = tid >> 5, pn = (tid >> 1) & 15, phalf = tid & 1;
   for (int it = 0; ok && it < a.steps; ++it) {
@@ -1243,6 +1262,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
     const uint32_t tag = (uint32_t)(s + 1);
     const int par = (int)(s & 1);
     const int64_t r0 = (int64_t)(s % (uint64_t)a.nbatches) * a.batch;
+    if constexpr (!DP) pk_jit(jit, blk, s, 3);
 
     // this step's labels first: their memory round trip hides under the waits
     const int srow = w * 4 + (lane >> 4);  // softmax: 16 lanes per row, 4 rows per wave
@@ -1941,11 +1961,13 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
   bool ok = true;
   const bool local = pk_upper_local(a, s0, poll, ok, kNCH + GTile<NL>::kN);
   const int stamp_on = g_pk_stamp_on && g == 0;
+  const int jit = g_pk_jitter;
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(2, 0);
     const uint64_t s = s0 + (uint64_t)it;
     const uint32_t tag = (uint32_t)(s + 1);
     const int par = (int)(s & 1);
+    pk_jit(jit, blk, s, 4);
     // ---- part 0: the tile's H1 columns of the 64 rows (flagged in the chains' forward) ----
     if (tid < kNCH && !wait_flag(rb, kOffCxf + par * kNCH + tid, tag, poll)) ok = false;
     ok = __syncthreads_and(ok ? 1 : 0) != 0;
@@ -2057,6 +2079,7 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
     }
     __syncthreads();
     PK_STAMP(2, 3);
+    pk_jit(jit, blk, s, 5);
     // ---- publish the tile into WXS[par] (the chains' order) ----
     {
       const int64_t base = kOffWxs * 2 + (int64_t)par * kWXS;
@@ -2140,6 +2163,10 @@ void mlp_persist_k(PersistArgs a) {
 hipError_t mlp_persist_read_stamps(uint64_t* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pk_stamps), sizeof(uint64_t) * 4 * 8 * 8, 0,
                              hipMemcpyDeviceToHost);
+}
+void mlp_persist_set_jitter(int ticks) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_jitter), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
 }
 void mlp_persist_set_stamping(bool on) {
   const int v = on ? 1 : 0;

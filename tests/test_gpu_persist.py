@@ -122,3 +122,26 @@ def test_persistent_handoff_timeout_is_reported_and_recoverable():
     t.train_steps(3)
     t.synchronize()
     assert not t.runner.persist_failed()
+
+
+@pytest.mark.parametrize("spec", [SPEC, REF_SPEC], ids=str)
+def test_persistent_uneven_load_is_bit_exact(spec):
+    """Uneven load: with jitter injection every block sleeps a pseudo-random
+    0-8 us before its hand-off waits and publications, so producers and
+    consumers (and the chains among themselves) drift apart; the parity /
+    tag protocol must still give the same bits, across a launch split too."""
+    from hipdsml.ops.native import require_native
+
+    C = require_native()
+    ds = synthetic_mnist(64 * 5, seed=16)
+    a, b = _tr(ds, True, spec=spec), _tr(ds, True, spec=spec)
+    a.train_steps(23)
+    a.synchronize()
+    C.mlp_persist_set_jitter(300)
+    try:
+        for n in (9, 14):
+            b.train_steps(n)
+        b.synchronize()
+    finally:
+        C.mlp_persist_set_jitter(0)
+    assert torch.equal(a.P, b.P)
