@@ -179,8 +179,8 @@ def run(a) -> int:
         sync_us = tr.sync_times  # auto already timed every candidate
     elif n > 1 and tr.backend == "hip" and not a.no_sync_sweep:
         # every sync candidate's µs/step, measured the way training runs it
-        cands = (["pk", "pk2", "xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu
-                 else ["pk", "pk2", "xact", "xgmi", "torch"])
+        cands = (["pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu
+                 else ["pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "torch"])
         sync_us = tr.time_sync_modes(cands, steps=max(100, a.graph_steps * 2))
     tr.train_steps(a.warmup)
     tr.synchronize()
@@ -271,11 +271,14 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--sync", default="auto",
-                    choices=["auto", "pk", "pk2", "xact", "xgmi", "rccl", "ring", "torch"],
+                    choices=["auto", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch"],
                     help="gradient sync (N>1): pk = the one-launch persistent step with the weight "
                          "gradients summed over the replicas inside the launch (xGMI pushes of "
                          "every slot to every peer), pk2 = the same with a two-shot sum "
                          "(reduce-scatter + all-gather per slot, 2(N-1)/N slots per link), "
+                         "pkg / pkg2 = the persistent step in Gram form across replicas (every "
+                         "peer's dZ1 pushed for the layer-1 correction; gradient slots summed "
+                         "one- / two-shot off the critical path), "
                          "xact = activation exchange over xGMI (every GPU "
                          "pushes its activations and computes the global-batch weight gradients), "
                          "xgmi = one-shot gradient exchange fused into the weight-gradient kernel, "

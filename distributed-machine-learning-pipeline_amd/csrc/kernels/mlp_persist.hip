@@ -136,6 +136,7 @@ template <> struct GLay<2> {
   static constexpr int B2 = W2 + 16 * kSW;           // [16]
   static constexpr int TOTAL = B2 + 16;
 };
+constexpr int cmax_(int a, int b) { return a > b ? a : b; }
 // Layer-1 block of the single-replica (Gram-corrected) step: three X tiles
 // (X(s) for the backward, X(s+1) for the next forward, X(s+2) in flight), and
 // in the gk == 0 blocks the Gram block G1^T(s+1) = (X(s) X(s+1)^T + 1) [64][64].
@@ -144,8 +145,10 @@ struct L1GLay {
   static constexpr int W = X0 + 3 * kB * kKC;         // W1 tile [16][kXS]
   static constexpr int DZ = W + 16 * kXS;             // dZ1 tile [64][17]
   static constexpr int B1 = DZ + kB * 17;             // b1 slice [16]
-  static constexpr int G = B1 + 16;                   // G1^T [64 m'][64 m] (LDS-DMA image)
-  static constexpr int TOTAL = G + kB * kB;
+  static constexpr int G = B1 + 16;                   // G1^T [64 m'][64 m] (LDS-DMA image); in the
+                                                      // data-parallel form the other replicas'
+                                                      // dZ1 tiles [kMaxPeers - 1][64][17] instead
+  static constexpr int TOTAL = G + cmax_(kB * kB, (kMaxPeers - 1) * kB * 17);
 };
 static_assert(L1GLay::G % 4 == 0, "LDS-DMA image must be 16-B aligned");
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -359,6 +362,8 @@ struct PersistArgs {
   int32_t algo;    // 0: one-shot (every slot to every peer), 1: two-shot (reduce-scatter + all-gather)
   int64_t xhalf;   // floats per parity half of a receive buffer (>= px_half)
   uint32_t* xerr;  // the exchange's error word (a peer that did not arrive)
+  int32_t pxslots;  // wave slots per source (kPxSlots; kPxSlotsG in the Gram form)
+  int64_t dzr_off;  // Gram form: floats from a parity half's start to its dZ1 receive region
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -367,8 +372,20 @@ struct PersistArgs {
 constexpr int kPxSlot = 64 * 16, kPxSlots = kNL1 * 4 + kNG * 4;
 // Two-shot adds an all-gather region [slot][64 lanes][16 floats] per parity
 // half and its flags [owner][slot].
-int64_t px_half(int n, int algo) { return (int64_t)(n + (algo ? 1 : 0)) * kPxSlots * kPxSlot; }
-int px_ntiles(int n, int algo) { return (algo ? 2 : 1) * n * kPxSlots; }
+// Data-parallel Gram form (algo 2 / 3 = one- / two-shot slot sums): slots
+// 0..223 the layer-1 waves as above, 224..287 gradient tile g, wave w at
+// 224 + 4 g + w; after the slot regions of a parity half, every source's dZ1
+// rows as tagged granules DZR[src][64][128] (2 floats a granule).
+constexpr int kPxSlotsG = kNL1 * 4 + 16 * 4;
+constexpr int64_t kDzrFloats = (int64_t)kB * kD1 * 2;
+static int64_t px_slots_half(int n, int algo, int slots) {
+  return (int64_t)(n + ((algo & 1) ? 1 : 0)) * slots * kPxSlot;
+}
+int64_t px_half(int n, int algo) {
+  if (algo >= 2) return px_slots_half(n, algo, kPxSlotsG) + n * kDzrFloats;
+  return px_slots_half(n, algo, kPxSlots);
+}
+int px_ntiles(int n, int algo) { return ((algo & 1) ? 2 : 1) * n * (algo >= 2 ? kPxSlotsG : kPxSlots); }
 
 // One wave's slot: push v into every peer, raise their flags, wait for every
 // peer's slot of step s here, then v = the rank-ordered sum over all
@@ -378,7 +395,7 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
                                                   int slot) {
   const int lane = threadIdx.x & 63;
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
-  const int64_t per_src = (int64_t)kPxSlots * kPxSlot;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint64_t tag = s + 1;
   for (int d = 0; d < a.nrep; ++d) {
     if (d == a.rep) continue;
@@ -393,11 +410,11 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   if (lane == 0)
     for (int d = 0; d < a.nrep; ++d)
       if (d != a.rep)
-        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + a.rep * kPxSlots), tag,
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + a.rep * a.pxslots), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool ok = true;
   if (lane < a.nrep && lane != a.rep)
-    ok = poll_flag_ge<1>(a.xt.flags[a.rep] + slot + lane * kPxSlots, tag, a.xerr, a.timeout_ticks);
+    ok = poll_flag_ge<1>(a.xt.flags[a.rep] + slot + lane * a.pxslots, tag, a.xerr, a.timeout_ticks);
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
   if (!ok) return false;
@@ -431,7 +448,7 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
   const int n = a.nrep, me = a.rep;
   const int own = lane % n;
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
-  const int64_t per_src = (int64_t)kPxSlots * kPxSlot;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const int64_t ag = (int64_t)n * per_src;  // all-gather region of a parity half
   const uint64_t tag = s + 1;
   // ---- reduce-scatter: values to their owner ----
@@ -448,11 +465,11 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
   if (lane == 0)
     for (int d = 0; d < n; ++d)
       if (d != me)
-        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + me * kPxSlots), tag,
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + me * a.pxslots), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool ok = true;
   if (lane < n && lane != me)
-    ok = poll_flag_ge<1>(a.xt.flags[me] + slot + lane * kPxSlots, tag, a.xerr, a.timeout_ticks);
+    ok = poll_flag_ge<1>(a.xt.flags[me] + slot + lane * a.pxslots, tag, a.xerr, a.timeout_ticks);
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
   if (!ok) return false;
@@ -485,11 +502,11 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
   if (lane == 0)
     for (int d = 0; d < n; ++d)
       if (d != me)
-        __hip_atomic_store((px_g64*)(a.xt.flags[d] + n * kPxSlots + me * kPxSlots + slot), tag,
+        __hip_atomic_store((px_g64*)(a.xt.flags[d] + n * a.pxslots + me * a.pxslots + slot), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   ok = true;
   if (lane < n && lane != me)
-    ok = poll_flag_ge<1>(a.xt.flags[me] + n * kPxSlots + lane * kPxSlots + slot, tag, a.xerr,
+    ok = poll_flag_ge<1>(a.xt.flags[me] + n * a.pxslots + lane * a.pxslots + slot, tag, a.xerr,
                          a.timeout_ticks);
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
@@ -848,7 +865,13 @@ __device__ __forceinline__ bool pk_l1_gather(__amdgpu_buffer_rsrc_t rb, f4v& z, 
   return true;
 }
 
-template <int NL>
+// XM: the data-parallel Gram form.  Each replica r's correction then sums over
+// every replica r': C_r(s+1) = -(lr/N) sum_r' (X_r(s+1) X_r'(s)^T + 1) dZ1_r'(s),
+// with every peer's dZ1 rows pushed by its chains into this replica's DZR
+// region (tagged granules) and the cross-replica Gram blocks from the table
+// [nbatches][N][64 m'][64 m]; the W1 update sums each wave's dW1 fragments
+// over the replicas (the pk slot exchange) -- off the critical path here.
+template <int NL, bool XM>
 __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
@@ -935,7 +958,24 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     // finished before the barrier that ended that step); the column tile's
     // Gram block of step s+1 for the correction
     pk_glds_x_to(a, xbuf(s + 2), s + 2, lane, w, k0);
-    if (gk == 0) pk_glds_gram(a, Gl, s + 1, lane, w);
+    // the cross-replica Gram blocks of step s+1 go straight into registers
+    // (data only: in flight during the dZ1 wait): lane (i, q) holds
+    // G[r'][m = 16 w + i][m' = 4 ks + q] for ks = 0..15
+    float gv[XM ? kMaxPeers : 1][16];
+    if constexpr (XM) {
+      if (gk == 0) {
+        const float* gb = a.gram + (int64_t)((s + 1) % (uint64_t)a.nbatches) * a.nrep * (kB * kB);
+#pragma unroll
+        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
+          if (r2 < a.nrep) {
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) gv[r2][ks] = gb[((int64_t)r2 * kB + 4 * ks + q) * kB + 16 * w + i];
+          }
+        }
+      }
+    } else {
+      if (gk == 0) pk_glds_gram(a, Gl, s + 1, lane, w);
+    }
     pk_jit(jit, blk, s, 2);
 
     // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
@@ -972,13 +1012,51 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     PK_STAMP(0, 2);
 
     // ---- gk == 0: C(s+1)[64 x 16] = -lr G1(s+1) dZ1(s)[:, tile]; wave w: rows
-    // 16 w .. +15 (chain w's rows), K = 64 batch rows ----
+    // 16 w .. +15 (chain w's rows), K = 64 batch rows (x N replicas) ----
     if (gk == 0) {
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (XM) {
+        // every other replica's dZ1[:, tile] (pushed by its chains), in rank order
+        float* DzX = Gl;
+        const int m = tid >> 2, qq = tid & 3;
+        bool pok = true;
+        for (int r2 = 0, slot = 0; r2 < a.nrep; ++r2) {
+          if (r2 == a.rep) continue;
+          const __amdgpu_buffer_rsrc_t rr = rsrc(a.xt.buf[a.rep] + (int64_t)(s & 1) * a.xhalf + a.dzr_off +
+                                                 (int64_t)r2 * kDzrFloats);
+          const int off = (m * kD1 + n0 + 4 * qq) * 8;
+          nu4v v0, v1;
+          poll.start();
+          for (;;) {
+            v0 = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
+            v1 = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
+            if (v0.y == tag && v0.w == tag && v1.y == tag && v1.w == tag) break;
+            if (!poll.again()) { pok = false; break; }
+          }
+          float* d = DzX + slot * (kB * 17) + m * 17 + 4 * qq;
+          d[0] = __uint_as_float(v0.x); d[1] = __uint_as_float(v0.z);
+          d[2] = __uint_as_float(v1.x); d[3] = __uint_as_float(v1.z);
+          ++slot;
+        }
+        ok = __syncthreads_and(pok ? 1 : 0) != 0;
+        if (!ok) break;
 #pragma unroll
-      for (int ks = 0; ks < kB / 4; ks += 2) {
-        c0 = mfma_f32_16x16x4(Gl[(4 * ks + q) * kB + 16 * w + i], Dz[(4 * ks + q) * 17 + i], c0);
-        c1 = mfma_f32_16x16x4(Gl[(4 * ks + 4 + q) * kB + 16 * w + i], Dz[(4 * ks + 4 + q) * 17 + i], c1);
+        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
+          if (r2 < a.nrep) {
+            const float* Dr = r2 == a.rep ? Dz : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17);
+#pragma unroll
+            for (int ks = 0; ks < kB / 4; ks += 2) {
+              c0 = mfma_f32_16x16x4(gv[r2][ks], Dr[(4 * ks + q) * 17 + i], c0);
+              c1 = mfma_f32_16x16x4(gv[r2][ks + 1], Dr[(4 * ks + 4 + q) * 17 + i], c1);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < kB / 4; ks += 2) {
+          c0 = mfma_f32_16x16x4(Gl[(4 * ks + q) * kB + 16 * w + i], Dz[(4 * ks + q) * 17 + i], c0);
+          c1 = mfma_f32_16x16x4(Gl[(4 * ks + 4 + q) * kB + 16 * w + i], Dz[(4 * ks + 4 + q) * 17 + i], c1);
+        }
       }
       // Z1(s+1) = P(s+1) + C(s+1), one tagged granule per value: the chains
       // poll the data itself
@@ -1016,6 +1094,17 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
       for (int ms = 0; ms < kB / 4; ++ms) db += dv[ms];
       db += __shfl_xor(db, 16, 64);
       db += __shfl_xor(db, 32, 64);
+    }
+    if constexpr (XM) {  // data parallel: this wave's fragments summed over the replicas
+      float4 v[2];
+      v[0] = make_float4(g[0][0], g[0][1], g[0][2], g[0][3]);
+      v[1] = w < 3 ? make_float4(g[1][0], g[1][1], g[1][2], g[1][3]) : make_float4(db, 0.f, 0.f, 0.f);
+      const bool xok = px_sum_wave<2>(a, s, v, lb * 4 + w);
+      g[0] = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
+      if (w < 3) g[1] = f32x4{v[1].x, v[1].y, v[1].z, v[1].w};
+      else db = v[1].x;
+      ok = __syncthreads_and(xok ? 1 : 0) != 0;
+      if (!ok) break;
     }
     // every wave read this step's W1 tile in the P(s+1) forward, before the
     // barrier that followed it
@@ -1210,7 +1299,20 @@ __device__ __forceinline__ void pk_chain_rows_out(__amdgpu_buffer_rsrc_t rb, con
   }
 }
 
-template <int NL, bool DP>
+// Data-parallel Gram form: a chain's dZ1 rows also go to every peer's DZR
+// region (this replica's slot, parity by step), as system-scope granules.
+__device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, int row, int col, float v,
+                                            uint32_t tag) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const u2 wv = {__float_as_uint(v), tag};
+  const int64_t base = (int64_t)(s & 1) * a.xhalf + a.dzr_off + (int64_t)a.rep * kDzrFloats;
+  for (int d = 0; d < a.nrep; ++d) {
+    if (d == a.rep) continue;
+    __builtin_amdgcn_raw_buffer_store_b64(wv, rsrc(a.xt.buf[d] + base), (row * kD1 + col) * 8, 0, kScSys);
+  }
+}
+
+template <int NL, bool DP, bool XM = false>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c, int blk) {
   using L = ChLay<NL>;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1502,6 +1604,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? a0[tt][r] + a1[tt][r] : 0.f;
             st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
+            if constexpr (XM) pk_push_dz1(a, s, rb0 + m, n, v, tag);
           }
         }
       }
@@ -1572,6 +1675,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? acc[tt][r] : 0.f;
             st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
+            if constexpr (XM) pk_push_dz1(a, s, rb0 + m, n, v, tag);
           }
         }
       }
@@ -1920,7 +2024,7 @@ struct GTLay {
   static constexpr int TOTAL = B + 32;
 };
 
-template <int NL>
+template <int NL, bool XM>
 __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
@@ -2053,6 +2157,22 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
       float sb3 = 0.f;
       if (w == 3 && g == 0) sb3 = rowsum(DZ3T);                  // db3
       PK_STAMP(2, 2);
+      if constexpr (XM) {  // data parallel: this wave's gradients summed over the replicas
+        bool xok = true;
+        float4 v[1];
+        if (w < 2 || (w == 2 && own3)) {
+          v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
+        } else if (w == 3 && (own3 || g == 0)) {
+          v[0] = make_float4(sb, sb3, 0.f, 0.f);
+          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          sb = v[0].x;
+          sb3 = v[0].y;
+        }
+        ok = __syncthreads_and(xok ? 1 : 0) != 0;
+        if (!ok) break;
+      }
       // ---- SGD on the resident tile ----
       if (w < 2) {
 #pragma unroll
@@ -2069,6 +2189,21 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
       if (w == 0) gw = tile16(DZ2T, H1T);                         // dW2 [16 o][16 n]
       else if (w == 1 && g == 0) sb = rowsum(DZ2T);               // db2
       PK_STAMP(2, 2);
+      if constexpr (XM) {
+        bool xok = true;
+        float4 v[1];
+        if (w == 0) {
+          v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
+        } else if (w == 1 && g == 0) {
+          v[0] = make_float4(sb, 0.f, 0.f, 0.f);
+          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          sb = v[0].x;
+        }
+        ok = __syncthreads_and(xok ? 1 : 0) != 0;
+        if (!ok) break;
+      }
       if (w == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -2132,14 +2267,16 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
 // an XCD, so the chains and gradient blocks (b % 8 == 0) share one XCD and the
 // 8 layer-1 blocks of one k slice (b % 8 == gk + 1) share another, whose L2
 // then serves their common X slice once.
-template <int NL, bool DP>
+// MODE 0: single replica (Gram form); 1: data parallel, direct form (pk /
+// pk2); 2: data parallel, Gram form (pkg / pkg2).
+template <int NL, int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void mlp_persist_k(PersistArgs a) {
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int b = blockIdx.x;
   const int x = b & 7, y = b >> 3;
-  if constexpr (DP) {
+  if constexpr (MODE == 1) {
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, true>(a, lds, y, b);
       else pk_grad<NL, true>(a, lds, y - kNCH, b);
@@ -2150,12 +2287,13 @@ void mlp_persist_k(PersistArgs a) {
     // 4 chains + the gradient tiles at blockIdx 8 k (one XCD under
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
+    constexpr bool XM = MODE == 2;
     if (!pk_sr_active<NL>(b)) return;
     if (x == 0) {
-      if (y < kNCH) pk_chain<NL, false>(a, lds, y, b);
-      else pk_gtile<NL>(a, lds, y - kNCH, b);
+      if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
+      else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
     } else {
-      pk_layer1_gram<NL>(a, lds, y + kGN * (x - 1), b);
+      pk_layer1_gram<NL, XM>(a, lds, y + kGN * (x - 1), b);
     }
   }
 }
@@ -2184,12 +2322,12 @@ bool mlp_persist_supported(const MlpDesc& d) {
 
 int64_t mlp_persist_xbuf_granules() { return kTotalG; }
 
-template <int NL, bool DP>
+template <int NL, int MODE>
 static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
   const size_t lds = (size_t)lds_floats<NL>() * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    const void* f = reinterpret_cast<const void*>(mlp_persist_k<NL, DP>);
+    const void* f = reinterpret_cast<const void*>(mlp_persist_k<NL, MODE>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     // Every block waits on others: the whole grid must be co-resident.  This
@@ -2201,10 +2339,10 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return e;
-    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(DP)) return hipErrorCooperativeLaunchTooLarge;
+    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(MODE == 1)) return hipErrorCooperativeLaunchTooLarge;
     attr = true;
   }
-  hipLaunchKernelGGL((mlp_persist_k<NL, DP>), dim3(pk_grid<NL>(DP)), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(pk_grid<NL>(MODE == 1)), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -2244,16 +2382,24 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks, algo) ||
         xa->err == nullptr)
       return hipErrorInvalidValue;
+    if (algo < 0 || algo > 3) return hipErrorInvalidValue;
     a.xt = *tab;
     a.nrep = xa->nranks;
     a.rep = xa->rank;
     a.xhalf = xa->half;
     a.xerr = xa->err;
-    a.algo = algo;
+    a.algo = algo & 1;
+    a.pxslots = algo >= 2 ? kPxSlotsG : kPxSlots;
+    a.dzr_off = px_slots_half(a.nrep, algo, kPxSlotsG);
+    // Gram form: the previous launch's last Z1 carries over as in the single
+    // replica (every replica launches the same sequence, so all agree)
+    if (algo < 2) a.carry = 0;
   }
-  if (a.nrep == 1 && (gram == nullptr || ((uintptr_t)gram & 15) != 0)) return hipErrorInvalidValue;
-  if (d.nlayers == 3) return a.nrep > 1 ? pk_launch<3, true>(a, s) : pk_launch<3, false>(a, s);
-  return a.nrep > 1 ? pk_launch<2, true>(a, s) : pk_launch<2, false>(a, s);
+  const int mode = a.nrep == 1 ? 0 : (algo >= 2 ? 2 : 1);
+  if (mode != 1 && (gram == nullptr || ((uintptr_t)gram & 15) != 0)) return hipErrorInvalidValue;
+  if (d.nlayers == 3)
+    return mode == 0 ? pk_launch<3, 0>(a, s) : mode == 1 ? pk_launch<3, 1>(a, s) : pk_launch<3, 2>(a, s);
+  return mode == 0 ? pk_launch<2, 0>(a, s) : mode == 1 ? pk_launch<2, 1>(a, s) : pk_launch<2, 2>(a, s);
 }
 
 }  // namespace dsml

@@ -366,7 +366,8 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
     const int n = x->nranks();
     if (!x->connected() || n < 2 || n != world_)
       throw std::invalid_argument("set_persist: the replica exchange must connect world_size >= 2 ranks");
-    if (algo != 0 && algo != 1) throw std::invalid_argument("set_persist: algo must be 0 or 1");
+    if (algo < 0 || algo > 3)
+      throw std::invalid_argument("set_persist: algo must be 0 / 1 (pk / pk2) or 2 / 3 (pkg / pkg2)");
     if (x->ntiles() < px_ntiles(n, algo) || x->half() < px_half(n, algo))
       throw std::invalid_argument("set_persist: exchange buffers too small for the persistent step");
     xchg_ = nullptr;  // the three-launch exchanges are off while the persistent step runs
@@ -392,19 +393,26 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
 void MlpRunner::enqueue_steps(int n, hipStream_t s) {
   if (n <= 0) return;
   if (pk_xb_ != nullptr) {
+    const bool gram = pk_x_ == nullptr || pk_algo_ >= 2;
+    if (gram && pk_gram_ == nullptr)
+      throw std::invalid_argument("persistent step: set_persist_gram first (the Gram form's table)");
+    if (gram && !pk_carry_) {
+      // A launch without carried state recomputes the first step's Z1 in its
+      // prologue under the SAME hand-off tags the previous launch's last step
+      // published (partials and Z1 of step s0): clear them so no block can
+      // take a stale granule for this launch's.
+      DSML_HIP_CHECK(hipMemsetAsync(pk_xb_, 0, (size_t)mlp_persist_xbuf_granules() * sizeof(uint64_t), s));
+    }
     if (pk_x_ != nullptr)
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_,
                                        lr_ / (float)pk_x_->nranks(), n, pk_xb_, b_.stats, pk_err_,
                                        pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table(),
-                                       pk_algo_));
-    else {
-      if (pk_gram_ == nullptr)
-        throw std::invalid_argument("persistent step: set_persist_gram first (single replica)");
+                                       pk_algo_, gram ? pk_gram_ : nullptr, pk_carry_ ? 1 : 0));
+    else
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
                                        b_.stats, pk_err_, pk_herr_, pk_timeout_, s, nullptr, nullptr,
                                        0, pk_gram_, pk_carry_ ? 1 : 0));
-      pk_carry_ = true;  // the next launch, in stream order, finds this one's state
-    }
+    if (gram) pk_carry_ = true;  // the next launch, in stream order, finds this one's state
     return;
   }
   for (int i = 0; i < n; ++i) enqueue_step(s);

@@ -26,12 +26,16 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("auto", "pk", "pk2", "xact", "xgmi", "rccl", "ring", "torch")
+SYNC_MODES = ("auto", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch")
 # fused over xGMI peer memory: into K_C (xact, xgmi) or into the persistent step
 # (pk: one-shot sum of every wave's gradient slot, pk2: two-shot, i.e.
 # reduce-scatter + all-gather per slot: 2(N-1)/N slots per link instead of N-1)
-EXCHANGE_MODES = ("pk", "pk2", "xact", "xgmi")
-PERSIST_MODES = {"pk": 0, "pk2": 1}
+EXCHANGE_MODES = ("pk", "pk2", "pkg", "pkg2", "xact", "xgmi")
+# persistent-step replica exchanges -> kernel algo (kernels/mlp_persist.hip):
+# pk / pk2 the direct form with one- / two-shot gradient-slot sums; pkg / pkg2
+# the Gram form (every peer's dZ1 pushed for the layer-1 correction, the
+# gradient-slot sums off the critical path)
+PERSIST_MODES = {"pk": 0, "pk2": 1, "pkg": 2, "pkg2": 3}
 
 
 @dataclass
@@ -285,6 +289,15 @@ class MlpTrainer:
                 if not (self._want_persist and C.mlp_persist_supported(self.layout.desc_list())):
                     raise X.ExchangeUnavailable("the persistent step covers 784-128-64-10 and "
                                                 "784-128-10 at batch <= 64")
+                if PERSIST_MODES[mode] >= 2:
+                    if self._replicas_per_gpu() > 2:
+                        # the Gram grid places every replica's 4 chain + 16 tile
+                        # blocks on XCD 0 (32 CUs, one block each): three
+                        # replicas sharing a GPU cannot all be resident
+                        raise X.ExchangeUnavailable("the Gram form runs at most 2 replicas per GPU")
+                    if self.pk_gram_dp is None:
+                        self.pk_gram_dp = self._gram_table_dp()  # collective
+                    self.runner.set_persist_gram(self.pk_gram_dp)
                 half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size,
                                                              PERSIST_MODES[mode])
                 x = X.make_exchange(self.ctx, half, ntiles, self.xchg_timeout_ms)
@@ -308,7 +321,9 @@ class MlpTrainer:
         diff = X.verify_against_allreduce(self)  # collective, same result on all ranks
         self._activate(None)
         self._rewound()  # the step counter went back: stale persistent hand-off tags
-        return "" if diff <= 1e-5 else f"self-test mismatch {diff}"
+        # fp32 against fp32 torch, different summation orders (the Gram forms add
+        # the correction to a separately rounded partial): the unit tests' bound
+        return "" if diff <= 2e-5 else f"self-test mismatch {diff}"
 
     def _init_exchanges(self) -> None:
         """Set up the fused xGMI exchanges, self-test each against a
@@ -323,10 +338,12 @@ class MlpTrainer:
         * rccl — ncclAllReduce of the gradient between fwd/bwd and the update."""
         self._exchanges: Dict[str, object] = {}
         self.Xall = None
+        self.pk_gram_dp = None
         strict = self.sync in EXCHANGE_MODES
         # pk2 pays one more flag round trip per slot for fewer bytes: a
         # candidate from 3 replicas on (at 2 it moves the same bytes as pk)
-        auto = ["pk"] + (["pk2"] if self.ctx.world_size >= 3 else []) + ["xact", "xgmi"]
+        two = self.ctx.world_size >= 3
+        auto = ["pkg"] + (["pkg2"] if two else []) + ["pk"] + (["pk2"] if two else []) + ["xact", "xgmi"]
         modes = [self.sync] if strict else auto
         ok = []
         for m in modes:
@@ -448,6 +465,61 @@ class MlpTrainer:
             b1 = min(nb, b0 + step)
             prev = Xb[torch.arange(b0 - 1, b1 - 1, device=Xb.device) % nb]
             torch.bmm(prev, Xb[b0:b1].transpose(1, 2), out=G[b0:b1])
+        G += 1.0
+        return G.contiguous()
+
+    def _gather_plain(self) -> torch.Tensor:
+        """Every rank's input rows (fp32 [world][rows][d0], rank order) on this
+        GPU.  Collective."""
+        import torch.distributed as dist
+
+        from ..parallel.xchg import ExchangeUnavailable
+
+        ctx = self.ctx
+        rows = self.nbatches * self.batch
+        lo = ctx.all_reduce_scalars(float(rows), op="min")[0]
+        hi = ctx.all_reduce_scalars(float(rows), op="max")[0]
+        if lo != hi:
+            raise ExchangeUnavailable("ranks hold different numbers of batches")
+        own = self.X[:rows, : self.spec.dims[0]].contiguous()
+        if ctx.backend == "nccl":
+            out = torch.empty((ctx.world_size,) + tuple(own.shape), dtype=own.dtype, device=self.device)
+            dist.all_gather_into_tensor(out, own)
+            return out
+        parts = [torch.empty(own.shape, dtype=own.dtype) for _ in range(ctx.world_size)]
+        dist.all_gather(parts, own.cpu())
+        return torch.stack(parts).to(self.device)
+
+    def _replicas_per_gpu(self) -> int:
+        """How many ranks share this rank's GPU (1 on a node, one process per
+        GPU; more in a one-GPU rehearsal).  Collective; the max over ranks."""
+        if getattr(self, "_rpg", None) is None:
+            import torch.distributed as dist
+
+            ids = [None] * self.ctx.world_size
+            dist.all_gather_object(ids, str(torch.cuda.get_device_properties(self.device).uuid))
+            self._rpg = max(ids.count(u) for u in ids)
+        return self._rpg
+
+    def _gram_table_dp(self) -> torch.Tensor:
+        """Cross-replica Gram blocks of the data-parallel persistent step in Gram
+        form (sync pkg / pkg2): G1T[b][r'][m'][m] = X_{r'}(b-1)[m'] . X_rank(b)[m] + 1
+        for every replica r' in rank order, b - 1 wrapping, rows past the batch
+        repeating its last row.  float[nbatches][world][64][64].  Collective."""
+        nb, B, d0, N = self.nbatches, self.batch, self.spec.dims[0], self.ctx.world_size
+        Xall = self._gather_plain().view(N, nb, B, d0)
+        if B < 64:
+            Xall = Xall[:, :, torch.clamp(torch.arange(64, device=Xall.device), max=B - 1), :]
+        me = Xall[self.ctx.rank]
+        G = torch.empty((nb, N, 64, 64), dtype=torch.float32, device=self.device)
+        step = 128
+        for b0 in range(0, nb, step):
+            b1 = min(nb, b0 + step)
+            prev_idx = torch.arange(b0 - 1, b1 - 1, device=Xall.device) % nb
+            cur_t = me[b0:b1].transpose(1, 2)
+            for r2 in range(N):
+                torch.bmm(Xall[r2][prev_idx], cur_t, out=G[b0:b1, r2])
+        del Xall
         G += 1.0
         return G.contiguous()
 

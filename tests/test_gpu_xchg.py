@@ -190,11 +190,13 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
                     ctx=ctx, seed=7, sync=sync, graph_steps=graph_steps, xchg_timeout_ms=5000.0,
                     xact_waves=xact_waves, auto_fallback="torch")
     if sync == "auto":  # every candidate self-tested and timed; any may win on a shared GPU
-        assert tr.sync_active in ("pk", "xact", "xgmi", "torch"), tr.sync_active
-        assert set(tr.sync_times) == {"pk", "xact", "xgmi", "torch"}, tr.sync_times
+        # (3 replicas on one GPU: the Gram form reports itself unavailable)
+        cands = {"pkg", "pk", "xact", "xgmi", "torch"} if world == 2 else {"pk", "pk2", "xact", "xgmi", "torch"}
+        assert tr.sync_active in cands, tr.sync_active
+        assert set(tr.sync_times) == cands, tr.sync_times
     else:
         assert tr.sync_active == sync
-    if sync in ("pk", "pk2"):  # launches split anywhere: the step counter and tags carry over
+    if sync in ("pk", "pk2", "pkg", "pkg2"):  # launches split anywhere: counter and tags carry over
         assert tr.persistent
         tr.train_steps(2)
         tr.train_steps(4)
@@ -208,7 +210,8 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
 @pytest.mark.parametrize("world,graph_steps,sync", [(2, 0, "xgmi"), (2, 3, "xgmi"), (2, 0, "xact"),
                                                     (2, 3, "xact"), (3, 3, "xact"), (3, 3, "xgmi"),
                                                     (2, 0, "pk"), (3, 0, "pk"), (2, 0, "pk2"),
-                                                    (3, 0, "pk2"), (2, 3, "auto")])
+                                                    (3, 0, "pk2"), (2, 0, "pkg"), (2, 0, "pkg2"),
+                                                    (2, 3, "auto"), (3, 3, "auto")])
 def test_two_processes_ipc(world, graph_steps, sync):
     """N processes sharing the GPU through IPC handles.  Sharing one GPU, every
     process's spinning weight-gradient launch must be resident at once: the
@@ -219,7 +222,10 @@ def test_two_processes_ipc(world, graph_steps, sync):
     node each GPU runs one process and one launch.  sync='pk' runs the
     persistent step in every process (64 workgroups each, all resident) with
     the weight gradients summed over the replicas inside the launch; 'pk2'
-    sums them two-shot (reduce-scatter + all-gather per wave slot)."""
+    sums them two-shot (reduce-scatter + all-gather per wave slot).  'pkg' /
+    'pkg2' run the persistent step in Gram form across the replicas: every
+    chain's dZ1 rows pushed to every peer for the layer-1 correction (cross-
+    replica Gram blocks), the gradient slots summed one- / two-shot."""
     with tempfile.TemporaryDirectory() as d:
         spawn_group(_ipc_worker, world, lambda port: (world, port, d, graph_steps, sync,
                                               4 if sync in ("xact", "auto") else 0))
