@@ -452,21 +452,11 @@ class MlpTrainer:
 
     def _gram_table(self) -> torch.Tensor:
         """Per-batch Gram blocks of the single-replica persistent step
-        (kernels/mlp_persist.hip, "Gram form"): G1T[b][m'][m] = X_{b-1}[m'] .
-        X_b[m] + 1, b - 1 wrapping, rows past the batch repeating its last row
-        as the kernel's X tiles do.  float[nbatches][64][64] (16 KB a batch)."""
+        (engine/gram.py gram_table: float[nbatches][64][64], 16 KB a batch)."""
+        from .gram import gram_table
+
         nb, B, d0 = self.nbatches, self.batch, self.spec.dims[0]
-        Xb = self.X[: nb * B, :d0].reshape(nb, B, d0)
-        if B < 64:
-            Xb = Xb[:, torch.clamp(torch.arange(64, device=Xb.device), max=B - 1), :]
-        G = torch.empty((nb, 64, 64), dtype=torch.float32, device=self.device)
-        step = 256  # bounded temporaries for large shards
-        for b0 in range(0, nb, step):
-            b1 = min(nb, b0 + step)
-            prev = Xb[torch.arange(b0 - 1, b1 - 1, device=Xb.device) % nb]
-            torch.bmm(prev, Xb[b0:b1].transpose(1, 2), out=G[b0:b1])
-        G += 1.0
-        return G.contiguous()
+        return gram_table(self.X[: nb * B, :d0].reshape(nb, B, d0)).contiguous()
 
     def _gather_plain(self) -> torch.Tensor:
         """Every rank's input rows (fp32 [world][rows][d0], rank order) on this
@@ -503,25 +493,12 @@ class MlpTrainer:
 
     def _gram_table_dp(self) -> torch.Tensor:
         """Cross-replica Gram blocks of the data-parallel persistent step in Gram
-        form (sync pkg / pkg2): G1T[b][r'][m'][m] = X_{r'}(b-1)[m'] . X_rank(b)[m] + 1
-        for every replica r' in rank order, b - 1 wrapping, rows past the batch
-        repeating its last row.  float[nbatches][world][64][64].  Collective."""
+        form (sync pkg / pkg2; engine/gram.py gram_table_dp:
+        float[nbatches][world][64][64]).  Collective (all-gathers the shards)."""
+        from .gram import gram_table_dp
+
         nb, B, d0, N = self.nbatches, self.batch, self.spec.dims[0], self.ctx.world_size
-        Xall = self._gather_plain().view(N, nb, B, d0)
-        if B < 64:
-            Xall = Xall[:, :, torch.clamp(torch.arange(64, device=Xall.device), max=B - 1), :]
-        me = Xall[self.ctx.rank]
-        G = torch.empty((nb, N, 64, 64), dtype=torch.float32, device=self.device)
-        step = 128
-        for b0 in range(0, nb, step):
-            b1 = min(nb, b0 + step)
-            prev_idx = torch.arange(b0 - 1, b1 - 1, device=Xall.device) % nb
-            cur_t = me[b0:b1].transpose(1, 2)
-            for r2 in range(N):
-                torch.bmm(Xall[r2][prev_idx], cur_t, out=G[b0:b1, r2])
-        del Xall
-        G += 1.0
-        return G.contiguous()
+        return gram_table_dp(self._gather_plain().view(N, nb, B, d0), self.ctx.rank)
 
     def _params_rewritten(self) -> None:
         """P changed outside the persistent launches: the partials the last
