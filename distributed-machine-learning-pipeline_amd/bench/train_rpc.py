@@ -11,9 +11,9 @@ Two client flows are timed:
   k in {1, 50, 937} it reports samples/s at the client and the per-RPC
   overhead = client wall - the device's own elapsedUs of the call.
 * ``rpc`` — the reference's per-step pipeline, made correct: Memcpy of the
-  batch and labels, RunForward, RunBackward, AllReduceRing (n = 1: trivially
-  SUCCESS, ``gpu_coordinator_server.go:289-295``), ApplyGradients: five
-  RPCs per step.
+  batch, Memcpy of the labels, RunForward, RunBackward, AllReduceRing (n = 1:
+  trivially SUCCESS, ``gpu_coordinator_server.go:289-295``), ApplyGradients:
+  six RPCs per step.
 
 Synthetic 28x28 data and random-init weights (no dataset on the box).  Prints
 one JSON line; ``--out`` also writes it to a file."""
@@ -84,7 +84,7 @@ def run(a) -> dict:
                                  "device_us_per_step": round(1e6 * d / k, 2),
                                  "rpc_overhead_us": round(1e6 * (w - d), 1)}
             out["device_flow"] = dflow
-            # the reference's per-step pipeline (five RPCs per step)
+            # the reference's per-step pipeline (six RPCs per step)
             ds = synthetic_mnist(a.batch * max(a.rpc_steps, 1), seed=1000)
             res = cl.train_rpc_mode(1, ds.X.numpy(), ds.y.numpy(), steps_per_epoch=a.rpc_steps)
             out["rpc_flow"] = {"steps": a.rpc_steps, "rpcs_per_step": 6,

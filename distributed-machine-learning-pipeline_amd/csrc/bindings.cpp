@@ -818,7 +818,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                     "gram: contiguous float[nbatches][64][64]");
         TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr<float>()) & 15) == 0, "gram: 16-B aligned");
         s.keep.push_back(g);
-        s.r->set_persist_gram(g.data_ptr<float>());
+        s.r->set_persist_gram(g.data_ptr<float>(), g.numel());
       }, py::arg("gram"),
            "single-replica persistent step: the per-batch Gram table G1T[b][m'][m] = "
            "X_{b-1}[m'] . X_b[m] + 1 (trainer._gram_table)")

@@ -396,6 +396,15 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
     const bool gram = pk_x_ == nullptr || pk_algo_ >= 2;
     if (gram && pk_gram_ == nullptr)
       throw std::invalid_argument("persistent step: set_persist_gram first (the Gram form's table)");
+    if (gram) {
+      // the data-parallel Gram forms read [nbatches][nrep][64][64]
+      const int64_t reps = pk_x_ != nullptr ? pk_x_->nranks() : 1;
+      if (pk_gram_numel_ < (int64_t)d_.nbatches * reps * 64 * 64)
+        throw std::invalid_argument("persistent step: the Gram table is smaller than nbatches x "
+                                    "replicas x 64 x 64 (a table built for another world size?)");
+    }
+    // a launch that gave up left a half-written pipeline: never carry it over
+    if (persist_failed()) pk_carry_ = false;
     if (gram && !pk_carry_) {
       // A launch without carried state recomputes the first step's Z1 in its
       // prologue under the SAME hand-off tags the previous launch's last step

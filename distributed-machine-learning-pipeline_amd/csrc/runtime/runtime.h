@@ -290,7 +290,13 @@ class MlpRunner {
   // the previous launch's pipeline state -- set by every single-replica
   // launch, cleared by set_persist / clear_persist_error and by the owner
   // whenever it rewrites the parameters or the buffer.
-  void set_persist_gram(const float* g) { pk_gram_ = g; pk_carry_ = false; }
+  // `numel` floats: enqueue_steps checks it against nbatches * 4096 (times the
+  // replica count in the data-parallel Gram forms, which read [b][N][64][64]).
+  void set_persist_gram(const float* g, int64_t numel) {
+    pk_gram_ = g;
+    pk_gram_numel_ = numel;
+    pk_carry_ = false;
+  }
   void set_persist_carry(bool c) { pk_carry_ = c; }
   bool persist_carry() const { return pk_carry_; }
   // Whether a persistent launch gave up on a hand-off (read from host-mapped
@@ -342,6 +348,7 @@ class MlpRunner {
   uint32_t* pk_herr_ = nullptr;  // hipHostMalloc'd, device-visible
   uint64_t pk_timeout_ = 0;
   const float* pk_gram_ = nullptr;
+  int64_t pk_gram_numel_ = 0;
   bool pk_carry_ = false;
   int algo_ = 0;
   int world_ = 1;

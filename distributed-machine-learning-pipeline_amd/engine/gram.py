@@ -39,17 +39,24 @@ def _pad_rows(Xb: torch.Tensor) -> torch.Tensor:
     return Xb.index_select(Xb.dim() - 2, idx)
 
 
+def _bmm64(A: torch.Tensor, Bt: torch.Tensor) -> torch.Tensor:
+    """A . Bt accumulated in float64, rounded once to fp32 (+ 1 added first):
+    the table never depends on the process's matmul precision flags (a TF32 /
+    xf32 GEMM would move the correction off the fp32 reference)."""
+    return (torch.bmm(A.double(), Bt.double()) + 1.0).float()
+
+
 def gram_table(Xb: torch.Tensor, step: int = 256, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Single replica: Xb [nb][B][d0] (the shard's batches in step order) ->
-    T [nb][64][64], T[b][m'][m] = X(b-1)[m'] . X(b)[m] + 1 (fp32)."""
+    T [nb][64][64], T[b][m'][m] = X(b-1)[m'] . X(b)[m] + 1 (fp32 of a float64
+    product)."""
     Xp = _pad_rows(Xb.float())
     nb = Xp.shape[0]
     T = out if out is not None else torch.empty((nb, ROWS, ROWS), dtype=torch.float32, device=Xb.device)
     for b0 in range(0, nb, step):  # bounded temporaries for large shards
         b1 = min(nb, b0 + step)
         prev = Xp[torch.arange(b0 - 1, b1 - 1, device=Xp.device) % nb]
-        torch.bmm(prev, Xp[b0:b1].transpose(1, 2), out=T[b0:b1])
-    T += 1.0
+        T[b0:b1] = _bmm64(prev, Xp[b0:b1].transpose(1, 2))
     return T
 
 
@@ -65,8 +72,7 @@ def gram_table_dp(Xall: torch.Tensor, rank: int, step: int = 128) -> torch.Tenso
         prev_idx = torch.arange(b0 - 1, b1 - 1, device=Xp.device) % nb
         cur_t = me[b0:b1].transpose(1, 2)
         for r2 in range(N):
-            T[b0:b1, r2] = torch.bmm(Xp[r2][prev_idx], cur_t)
-    T += 1.0
+            T[b0:b1, r2] = _bmm64(Xp[r2][prev_idx], cur_t)
     return T.contiguous()
 
 

@@ -582,6 +582,7 @@ class MlpTrainer:
 
                     check(self.xchg)
                 if self.pk_buf is not None and self.runner.persist_failed():
+                    self.runner.set_persist_carry(False)  # the launch left a half-written pipeline
                     raise RuntimeError("persistent step: an on-chip hand-off timed out "
                                        "(launch ended early; parameters are not valid)")
             elif self.device.type == "cuda":
@@ -729,9 +730,22 @@ class MlpTrainer:
               "lr": self.lr, "batch": self.batch}
         if self._carries_state():
             # the single-replica persistent step's pipeline state (the next step's
-            # partials and correction), so a resume is bit-identical to running on
+            # partials and correction), so a resume is bit-identical to running on;
+            # valid only for the same batching of the same data (persist_meta)
             sd["persist_carry"] = self.pk_buf.detach().cpu().clone()
+            sd["persist_meta"] = self._carry_meta()
         return sd
+
+    def _carry_meta(self) -> Dict[str, object]:
+        """What the carried pipeline state was computed from: the batching and a
+        fingerprint of the Gram table (first and last batch blocks)."""
+        import hashlib
+
+        h = hashlib.sha256()
+        if getattr(self, "pk_gram", None) is not None:
+            h.update(self.pk_gram[0].detach().cpu().numpy().tobytes())
+            h.update(self.pk_gram[-1].detach().cpu().numpy().tobytes())
+        return {"batch": self.batch, "nbatches": self.nbatches, "gram_sha": h.hexdigest()[:32]}
 
     def _carries_state(self) -> bool:
         return (self.pk_buf is not None and not self.ctx.is_distributed and self.runner is not None
@@ -750,7 +764,10 @@ class MlpTrainer:
             self.ctr.fill_(self.steps_done)
             self._rewound()
             carry = sd.get("persist_carry")
-            if (carry is not None and self.pk_buf is not None and not self.ctx.is_distributed
+            # a carry computed for another batching or data would feed a stale Z1
+            # into the first resumed step: dropped, the prologue then recomputes it
+            same = sd.get("persist_meta") == (self._carry_meta() if self.pk_buf is not None else None)
+            if (carry is not None and same and self.pk_buf is not None and not self.ctx.is_distributed
                     and self.runner.persist_active() and carry.numel() == self.pk_buf.numel()):
                 self.pk_buf.copy_(carry.to(self.device))
                 self.runner.set_persist_carry(True)

@@ -6,6 +6,14 @@ flat fp32 parameter buffer (plus momentum) and the step counter — everything a
 replica needs, since all DP replicas hold identical state.  Rank 0 writes;
 every rank reads.
 
+Optional keys of a single-replica persistent-step trainer
+(engine/trainer.py state_dict): ``persist_carry``, the hand-off buffer with
+the next step's layer-1 partials and correction (int64[kTotalG], about 0.95 MB,
+twice the 437 KB of parameters), so a resume is bit-identical to an
+uninterrupted run; and ``persist_meta`` (batch, nbatches, a Gram-table
+fingerprint): a carry whose meta does not match the resuming trainer is
+dropped and the first resumed step's Z1 is recomputed instead.
+
 Format: a ``torch.save`` dict of tensors and plain scalars, written atomically
 (temporary file + ``os.replace``) as ``<dir>/ckpt_<step>.pt``, and loaded
 with ``torch.load(weights_only=True)`` so nothing in the file is executed.

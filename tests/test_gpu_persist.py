@@ -93,6 +93,30 @@ def test_persistent_resume_rewinds_tags(tmp_path):
     assert torch.equal(a.P, b.P)
 
 
+def test_persistent_resume_into_other_batching_drops_the_carry():
+    """A checkpoint's carried pipeline state (next step's Z1 partials) belongs to
+    its batch size and data: resuming into a trainer with another batch size
+    must recompute the first step instead of feeding the stale Z1."""
+    ds = synthetic_mnist(64 * 4, seed=17)
+    a = _tr(ds, True, batch=64)
+    a.train_steps(5)
+    sd = a.state_dict()
+    assert "persist_carry" in sd and sd["persist_meta"]["batch"] == 64
+    b = _tr(ds, True, batch=32)
+    sd = dict(sd, steps_done=0)  # same params, step 0 of the 32-row batching
+    b.load_state_dict(sd)
+    assert not b.runner.persist_carry()
+    b.train_steps(3)
+    b.synchronize()
+    # reference: plain SGD on 32-row batches from the checkpoint's params
+    lay = MlpLayout(SPEC, 32, len(ds) // 32)
+    P = sd["params"].clone()
+    for s in range(3):
+        g, _, _ = grads_ref(lay, P, ds.X[s * 32:(s + 1) * 32], ds.y[s * 32:(s + 1) * 32])
+        P = P - 0.05 * g
+    assert (b.P.cpu() - P).abs().max().item() < 2e-5
+
+
 def test_persistent_long_run_converges():
     ds = synthetic_mnist(64 * 50, seed=14)
     t = _tr(ds, True, lr=0.05)
