@@ -179,8 +179,8 @@ def run(a) -> int:
         sync_us = tr.sync_times  # auto already timed every candidate
     elif n > 1 and tr.backend == "hip" and not a.no_sync_sweep:
         # every sync candidate's µs/step, measured the way training runs it
-        cands = (["pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu
-                 else ["pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "torch"])
+        cands = (["pkx", "pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "rccl", "ring"] if not a.rehearse_one_gpu
+                 else ["pkx", "pkg", "pkg2", "pk", "pk2", "xact", "xgmi", "torch"])
         sync_us = tr.time_sync_modes(cands, steps=max(100, a.graph_steps * 2))
     tr.train_steps(a.warmup)
     tr.synchronize()
@@ -239,6 +239,12 @@ def run(a) -> int:
                 "sync_candidates_us": tr.sync_times or None,
                 "graph_steps": a.graph_steps,
                 "lr": a.lr,
+                # data-only tables built once at init, outside the timed region
+                # (the Gram forms assume the reference's fixed batch order,
+                # client.go:596: no shuffle), with their build times
+                "precompute": ({"gram_table": "gram_table" in tr.precompute_ms or
+                                "gram_table_dp" in tr.precompute_ms, "ms": dict(tr.precompute_ms)}
+                               if getattr(tr, "precompute_ms", None) else None),
             },
             "world_size": n,
             "rccl_nranks": rccl_nranks,
@@ -271,8 +277,12 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--sync", default="auto",
-                    choices=["auto", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch"],
-                    help="gradient sync (N>1): pk = the one-launch persistent step with the weight "
+                    choices=["auto", "pkx", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch"],
+                    help="gradient sync (N>1): pkx = the persistent step in Gram form with an "
+                         "exchange-free layer 1 (every replica forms the global-batch dW1 from the "
+                         "peers' dZ1 rows and the all-gathered input shards; only the upper "
+                         "layers' gradient slots cross xGMI), "
+                         "pk = the one-launch persistent step with the weight "
                          "gradients summed over the replicas inside the launch (xGMI pushes of "
                          "every slot to every peer), pk2 = the same with a two-shot sum "
                          "(reduce-scatter + all-gather per slot, 2(N-1)/N slots per link), "

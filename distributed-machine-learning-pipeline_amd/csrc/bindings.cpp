@@ -701,6 +701,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
+  m.def("mlp_persist_set_probe", [](bool on) { mlp_persist_set_probe(on); },
+        "testing only: peers' dZ1 rows taken as arrived (lone-replica probe of the Gram forms)");
   m.def("mlp_persist_set_jitter", [](int ticks) { mlp_persist_set_jitter(ticks); },
         "testing only: every block of the single-replica persistent step sleeps a pseudo-random "
         "0..ticks x 64 cycles before its hand-offs (0 = off)");
@@ -823,6 +825,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "single-replica persistent step: the per-batch Gram table G1T[b][m'][m] = "
            "X_{b-1}[m'] . X_b[m] + 1 (trainer._gram_table)")
       .def("set_persist_carry", [](PyMlpRunner& s, bool c) { s.r->set_persist_carry(c); }, py::arg("carry"))
+      .def("set_persist_xall", [](PyMlpRunner& s, torch::Tensor x, int64_t stride) {
+        check_f32(x, "xsw");
+        TORCH_CHECK(x.is_contiguous() && stride > 0 && stride % 4 == 0, "xsw: contiguous, stride % 4 == 0");
+        TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr<float>()) & 15) == 0, "xsw: 16-B aligned");
+        s.keep.push_back(x);
+        s.r->set_persist_xall(x.data_ptr<float>(), stride, x.numel());
+      }, py::arg("xsw"), py::arg("stride"),
+           "exchange-free data-parallel persistent step (pkx): every replica's input shard in "
+           "MFMA fragment order (parallel/xchg.py swizzle_inputs), replica r at r * stride floats")
       .def("persist_carry", [](PyMlpRunner& s) { return s.r->persist_carry(); },
            "the hand-off buffer holds the last launch's pipeline state (next partials + correction)")
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })

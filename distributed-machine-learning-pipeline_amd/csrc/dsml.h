@@ -100,7 +100,9 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
                              hipStream_t s, const struct XchgArgs* xa = nullptr,
                              const struct XchgTab* tab = nullptr, int algo = 0,
-                             const float* gram = nullptr, int carry = 0);
+                             const float* gram = nullptr, int carry = 0,
+                             const float* xsw = nullptr, int64_t xsw_stride = 0);
+void mlp_persist_set_probe(bool on);  // testing only: lone-replica probe of the Gram forms
 // Single replica: the Gram table the persistent step reads, float[nbatches][64][64]
 // with G1T[b][m'][m] = X_{b-1}[m'] . X_b[m] + 1 (rows past the batch repeat its
 // last row; b - 1 wraps), and `carry` = 1 when the hand-off buffer still holds
@@ -108,7 +110,10 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
 // Data-parallel form (xa->nranks > 1): the receive buffers / flags each replica
 // needs (PeerExchange half >= px_half(n, algo), ntiles >= px_ntiles(n, algo));
 // lr is passed as lr / n.  algo 0: one-shot sum (sync 'pk'), 1: two-shot
-// reduce-scatter + all-gather per wave slot (sync 'pk2').
+// reduce-scatter + all-gather per wave slot (sync 'pk2'); 2 / 3: the Gram form
+// with the same sums (pkg / pkg2); 4: the Gram form with an exchange-free layer
+// 1 (pkx): `xsw` = every replica's input shard in MFMA fragment order
+// (float[n][nbatches][49][4][64][4], replica r at xsw + r * xsw_stride).
 int64_t px_half(int n, int algo = 0);
 int px_ntiles(int n, int algo = 0);
 

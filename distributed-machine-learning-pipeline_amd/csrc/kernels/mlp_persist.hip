@@ -145,10 +145,10 @@ struct L1GLay {
   static constexpr int W = X0 + 3 * kB * kKC;         // W1 tile [16][kXS]
   static constexpr int DZ = W + 16 * kXS;             // dZ1 tile [64][17]
   static constexpr int B1 = DZ + kB * 17;             // b1 slice [16]
-  static constexpr int G = B1 + 16;                   // G1^T [64 m'][64 m] (LDS-DMA image); in the
-                                                      // data-parallel form the other replicas'
-                                                      // dZ1 tiles [kMaxPeers - 1][64][17] instead
-  static constexpr int TOTAL = G + cmax_(kB * kB, (kMaxPeers - 1) * kB * 17);
+  static constexpr int G = B1 + 16;                   // data-parallel forms: the other replicas'
+                                                      // dZ1 tiles [kMaxPeers - 1][64][17]
+  static constexpr int RED = G + (kMaxPeers - 1) * kB * 17;  // correction partials [4 waves][64 lanes][4]
+  static constexpr int TOTAL = RED + 4 * 256;
 };
 static_assert(L1GLay::G % 4 == 0, "LDS-DMA image must be 16-B aligned");
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -308,6 +308,10 @@ __device__ int g_pk_stamp_on;
 // apart by microseconds -- the results must stay bit-identical
 // (tests/test_gpu_persist.py).  0 in production: one scalar load per block.
 __device__ int g_pk_jitter;
+// Testing only (tools/pk_probe.py, the lone-replica probe): peers' dZ1 rows are
+// taken as arrived whatever their tags, so ONE replica can run the N-rank Gram
+// forms with no peer (its flags preset).  0 in production.
+__device__ int g_pk_probe;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;
   uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
@@ -364,6 +368,17 @@ struct PersistArgs {
   uint32_t* xerr;  // the exchange's error word (a peer that did not arrive)
   int32_t pxslots;  // wave slots per source (kPxSlots; kPxSlotsG in the Gram form)
   int64_t dzr_off;  // Gram form: floats from a parity half's start to its dZ1 receive region
+                    // (dzr3: from the buffer's start to the 3-slot region)
+  // Exchange-free layer 1 (algo 4, sync 'pkx'): every replica's input shard in
+  // MFMA fragment order (parallel/xchg.py swizzle_inputs), replica r's
+  // [nbatches][49][4 w][64 lanes][4 j] at xsw + r * xsw_stride, so each replica
+  // forms the global-batch dW1 = sum_r dZ1_r^T X_r itself from the peers' dZ1
+  // rows it already receives for the Gram correction; those rows then rotate
+  // over 3 slots (dzr3) -- every layer-1 block reads them, and a peer can be
+  // two steps ahead of the slowest one (see pk_dzr_base).
+  const float* xsw;
+  int64_t xsw_stride;
+  int32_t dzr3;
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -381,11 +396,28 @@ constexpr int64_t kDzrFloats = (int64_t)kB * kD1 * 2;
 static int64_t px_slots_half(int n, int algo, int slots) {
   return (int64_t)(n + ((algo & 1) ? 1 : 0)) * slots * kPxSlot;
 }
+// Exchange-free form (algo 4): the gradient tiles' slots (one-shot) in both
+// parity halves, then DZR[3][src][64][128] granules after the second half.
 int64_t px_half(int n, int algo) {
+  if (algo == 4) return px_slots_half(n, 0, kPxSlotsG) + (3 * n * kDzrFloats + 1) / 2;
   if (algo >= 2) return px_slots_half(n, algo, kPxSlotsG) + n * kDzrFloats;
   return px_slots_half(n, algo, kPxSlots);
 }
-int px_ntiles(int n, int algo) { return ((algo & 1) ? 2 : 1) * n * (algo >= 2 ? kPxSlotsG : kPxSlots); }
+int px_ntiles(int n, int algo) {
+  if (algo == 4) return n * kPxSlotsG;
+  return ((algo & 1) ? 2 : 1) * n * (algo >= 2 ? kPxSlotsG : kPxSlots);
+}
+// Floats from the start of a receive buffer to source `src`'s dZ1 rows of step
+// s.  Gram form (pkg / pkg2): one region per parity half -- only the gk == 0
+// blocks read it, before they publish Z1(s+1), and a peer's dZ1(s+2) needs
+// that Z1 (through this replica's dZ1(s+1)).  Exchange-free (pkx): every
+// layer-1 block reads it for dW1, possibly after Z1(s+1) is out; a peer's
+// dZ1(s+3) needs this replica's P(s+2), which each block publishes only after
+// its dW1(s) -- so three slots never overwrite rows still being read.
+__device__ __forceinline__ int64_t pk_dzr_base(const PersistArgs& a, uint64_t s, int src) {
+  if (a.dzr3) return a.dzr_off + (int64_t)(s % 3u) * a.nrep * kDzrFloats + (int64_t)src * kDzrFloats;
+  return (int64_t)(s & 1) * a.xhalf + a.dzr_off + (int64_t)src * kDzrFloats;
+}
 
 // One wave's slot: push v into every peer, raise their flags, wait for every
 // peer's slot of step s here, then v = the rank-ordered sum over all
@@ -419,15 +451,28 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   asm volatile("" ::: "memory");
   if (!ok) return false;
   const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot;
+  // every source's slot loaded first (all in flight together), then summed in
+  // rank order
+  float4 x[kMaxPeers][NV];
+#pragma unroll
+  for (int src = 0; src < kMaxPeers; ++src) {
+    if (src < a.nrep && src != a.rep) {
+      const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) x[src][j] = px_ld4(r, (lane * 16 + 4 * j) * 4);
+    }
+  }
   float4 acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int src = 0; src < a.nrep; ++src) {
-    const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const float4 x = src == a.rep ? v[j] : px_ld4(r, (lane * 16 + 4 * j) * 4);
-      acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
+  for (int src = 0; src < kMaxPeers; ++src) {
+    if (src < a.nrep) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float4 y = src == a.rep ? v[j] : x[src][j];
+        acc[j].x += y.x; acc[j].y += y.y; acc[j].z += y.z; acc[j].w += y.w;
+      }
     }
   }
 #pragma unroll
@@ -810,13 +855,6 @@ __device__ __forceinline__ void pk_glds_x_to(const PersistArgs& a, float* xl, ui
                                      (pk_lptr)(xl + ch * 256), 16, 0, 0);
   }
 }
-// G1^T of the batch of step s -> LDS (16 KiB, 4 LDS-DMA chunks per wave).
-__device__ __forceinline__ void pk_glds_gram(const PersistArgs& a, float* gl, uint64_t s, int lane, int w) {
-  const float* src = a.gram + (int64_t)(s % (uint64_t)a.nbatches) * (kB * kB);
-#pragma unroll
-  for (int ch = w; ch < kB * kB / 256; ch += 4)
-    __builtin_amdgcn_global_load_lds((pk_gptr)(src + ch * 256 + lane * 4), (pk_lptr)(gl + ch * 256), 16, 0, 0);
-}
 // One wave's [16 rows x 16 n] of X . W1_tile^T (+ b1): lane (i, q) holds rows
 // 16 w + 4 q .. +3 of column i.
 __device__ __forceinline__ f4v pk_l1_fwd(const float* Xl, const float* Wl, const float* B1, int w, int i,
@@ -840,28 +878,25 @@ __device__ __forceinline__ f4v pk_l1_fwd(const float* Xl, const float* Wl, const
   for (int r = 0; r < 4; ++r) z[r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]) + bn;
   return z;
 }
-// ... stored (write-through) to its chain's run of partial slot `slot`, parity
-// `par`; drained by this wave.
-__device__ __forceinline__ void pk_l1_partial(__amdgpu_buffer_rsrc_t rb, const float* Xl, const float* Wl,
-                                              const float* B1, int par, int slot, int w, int i, int q) {
-  st_f4(rb, pk_part_off(par, slot, w) + i * 16 + 4 * q, pk_l1_fwd(Xl, Wl, B1, w, i, q));
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-// gk == 0 block: its own k-partial plus the 6 other k-partials of its column
-// tile (slots gn + 8 gk), summed in gk order -- the partial sum of Z1 the
-// correction completes.  false: a wait gave up.  Block-wide (barrier inside).
-__device__ __forceinline__ bool pk_l1_gather(__amdgpu_buffer_rsrc_t rb, f4v& z, int par, int gn, uint32_t tag,
-                                             Poll& poll, int w, int i, int q) {
-  const int tid = threadIdx.x;
+// Wave c of gatherer block (gn, gk = c): its own k-partial z of chain c's rows
+// plus the 6 other k-partials of its column tile (slots gn + 8 gk'), summed in
+// gk' order -- the partial sum of Z1 the correction completes.  Wave-local (the
+// flags are polled by lanes 0-6 and agreed by a ballot); false: a wait gave up.
+__device__ __forceinline__ bool pk_l1_gather_rows(__amdgpu_buffer_rsrc_t rb, f4v& z, int par, int gn, int c,
+                                                  uint32_t tag, Poll& poll, int lane, int i, int q) {
   bool ok = true;
-  if (tid >= 1 && tid < kGK) ok = wait_flag(rb, pk_pf(par, gn + kGN * tid), tag, poll);
-  ok = __syncthreads_and(ok ? 1 : 0) != 0;
+  if (lane < kGK && lane != c) ok = wait_flag(rb, pk_pf(par, gn + kGN * lane), tag, poll);
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  asm volatile("" ::: "memory");
   if (!ok) return false;
-  f4v v[kGK - 1];
+  f4v v[kGK];
 #pragma unroll
-  for (int gk = 1; gk < kGK; ++gk) v[gk - 1] = ld_f4(rb, pk_part_off(par, gn + kGN * gk, w) + i * 16 + 4 * q);
+  for (int g2 = 0; g2 < kGK; ++g2)
+    if (g2 != c) v[g2] = ld_f4(rb, pk_part_off(par, gn + kGN * g2, c) + i * 16 + 4 * q);
+  f4v sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int gk = 1; gk < kGK; ++gk) z += v[gk - 1];
+  for (int g2 = 0; g2 < kGK; ++g2) sum += g2 == c ? z : v[g2];
+  z = sum;
   return true;
 }
 
@@ -871,8 +906,14 @@ __device__ __forceinline__ bool pk_l1_gather(__amdgpu_buffer_rsrc_t rb, f4v& z, 
 // region (tagged granules) and the cross-replica Gram blocks from the table
 // [nbatches][N][64 m'][64 m]; the W1 update sums each wave's dW1 fragments
 // over the replicas (the pk slot exchange) -- off the critical path here.
-template <int NL, bool XM>
+// XMODE 0: single replica; 1: data parallel, Gram form with the dW1 slot
+// exchange (pkg / pkg2); 2: data parallel, exchange-free layer 1 (pkx): every
+// layer-1 block reads the peers' dZ1 rows and forms the global-batch dW1 tile
+// itself from the swizzled input shards, so no layer-1 gradient crosses xGMI.
+constexpr int kKT = kD0 / 16;  // 49 k tiles of the swizzled shards
+template <int NL, int XMODE>
 __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
+  constexpr bool XM = XMODE >= 1, XL = XMODE == 2;
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -887,6 +928,20 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
   float* Gl = lds + L1GLay::G;
   auto xbuf = [&](uint64_t s) { return lds + L1GLay::X0 + (int)(s % 3u) * (kB * kKC); };
   const int jit = g_pk_jitter;
+  const int probe = XM ? g_pk_probe : 0;
+  // pkx, wave w's k tiles of the slice (waves 0-2: w and w + 4; wave 3: tile 3)
+  const int kt0 = kKC / 16 * gk + w, kt1 = kKC / 16 * gk + (w < 3 ? w + 4 : w);
+  // B operands of replica r's dW1 pass: the swizzled shard's [4 w'][lane][4 j]
+  // fragments of the wave's k tiles (one 16-B load per w' and tile)
+  auto xl_load = [&](float4 (&B)[2][4], int r, uint64_t s) __attribute__((always_inline)) {
+    const float* xr = a.xsw + (int64_t)r * a.xsw_stride +
+                      (int64_t)(s % (uint64_t)a.nbatches) * (kKT * 1024) + lane * 4;
+#pragma unroll
+    for (int wq = 0; wq < 4; ++wq) {
+      B[0][wq] = *reinterpret_cast<const float4*>(xr + kt0 * 1024 + wq * 256);
+      B[1][wq] = *reinterpret_cast<const float4*>(xr + kt1 * 1024 + wq * 256);  // wave 3: unused copy
+    }
+  };
 
   if (lb == 0) PK_EDGE(0);
   // ---- prologue: W1 tile, b1 slice, X of the first two steps ----
@@ -913,22 +968,30 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
   pk_glds_x_to(a, xbuf(s0 + 1), s0 + 1, lane, w, k0);
   __syncthreads();  // W1 / b1 stores and both X tiles (LDS-DMA, vmcnt) landed
   if (lb == 0) PK_EDGE(1);
+  // Row-split correction: block (gn, gk < 4) gathers and publishes Z1 for
+  // chain c = gk's 16 rows of column tile gn.  Its wave c keeps its own k-partial
+  // of those rows and sums the 6 others (pk_l1_gather_rows); all 4 waves split
+  // the correction's K (wave w: rows m' = 16 w .. +15 of every replica), and
+  // wave c adds their partials.  gk >= 4 blocks only publish partials.
+  const bool gat = gk < kNCH;
+  const int c = gk;
+  float* Red = lds + L1GLay::RED;
   if (!a.carry) {
     // no state from a previous launch: step s0's Z1 directly, correction 0
     const uint32_t t0 = (uint32_t)(s0 + 1);
     const int par0 = (int)(s0 & 1);
-    if (gk != 0) {
-      pk_l1_partial(rb, xbuf(s0), Wl, B1, par0, lb, w, i, q);
-      __syncthreads();
-      if (tid == 0) st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
-    } else {
-      f4v z = pk_l1_fwd(xbuf(s0), Wl, B1, w, i, q);
-      if (!pk_l1_gather(rb, z, par0, gn, t0, poll, w, i, q)) {
+    f4v z = pk_l1_fwd(xbuf(s0), Wl, B1, w, i, q);
+    st_f4(rb, pk_part_off(par0, lb, w) + i * 16 + 4 * q, z);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
+    if (gat && w == c) {
+      if (!pk_l1_gather_rows(rb, z, par0, gn, c, t0, poll, lane, i, q)) {
         pk_report(a, false);
         return;
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) st_gran(rb, kOffCg + (int64_t)(16 * w + 4 * q + r) * kD1 + n0 + i, z[r], t0);
+      for (int r = 0; r < 4; ++r) st_gran(rb, kOffCg + (int64_t)(16 * c + 4 * q + r) * kD1 + n0 + i, z[r], t0);
     }
   }
 
@@ -942,40 +1005,37 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     const int parn = (int)((s + 1) & 1);
     pk_jit(jit, blk, s, 1);
 
-    // ---- P(s+1) = X(s+1) W1(s)^T + b1(s), before dZ1(s) exists: published
-    // by gk >= 1; the gk == 0 block keeps its own and gathers the other six ----
-    f4v zs;
-    if (gk != 0) {
-      pk_l1_partial(rb, xbuf(s + 1), Wl, B1, parn, lb, w, i, q);
-      __syncthreads();
-      if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
-    } else {
-      zs = pk_l1_fwd(xbuf(s + 1), Wl, B1, w, i, q);
-      if (!pk_l1_gather(rb, zs, parn, gn, tagn, poll, w, i, q)) { ok = false; break; }
-    }
-    PK_STAMP(0, 1);
+    // ---- P(s+1) = X(s+1) W1(s)^T + b1(s), before dZ1(s) exists: every block
+    // publishes its k-partial; wave c of a gatherer keeps its own and sums the
+    // six others of chain c's rows ----
+    f4v zs = pk_l1_fwd(xbuf(s + 1), Wl, B1, w, i, q);
+    st_f4(rb, pk_part_off(parn, lb, w) + i * 16 + 4 * q, zs);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
     // X(s+2) into the third buffer (its last reader, step s-1's backward,
-    // finished before the barrier that ended that step); the column tile's
-    // Gram block of step s+1 for the correction
+    // finished before the barrier that ended that step)
     pk_glds_x_to(a, xbuf(s + 2), s + 2, lane, w, k0);
-    // the cross-replica Gram blocks of step s+1 go straight into registers
-    // (data only: in flight during the dZ1 wait): lane (i, q) holds
-    // G[r'][m = 16 w + i][m' = 4 ks + q] for ks = 0..15
-    float gv[XM ? kMaxPeers : 1][16];
-    if constexpr (XM) {
-      if (gk == 0) {
-        const float* gb = a.gram + (int64_t)((s + 1) % (uint64_t)a.nbatches) * a.nrep * (kB * kB);
+    // the Gram fragments of step s+1 go straight into registers (data only: in
+    // flight during the waits): lane (i, q) holds G_r'[m = 16 c + i][m' =
+    // 16 w + 4 kk + q] = T[r'][m'][m] for kk = 0..3
+    float gv[XM ? kMaxPeers : 1][4];
+    if (gat) {
+      const int64_t bb = (int64_t)((s + 1) % (uint64_t)a.nbatches) * (XM ? a.nrep : 1);
 #pragma unroll
-        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
-          if (r2 < a.nrep) {
+      for (int r2 = 0; r2 < (XM ? kMaxPeers : 1); ++r2) {
+        if (r2 < (XM ? a.nrep : 1)) {
+          const float* gb = a.gram + (bb + r2) * (kB * kB) + 16 * c + i;
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) gv[r2][ks] = gb[((int64_t)r2 * kB + 4 * ks + q) * kB + 16 * w + i];
-          }
+          for (int kk = 0; kk < 4; ++kk) gv[r2][kk] = gb[(16 * w + 4 * kk + q) * kB];
         }
       }
-    } else {
-      if (gk == 0) pk_glds_gram(a, Gl, s + 1, lane, w);
     }
+    // pkx: replica 0's dW1 operands are data only -- in flight during the waits
+    float4 xB[2][4];
+    if constexpr (XL) xl_load(xB, 0, s);
+    if (gat && w == c && !pk_l1_gather_rows(rb, zs, parn, gn, c, tagn, poll, lane, i, q)) ok = false;
+    PK_STAMP(0, 1);
     pk_jit(jit, blk, s, 2);
 
     // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
@@ -1002,7 +1062,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
       while (flag_tag(rb, kOffSf + tid) != t0)
         if (!poll.again()) { ok = false; break; }
     }
-    ok = __syncthreads_and(ok ? 1 : 0) != 0;  // also retires the X / G LDS-DMA
+    ok = __syncthreads_and(ok ? 1 : 0) != 0;  // also retires the X LDS-DMA
     if (!ok) break;
     if (lb == 0 && it + 1 == a.steps && tid == 0) {
       const uint64_t e = s0 + (uint64_t)a.steps;
@@ -1011,69 +1071,128 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
     }
     PK_STAMP(0, 2);
 
-    // ---- gk == 0: C(s+1)[64 x 16] = -lr G1(s+1) dZ1(s)[:, tile]; wave w: rows
-    // 16 w .. +15 (chain w's rows), K = 64 batch rows (x N replicas) ----
-    if (gk == 0) {
-      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (XM) {
-        // every other replica's dZ1[:, tile] (pushed by its chains), in rank order
-        float* DzX = Gl;
-        const int m = tid >> 2, qq = tid & 3;
-        bool pok = true;
-        for (int r2 = 0, slot = 0; r2 < a.nrep; ++r2) {
-          if (r2 == a.rep) continue;
-          const __amdgpu_buffer_rsrc_t rr = rsrc(a.xt.buf[a.rep] + (int64_t)(s & 1) * a.xhalf + a.dzr_off +
-                                                 (int64_t)r2 * kDzrFloats);
-          const int off = (m * kD1 + n0 + 4 * qq) * 8;
-          nu4v v0, v1;
-          poll.start();
-          for (;;) {
-            v0 = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
-            v1 = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
-            if (v0.y == tag && v0.w == tag && v1.y == tag && v1.w == tag) break;
-            if (!poll.again()) { pok = false; break; }
-          }
-          float* d = DzX + slot * (kB * 17) + m * 17 + 4 * qq;
-          d[0] = __uint_as_float(v0.x); d[1] = __uint_as_float(v0.z);
-          d[2] = __uint_as_float(v1.x); d[3] = __uint_as_float(v1.z);
-          ++slot;
-        }
-        ok = __syncthreads_and(pok ? 1 : 0) != 0;
-        if (!ok) break;
+    // ---- every other replica's dZ1[:, tile] (pushed by its chains), in rank
+    // order: for the correction (gatherers) and, in pkx, every block's dW1 ----
+    float* DzX = Gl;
+    if (XM && (XL || gat)) {
+      // every peer's granules loaded together (one round of loads in flight,
+      // not one poll per peer in turn); peers not yet complete are re-read
+      const int m = tid >> 2, qq = tid & 3;
+      const int off = (m * kD1 + n0 + 4 * qq) * 8;
+      const float* rbase = a.xt.buf[a.rep];
+      uint32_t need = 0;  // peers whose rows this thread still waits for
+#pragma unroll
+      for (int r2 = 0; r2 < kMaxPeers; ++r2)
+        if (r2 < a.nrep && r2 != a.rep) need |= 1u << r2;
+      bool pok = true;
+      poll.start();
+      while (need != 0u) {
+        nu4v v0[kMaxPeers], v1[kMaxPeers];
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
-          if (r2 < a.nrep) {
-            const float* Dr = r2 == a.rep ? Dz : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17);
-#pragma unroll
-            for (int ks = 0; ks < kB / 4; ks += 2) {
-              c0 = mfma_f32_16x16x4(gv[r2][ks], Dr[(4 * ks + q) * 17 + i], c0);
-              c1 = mfma_f32_16x16x4(gv[r2][ks + 1], Dr[(4 * ks + 4 + q) * 17 + i], c1);
-            }
+          if (need & (1u << r2)) {
+            const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
+            v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
+            v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
           }
         }
-      } else {
 #pragma unroll
-        for (int ks = 0; ks < kB / 4; ks += 2) {
-          c0 = mfma_f32_16x16x4(Gl[(4 * ks + q) * kB + 16 * w + i], Dz[(4 * ks + q) * 17 + i], c0);
-          c1 = mfma_f32_16x16x4(Gl[(4 * ks + 4 + q) * kB + 16 * w + i], Dz[(4 * ks + 4 + q) * 17 + i], c1);
+        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
+          if ((need & (1u << r2)) &&
+              (probe || (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
+            float* d = DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
+            d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
+            d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
+            need &= ~(1u << r2);
+          }
+        }
+        if (need != 0u && !poll.again()) { pok = false; break; }
+      }
+      ok = __syncthreads_and(pok ? 1 : 0) != 0;
+      if (!ok) break;
+    }
+    // ---- gatherers: C(s+1)[chain c's 16 rows x 16 n] = -lr sum_r' G_r'
+    // dZ1_r'(s)[:, tile]; wave w contracts m' = 16 w .. +15 of every replica,
+    // wave c adds the four partials in a fixed order and publishes Z1 ----
+    if (gat) {
+      f32x4 cw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r2 = 0; r2 < (XM ? kMaxPeers : 1); ++r2) {
+        if (r2 < (XM ? a.nrep : 1)) {
+          const float* Dr = (!XM || r2 == a.rep) ? Dz : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) cw = mfma_f32_16x16x4(gv[r2][kk], Dr[(16 * w + 4 * kk + q) * 17 + i], cw);
         }
       }
-      // Z1(s+1) = P(s+1) + C(s+1), one tagged granule per value: the chains
-      // poll the data itself
+      *reinterpret_cast<f4v*>(Red + w * 256 + lane * 4) = f4v{cw[0], cw[1], cw[2], cw[3]};
+      __syncthreads();
+      if (w == c) {
+        const f4v c0 = *reinterpret_cast<const f4v*>(Red + lane * 4);
+        const f4v c1 = *reinterpret_cast<const f4v*>(Red + 256 + lane * 4);
+        const f4v c2 = *reinterpret_cast<const f4v*>(Red + 512 + lane * 4);
+        const f4v c3 = *reinterpret_cast<const f4v*>(Red + 768 + lane * 4);
+        // Z1(s+1) = P(s+1) + C(s+1), one tagged granule per value: the chains
+        // poll the data itself
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        st_gran(rb, kOffCg + (int64_t)(16 * w + 4 * q + r) * kD1 + n0 + i, zs[r] + -a.lr * (c0[r] + c1[r]),
-                tagn);
+        for (int r = 0; r < 4; ++r)
+          st_gran(rb, kOffCg + (int64_t)(16 * c + 4 * q + r) * kD1 + n0 + i,
+                  zs[r] + -a.lr * ((c0[r] + c1[r]) + (c2[r] + c3[r])), tagn);
+      }
       PK_STAMP(0, 4);
     }
 
     // ---- backward: dW1 tile [16 n][112 k] = dZ1^T . X(s), SGD in LDS ----
+    f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float db = 0.f;
+    if constexpr (XL) {
+      // global batch: sum over the replicas in rank order, every operand from
+      // the swizzled shards (the SAME instruction sequence on every replica:
+      // identical W1 bits); row m = 4 w' + 16 j + q of MFMA (w', j)
+      // two named operand sets in ping-pong: replica r + 1's loads fly during
+      // replica r's MFMAs (no dynamically indexed register array)
+      auto pass = [&](const float4 (&cB)[2][4], int r) __attribute__((always_inline)) {
+        const float* Dr = r == a.rep ? Dz : DzX + (r < a.rep ? r : r - 1) * (kB * 17);
+#pragma unroll
+        for (int wq = 0; wq < 4; ++wq) {
+          const float d0 = Dr[(4 * wq + q) * 17 + i], d1 = Dr[(4 * wq + 16 + q) * 17 + i];
+          const float d2 = Dr[(4 * wq + 32 + q) * 17 + i], d3 = Dr[(4 * wq + 48 + q) * 17 + i];
+          if (w < 3) {
+            g[0] = mfma_f32_16x16x4(d0, cB[0][wq].x, g[0]);
+            g[1] = mfma_f32_16x16x4(d0, cB[1][wq].x, g[1]);
+            g[0] = mfma_f32_16x16x4(d1, cB[0][wq].y, g[0]);
+            g[1] = mfma_f32_16x16x4(d1, cB[1][wq].y, g[1]);
+            g[0] = mfma_f32_16x16x4(d2, cB[0][wq].z, g[0]);
+            g[1] = mfma_f32_16x16x4(d2, cB[1][wq].z, g[1]);
+            g[0] = mfma_f32_16x16x4(d3, cB[0][wq].w, g[0]);
+            g[1] = mfma_f32_16x16x4(d3, cB[1][wq].w, g[1]);
+          } else {  // one tile, two chains over the row phases
+            g[0] = mfma_f32_16x16x4(d0, cB[0][wq].x, g[0]);
+            g[1] = mfma_f32_16x16x4(d1, cB[0][wq].y, g[1]);
+            g[0] = mfma_f32_16x16x4(d2, cB[0][wq].z, g[0]);
+            g[1] = mfma_f32_16x16x4(d3, cB[0][wq].w, g[1]);
+            db += (d0 + d1) + (d2 + d3);
+          }
+        }
+      };
+      float4 xC[2][4];
+      for (int r = 0; r < a.nrep; r += 2) {
+        if (r + 1 < a.nrep) xl_load(xC, r + 1, s);
+        pass(xB, r);
+        if (r + 1 < a.nrep) {
+          if (r + 2 < a.nrep) xl_load(xB, r + 2, s);
+          pass(xC, r + 1);
+        }
+      }
+      if (w == 3) {
+        g[0] = g[0] + g[1];
+        db += __shfl_xor(db, 16, 64);
+        db += __shfl_xor(db, 32, 64);
+      }
+    } else {
     const float* Xl = xbuf(s);
     float dv[kB / 4];
 #pragma unroll
     for (int ms = 0; ms < kB / 4; ++ms) dv[ms] = Dz[(4 * ms + q) * 17 + i];
-    f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    float db = 0.f;
     if (w < 3) {
       const float* xb0 = Xl + q * kKC + 16 * w + i;
       const float* xb1 = xb0 + 64;
@@ -1095,7 +1214,8 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
       db += __shfl_xor(db, 16, 64);
       db += __shfl_xor(db, 32, 64);
     }
-    if constexpr (XM) {  // data parallel: this wave's fragments summed over the replicas
+    }
+    if constexpr (XMODE == 1) {  // data parallel: this wave's fragments summed over the replicas
       float4 v[2];
       v[0] = make_float4(g[0][0], g[0][1], g[0][2], g[0][3]);
       v[1] = w < 3 ? make_float4(g[1][0], g[1][1], g[1][2], g[1][3]) : make_float4(db, 0.f, 0.f, 0.f);
@@ -1301,14 +1421,24 @@ __device__ __forceinline__ void pk_chain_rows_out(__amdgpu_buffer_rsrc_t rb, con
 
 // Data-parallel Gram form: a chain's dZ1 rows also go to every peer's DZR
 // region (this replica's slot, parity by step), as system-scope granules.
-__device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, int row, int col, float v,
-                                            uint32_t tag) {
+// The lane's 8 values (rows row0 + r, r = 0..3, of columns col0 and col1), one
+// buffer descriptor per peer (built once, not once per value), every peer's
+// stores issued back to back.
+__device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, int row0, int col0, int col1,
+                                            const float (&v)[2][4], uint32_t tag) {
   typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  const u2 wv = {__float_as_uint(v), tag};
-  const int64_t base = (int64_t)(s & 1) * a.xhalf + a.dzr_off + (int64_t)a.rep * kDzrFloats;
-  for (int d = 0; d < a.nrep; ++d) {
-    if (d == a.rep) continue;
-    __builtin_amdgcn_raw_buffer_store_b64(wv, rsrc(a.xt.buf[d] + base), (row * kD1 + col) * 8, 0, kScSys);
+  const int64_t base = pk_dzr_base(a, s, a.rep);
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= a.nrep || d == a.rep) continue;
+    const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[d] + base);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u2 wv = {__float_as_uint(v[tt][k]), tag};
+        __builtin_amdgcn_raw_buffer_store_b64(wv, r, ((row0 + k) * kD1 + (tt ? col1 : col0)) * 8, 0, kScSys);
+      }
   }
 }
 
@@ -1596,6 +1726,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
             a1[tt] = mfma_f32_16x16x4(d1, W2[(4 * ks + 4 + q) * kS1 + n], a1[tt]);
           }
         }
+        float dzv[2][4];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           const int n = 16 * (w + 4 * tt) + i;
@@ -1603,10 +1734,11 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           for (int r = 0; r < 4; ++r) {
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? a0[tt][r] + a1[tt][r] : 0.f;
+            dzv[tt][r] = v;
             st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
-            if constexpr (XM) pk_push_dz1(a, s, rb0 + m, n, v, tag);
           }
         }
+        if constexpr (XM) pk_push_dz1(a, s, rb0 + 4 * q, 16 * w + i, 16 * (w + 4) + i, dzv, tag);
       }
     } else {
       // ---- logits = H1 W2^T + b2: K = 128 split over the 4 waves ----
@@ -1667,6 +1799,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           for (int tt = 0; tt < 2; ++tt)
             acc[tt] = mfma_f32_16x16x4(d, W2[(4 * ks + q) * kS1 + 16 * (w + 4 * tt) + i], acc[tt]);
         }
+        float dzv[2][4];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           const int n = 16 * (w + 4 * tt) + i;
@@ -1674,10 +1807,11 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
           for (int r = 0; r < 4; ++r) {
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? acc[tt][r] : 0.f;
+            dzv[tt][r] = v;
             st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
-            if constexpr (XM) pk_push_dz1(a, s, rb0 + m, n, v, tag);
           }
         }
+        if constexpr (XM) pk_push_dz1(a, s, rb0 + 4 * q, 16 * w + i, 16 * (w + 4) + i, dzv, tag);
       }
     }
     PK_STAMP(1, 4);
@@ -2268,7 +2402,8 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
 // 8 layer-1 blocks of one k slice (b % 8 == gk + 1) share another, whose L2
 // then serves their common X slice once.
 // MODE 0: single replica (Gram form); 1: data parallel, direct form (pk /
-// pk2); 2: data parallel, Gram form (pkg / pkg2).
+// pk2); 2: data parallel, Gram form (pkg / pkg2); 3: data parallel,
+// exchange-free layer 1 (pkx).
 template <int NL, int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void mlp_persist_k(PersistArgs a) {
@@ -2287,13 +2422,13 @@ void mlp_persist_k(PersistArgs a) {
     // 4 chains + the gradient tiles at blockIdx 8 k (one XCD under
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
-    constexpr bool XM = MODE == 2;
+    constexpr bool XM = MODE >= 2;
     if (!pk_sr_active<NL>(b)) return;
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
       else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
     } else {
-      pk_layer1_gram<NL, XM>(a, lds, y + kGN * (x - 1), b);
+      pk_layer1_gram<NL, MODE == 3 ? 2 : MODE == 2 ? 1 : 0>(a, lds, y + kGN * (x - 1), b);
     }
   }
 }
@@ -2304,6 +2439,11 @@ hipError_t mlp_persist_read_stamps(uint64_t* host_out) {
 }
 void mlp_persist_set_jitter(int ticks) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_jitter), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
+}
+void mlp_persist_set_probe(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_probe), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
 void mlp_persist_set_stamping(bool on) {
@@ -2350,7 +2490,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
                              hipStream_t s, const XchgArgs* xa, const XchgTab* tab, int algo,
-                             const float* gram, int carry) {
+                             const float* gram, int carry, const float* xsw, int64_t xsw_stride) {
   if (!mlp_persist_supported(d) || steps < 1 || xb == nullptr || err == nullptr || ctr == nullptr ||
       (ldx % 4) != 0 || ldx < kD0 || (((uintptr_t)X) & 15) != 0)
     return hipErrorInvalidValue;
@@ -2382,24 +2522,39 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     if (tab == nullptr || xa->nranks > kMaxPeers || xa->half < px_half(xa->nranks, algo) ||
         xa->err == nullptr)
       return hipErrorInvalidValue;
-    if (algo < 0 || algo > 3) return hipErrorInvalidValue;
+    if (algo < 0 || algo > 4) return hipErrorInvalidValue;
+    if (algo == 4 && (xsw == nullptr || ((uintptr_t)xsw & 15) != 0 ||
+                      xsw_stride < (int64_t)d.nbatches * kKT * 1024 || (xsw_stride % 4) != 0))
+      return hipErrorInvalidValue;
     a.xt = *tab;
     a.nrep = xa->nranks;
     a.rep = xa->rank;
     a.xhalf = xa->half;
     a.xerr = xa->err;
-    a.algo = algo & 1;
+    a.algo = algo == 4 ? 0 : (algo & 1);
     a.pxslots = algo >= 2 ? kPxSlotsG : kPxSlots;
     a.dzr_off = px_slots_half(a.nrep, algo, kPxSlotsG);
+    if (algo == 4) {
+      // the slot regions' parity halves are back to back ([2][slots_half], the
+      // parity offset is slots_half, not the buffer's half), then the 3
+      // rotating dZ1 slots: no slot region overlaps them
+      a.dzr3 = 1;
+      a.xhalf = px_slots_half(a.nrep, 0, kPxSlotsG);
+      a.dzr_off = 2 * a.xhalf;
+      a.xsw = xsw;
+      a.xsw_stride = xsw_stride;
+    }
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)
     if (algo < 2) a.carry = 0;
   }
-  const int mode = a.nrep == 1 ? 0 : (algo >= 2 ? 2 : 1);
+  const int mode = a.nrep == 1 ? 0 : (algo == 4 ? 3 : algo >= 2 ? 2 : 1);
   if (mode != 1 && (gram == nullptr || ((uintptr_t)gram & 15) != 0)) return hipErrorInvalidValue;
   if (d.nlayers == 3)
-    return mode == 0 ? pk_launch<3, 0>(a, s) : mode == 1 ? pk_launch<3, 1>(a, s) : pk_launch<3, 2>(a, s);
-  return mode == 0 ? pk_launch<2, 0>(a, s) : mode == 1 ? pk_launch<2, 1>(a, s) : pk_launch<2, 2>(a, s);
+    return mode == 0 ? pk_launch<3, 0>(a, s) : mode == 1 ? pk_launch<3, 1>(a, s)
+         : mode == 2 ? pk_launch<3, 2>(a, s) : pk_launch<3, 3>(a, s);
+  return mode == 0 ? pk_launch<2, 0>(a, s) : mode == 1 ? pk_launch<2, 1>(a, s)
+       : mode == 2 ? pk_launch<2, 2>(a, s) : pk_launch<2, 3>(a, s);
 }
 
 }  // namespace dsml

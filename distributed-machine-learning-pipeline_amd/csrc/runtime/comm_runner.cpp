@@ -366,8 +366,9 @@ void MlpRunner::set_persist(uint64_t* xbuf, uint32_t* err, double timeout_ms, Pe
     const int n = x->nranks();
     if (!x->connected() || n < 2 || n != world_)
       throw std::invalid_argument("set_persist: the replica exchange must connect world_size >= 2 ranks");
-    if (algo < 0 || algo > 3)
-      throw std::invalid_argument("set_persist: algo must be 0 / 1 (pk / pk2) or 2 / 3 (pkg / pkg2)");
+    if (algo < 0 || algo > 4)
+      throw std::invalid_argument("set_persist: algo must be 0 / 1 (pk / pk2), 2 / 3 (pkg / pkg2) "
+                                  "or 4 (pkx)");
     if (x->ntiles() < px_ntiles(n, algo) || x->half() < px_half(n, algo))
       throw std::invalid_argument("set_persist: exchange buffers too small for the persistent step");
     xchg_ = nullptr;  // the three-launch exchanges are off while the persistent step runs
@@ -405,6 +406,13 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
     }
     // a launch that gave up left a half-written pipeline: never carry it over
     if (persist_failed()) pk_carry_ = false;
+    if (pk_x_ != nullptr && pk_algo_ == 4) {
+      const int64_t per = (int64_t)d_.nbatches * (d_.dims[0] / 16) * 1024;
+      if (pk_xsw_ == nullptr || pk_xsw_stride_ < per ||
+          pk_xsw_numel_ < (int64_t)(pk_x_->nranks() - 1) * pk_xsw_stride_ + per)
+        throw std::invalid_argument("persistent step (pkx): set_persist_xall with every replica's "
+                                    "swizzled shard first");
+    }
     if (gram && !pk_carry_) {
       // A launch without carried state recomputes the first step's Z1 in its
       // prologue under the SAME hand-off tags the previous launch's last step
@@ -416,7 +424,8 @@ void MlpRunner::enqueue_steps(int n, hipStream_t s) {
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_,
                                        lr_ / (float)pk_x_->nranks(), n, pk_xb_, b_.stats, pk_err_,
                                        pk_herr_, pk_timeout_, s, &pk_x_->args(), &pk_x_->table(),
-                                       pk_algo_, gram ? pk_gram_ : nullptr, pk_carry_ ? 1 : 0));
+                                       pk_algo_, gram ? pk_gram_ : nullptr, pk_carry_ ? 1 : 0,
+                                       pk_xsw_, pk_xsw_stride_));
     else
       DSML_HIP_CHECK(mlp_persist_steps(b_.X, b_.ldx, b_.labels, b_.P, b_.ctr, d_, lr_, n, pk_xb_,
                                        b_.stats, pk_err_, pk_herr_, pk_timeout_, s, nullptr, nullptr,

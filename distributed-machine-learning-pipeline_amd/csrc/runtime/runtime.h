@@ -298,6 +298,14 @@ class MlpRunner {
     pk_carry_ = false;
   }
   void set_persist_carry(bool c) { pk_carry_ = c; }
+  // Exchange-free data-parallel form (algo 4): every replica's input shard in
+  // MFMA fragment order, replica r at xsw + r * stride floats (numel checked
+  // against the replica count at enqueue).
+  void set_persist_xall(const float* xsw, int64_t stride, int64_t numel) {
+    pk_xsw_ = xsw;
+    pk_xsw_stride_ = stride;
+    pk_xsw_numel_ = numel;
+  }
   bool persist_carry() const { return pk_carry_; }
   // Whether a persistent launch gave up on a hand-off (read from host-mapped
   // memory the kernel marks on the way out: valid after a stream sync, no copy).
@@ -349,6 +357,8 @@ class MlpRunner {
   uint64_t pk_timeout_ = 0;
   const float* pk_gram_ = nullptr;
   int64_t pk_gram_numel_ = 0;
+  const float* pk_xsw_ = nullptr;
+  int64_t pk_xsw_stride_ = 0, pk_xsw_numel_ = 0;
   bool pk_carry_ = false;
   int algo_ = 0;
   int world_ = 1;

@@ -26,16 +26,21 @@ from ..parallel.dist import DistContext, make_native_comm
 
 log = logging.getLogger("hipdsml.trainer")
 
-SYNC_MODES = ("auto", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch")
+SYNC_MODES = ("auto", "pkx", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi", "rccl", "ring", "torch")
 # fused over xGMI peer memory: into K_C (xact, xgmi) or into the persistent step
 # (pk: one-shot sum of every wave's gradient slot, pk2: two-shot, i.e.
 # reduce-scatter + all-gather per slot: 2(N-1)/N slots per link instead of N-1)
-EXCHANGE_MODES = ("pk", "pk2", "pkg", "pkg2", "xact", "xgmi")
+EXCHANGE_MODES = ("pkx", "pk", "pk2", "pkg", "pkg2", "xact", "xgmi")
 # persistent-step replica exchanges -> kernel algo (kernels/mlp_persist.hip):
 # pk / pk2 the direct form with one- / two-shot gradient-slot sums; pkg / pkg2
 # the Gram form (every peer's dZ1 pushed for the layer-1 correction, the
-# gradient-slot sums off the critical path)
-PERSIST_MODES = {"pk": 0, "pk2": 1, "pkg": 2, "pkg2": 3}
+# gradient-slot sums off the critical path); pkx the Gram form with an
+# exchange-free layer 1 (every replica forms the global-batch dW1 from the
+# peers' dZ1 rows it already receives and the all-gathered input shards: no
+# layer-1 gradient crosses xGMI, only the upper layers' 16 tile slots)
+PERSIST_MODES = {"pk": 0, "pk2": 1, "pkg": 2, "pkg2": 3, "pkx": 4}
+# the modes that read the all-gathered, swizzled input shards (self.Xall)
+XALL_MODES = ("xact", "pkx")
 
 
 @dataclass
@@ -131,6 +136,8 @@ class MlpTrainer:
         self.auto_fallback = auto_fallback
         self.sync_active = "none"
         self.sync_times: Dict[str, float] = {}
+        # data-only tables built at init, outside any timed region: name -> ms
+        self.precompute_ms: Dict[str, float] = {}
         self.Xall: Optional[torch.Tensor] = None
         self._exchanges: Dict[str, object] = {}
         self.runner = None
@@ -184,7 +191,10 @@ class MlpTrainer:
             if self._want_persist and plain and C.mlp_persist_supported(self.layout.desc_list()):
                 self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64, device=d)
                 self.pk_err = torch.zeros(1, dtype=torch.int32, device=d)
+                t0 = time.perf_counter()
                 self.pk_gram = self._gram_table()
+                torch.cuda.synchronize(d)
+                self.precompute_ms["gram_table"] = round(1e3 * (time.perf_counter() - t0), 2)
                 self.runner.set_persist_gram(self.pk_gram)
                 self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0)
                 self.sync_active = "none"
@@ -226,28 +236,13 @@ class MlpTrainer:
         """Every rank's input shard, replicated on this GPU in MFMA fragment
         order (parallel/xchg.py swizzle_inputs) — the activation exchange reads
         every rank's batch rows locally.  Collective."""
-        import torch.distributed as dist
-
-        from ..parallel.xchg import ExchangeUnavailable
-
-        ctx = self.ctx
-        rows = self.nbatches * self.batch
-        lo = ctx.all_reduce_scalars(float(rows), op="min")[0]
-        hi = ctx.all_reduce_scalars(float(rows), op="max")[0]
-        if lo != hi:
-            raise ExchangeUnavailable("ranks hold different numbers of batches")
-        own = self.X[:rows, : self.spec.dims[0]].contiguous()
-        if ctx.backend == "nccl":
-            out = torch.empty((ctx.world_size,) + tuple(own.shape), dtype=own.dtype,
-                              device=self.device)
-            dist.all_gather_into_tensor(out, own)
-        else:
-            parts = [torch.empty(own.shape, dtype=own.dtype) for _ in range(ctx.world_size)]
-            dist.all_gather(parts, own.cpu())
-            out = torch.stack(parts).to(self.device)
         from ..parallel.xchg import swizzle_inputs
 
-        return swizzle_inputs(out, self.batch)
+        t0 = time.perf_counter()
+        out = swizzle_inputs(self._gather_plain(), self.batch)
+        torch.cuda.synchronize(self.device)
+        self.precompute_ms["xall_swizzled"] = round(1e3 * (time.perf_counter() - t0), 2)
+        return out
 
     def _activate(self, mode: Optional[str]) -> None:
         """Point the native runner at one gradient-sync mode.  None keeps the
@@ -298,6 +293,10 @@ class MlpTrainer:
                     if self.pk_gram_dp is None:
                         self.pk_gram_dp = self._gram_table_dp()  # collective
                     self.runner.set_persist_gram(self.pk_gram_dp)
+                if mode == "pkx":
+                    if self.Xall is None:
+                        self.Xall = self._gather_inputs()  # collective
+                    self.runner.set_persist_xall(self.Xall, self.Xall[0].numel())
                 half, ntiles = C.MlpRunner.persist_xchg_size(self.ctx.world_size,
                                                              PERSIST_MODES[mode])
                 x = X.make_exchange(self.ctx, half, ntiles, self.xchg_timeout_ms)
@@ -343,7 +342,8 @@ class MlpTrainer:
         # pk2 pays one more flag round trip per slot for fewer bytes: a
         # candidate from 3 replicas on (at 2 it moves the same bytes as pk)
         two = self.ctx.world_size >= 3
-        auto = ["pkg"] + (["pkg2"] if two else []) + ["pk"] + (["pk2"] if two else []) + ["xact", "xgmi"]
+        auto = (["pkx", "pkg"] + (["pkg2"] if two else []) + ["pk"] + (["pk2"] if two else [])
+                + ["xact", "xgmi"])
         modes = [self.sync] if strict else auto
         ok = []
         for m in modes:
@@ -364,8 +364,8 @@ class MlpTrainer:
             log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
             self.sync_times = times
         self._set_mode(choice or self.sync_active)
-        if self.sync_active != "xact":
-            self.Xall = None  # the replicated inputs are only read by xact
+        if self.sync_active not in XALL_MODES:
+            self.Xall = None  # the replicated inputs are only read by xact / pkx
 
     @staticmethod
     def runner_module():
@@ -387,7 +387,7 @@ class MlpTrainer:
         for m in modes:
             if m in EXCHANGE_MODES and m not in self._exchanges:
                 continue
-            if m == "xact" and self.Xall is None:
+            if m in XALL_MODES and self.Xall is None:
                 continue  # its replicated inputs were released when another mode won
             if m in ("rccl", "ring") and self.comm is None:
                 continue
@@ -498,7 +498,11 @@ class MlpTrainer:
         from .gram import gram_table_dp
 
         nb, B, d0, N = self.nbatches, self.batch, self.spec.dims[0], self.ctx.world_size
-        return gram_table_dp(self._gather_plain().view(N, nb, B, d0), self.ctx.rank)
+        t0 = time.perf_counter()
+        T = gram_table_dp(self._gather_plain().view(N, nb, B, d0), self.ctx.rank)
+        torch.cuda.synchronize(self.device)
+        self.precompute_ms["gram_table_dp"] = round(1e3 * (time.perf_counter() - t0), 2)
+        return T
 
     def _params_rewritten(self) -> None:
         """P changed outside the persistent launches: the partials the last

@@ -191,12 +191,13 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
                     xact_waves=xact_waves, auto_fallback="torch")
     if sync == "auto":  # every candidate self-tested and timed; any may win on a shared GPU
         # (3 replicas on one GPU: the Gram form reports itself unavailable)
-        cands = {"pkg", "pk", "xact", "xgmi", "torch"} if world == 2 else {"pk", "pk2", "xact", "xgmi", "torch"}
+        cands = ({"pkx", "pkg", "pk", "xact", "xgmi", "torch"} if world == 2
+                 else {"pk", "pk2", "xact", "xgmi", "torch"})
         assert tr.sync_active in cands, tr.sync_active
         assert set(tr.sync_times) == cands, tr.sync_times
     else:
         assert tr.sync_active == sync
-    if sync in ("pk", "pk2", "pkg", "pkg2"):  # launches split anywhere: counter and tags carry over
+    if sync in ("pk", "pk2", "pkg", "pkg2", "pkx"):  # launches split anywhere: counter and tags carry over
         assert tr.persistent
         tr.train_steps(2)
         tr.train_steps(4)
@@ -211,7 +212,7 @@ def _ipc_worker(rank, world, port, outdir, graph_steps, sync="xgmi", xact_waves=
                                                     (2, 3, "xact"), (3, 3, "xact"), (3, 3, "xgmi"),
                                                     (2, 0, "pk"), (3, 0, "pk"), (2, 0, "pk2"),
                                                     (3, 0, "pk2"), (2, 0, "pkg"), (2, 0, "pkg2"),
-                                                    (2, 3, "auto"), (3, 3, "auto")])
+                                                    (2, 0, "pkx"), (2, 3, "auto"), (3, 3, "auto")])
 def test_two_processes_ipc(world, graph_steps, sync):
     """N processes sharing the GPU through IPC handles.  Sharing one GPU, every
     process's spinning weight-gradient launch must be resident at once: the
@@ -225,7 +226,9 @@ def test_two_processes_ipc(world, graph_steps, sync):
     sums them two-shot (reduce-scatter + all-gather per wave slot).  'pkg' /
     'pkg2' run the persistent step in Gram form across the replicas: every
     chain's dZ1 rows pushed to every peer for the layer-1 correction (cross-
-    replica Gram blocks), the gradient slots summed one- / two-shot."""
+    replica Gram blocks), the gradient slots summed one- / two-shot.  'pkx'
+    is the Gram form with an exchange-free layer 1: every replica forms the
+    global-batch dW1 from the peers' dZ1 rows and the all-gathered shards."""
     with tempfile.TemporaryDirectory() as d:
         spawn_group(_ipc_worker, world, lambda port: (world, port, d, graph_steps, sync,
                                               4 if sync in ("xact", "auto") else 0))
@@ -234,6 +237,35 @@ def test_two_processes_ipc(world, graph_steps, sync):
         assert torch.equal(Ps[0], P)
     err = (Ps[0] - _reference(world, 6, 0.05, 4)).abs().max().item()
     assert err < 2e-5, err
+
+
+def _long_worker(rank, world, port, outdir, sync, launches):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    ctx = DistContext.from_env(device="cuda", backend="gloo")
+    tr = MlpTrainer(MlpSpec(DIMS), synthetic_mnist(64 * 4, seed=300 + rank), batch=64, lr=0.05,
+                    ctx=ctx, seed=7, sync=sync, xchg_timeout_ms=5000.0, auto_fallback="torch")
+    assert tr.sync_active == sync and tr.persistent
+    for n in launches:
+        tr.train_steps(n)
+    tr.synchronize()
+    torch.save({"P": tr.P.cpu()}, os.path.join(outdir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+@pytest.mark.parametrize("sync", ["pkx", "pkg"])
+def test_gram_forms_many_steps_ipc(sync):
+    """37 steps in three launches (13, 1, 23): every parity half and every one
+    of pkx's three rotating dZ1 slots is reused many times over, across launch
+    splits and epoch wrap-arounds (4 batches), so a slot region that overlaps
+    another or a tag that can match stale rows would show here."""
+    launches = (13, 1, 23)
+    with tempfile.TemporaryDirectory() as d:
+        spawn_group(_long_worker, 2, lambda port: (2, port, d, sync, launches))
+        Ps = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)["P"] for r in range(2)]
+    assert torch.equal(Ps[0], Ps[1])
+    err = (Ps[0] - _reference(2, sum(launches), 0.05, 4)).abs().max().item()
+    assert err < 1e-4, err
 
 
 def _ar_worker(rank, world, port, outdir, algo="oneshot"):

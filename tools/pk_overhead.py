@@ -115,7 +115,7 @@ t.train_steps(20)
 t.synchronize()
 C.mlp_persist_set_stamping(False)
 v = C.mlp_persist_stamps()
-e = [v[(2 * 8 + 0) * 8 + p] for p in range(6)]
+e = [v[(3 * 8 + 0) * 8 + p] for p in range(6)]  # role 3, row 0: the launch edges
 us = lambda a_, b_: round((b_ - a_) / 100.0, 2)  # noqa: E731
 out["n20_kernel_edges_us"] = {
     "l1_prologue": us(e[0], e[1]), "l1_loop_and_epilogue": us(e[1], e[2]),

@@ -5,7 +5,11 @@ N-rank persistent launch while the other N-1 ranks' receive buffers live on
 the same device and every flag it would wait on is preset.  Each step then
 holds the kernel's own work plus its pushes (into local uncached HBM instead
 of over xGMI) but no link transfer and no peer skew -- the lone-replica probe
-of profiles/r1_sync_probe_lone_replica.json, for pk.
+of profiles/r1_sync_probe_lone_replica.json, for every persistent form:
+algo 0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx.  The Gram forms poll the peers' dZ1
+rows by their tags, which no preset can match: the probe switch of the kernel
+(mlp_persist_set_probe, testing only) takes them as arrived; pkx reads N
+copies of this replica's swizzled shard as the all-gathered inputs.
 
 Prints one JSON line per N, with the exchange bytes each replica sends per
 step (to all peers) from the kernel's slot layout."""
@@ -19,16 +23,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def pk_bytes_out(n: int, algo: int = 0) -> int:
-    """Bytes one replica pushes per step at n ranks (kernels/mlp_persist.hip):
-    each of the 224 layer-1 waves sums an 8-float-per-lane slot (2 KiB), the
-    16 gradient-block waves 16 / 8 / 4 floats per lane (3 layers: wave 0 four
-    float4, waves 1-3 two).  One-shot (pk): every slot to every peer; two-shot
-    (pk2): (n-1)/n of each slot to its owners, then the owners' (n-1)/n share
-    to every peer."""
-    slot_bytes = 224 * 64 * 8 * 4 + 4 * (64 * 16 * 4 + 3 * 64 * 8 * 4)
-    if algo == 0:
-        return (n - 1) * slot_bytes
-    return 2 * (n - 1) * slot_bytes // n
+    """Bytes one replica pushes per step at n ranks (kernels/mlp_persist.hip).
+    Direct form (pk / pk2): each of the 224 layer-1 waves sums an
+    8-float-per-lane slot (2 KiB), the 16 gradient-block waves 16 / 8 / 4
+    floats per lane (3 layers: wave 0 four float4, waves 1-3 two).  Gram forms
+    (pkg / pkg2 / pkx): the 224 layer-1 slots (not in pkx), the 16 gradient
+    tiles' slots (3 layers: 2 dW2 waves of 4 floats a lane each, the 4 W3
+    owners a dW3 wave and a bias wave: 40 slots of 1 KiB) and this replica's
+    dZ1 rows as 8-B granules (64 x 128 x 8 = 64 KiB) to every peer.  One-shot:
+    every slot to every peer; two-shot: (n-1)/n of each slot to its owners,
+    then the owners' (n-1)/n share to every peer."""
+    if algo <= 1:
+        slot_bytes = 224 * 64 * 8 * 4 + 4 * (64 * 16 * 4 + 3 * 64 * 8 * 4)
+    else:
+        slot_bytes = (224 * 64 * 8 * 4 if algo < 4 else 0) + 40 * 1024
+    out = (n - 1) * slot_bytes if algo in (0, 2, 4) else 2 * (n - 1) * slot_bytes // n
+    if algo >= 2:
+        out += (n - 1) * 64 * 128 * 8
+    return out
 
 
 def main() -> int:
@@ -36,7 +48,9 @@ def main() -> int:
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--launch", type=int, default=0, help="steps per launch (0: all in one)")
-    ap.add_argument("--algo", type=int, default=0, help="0: pk (one-shot), 1: pk2 (two-shot)")
+    ap.add_argument("--stamps", default="", help="also write the phase stamps of each N (JSON lines)")
+    ap.add_argument("--algo", type=int, default=0,
+                    help="0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx (exchange-free layer 1)")
     a = ap.parse_args()
     import torch
 
@@ -60,6 +74,17 @@ def main() -> int:
             for x in xs:
                 x.fill_flags(1 << 62)
             tr.runner.set_world_size(n)
+            if a.algo >= 2:
+                from hipdsml.engine.gram import gram_table_dp
+                from hipdsml.parallel.xchg import swizzle_inputs
+
+                nb = tr.nbatches
+                Xs = tr.X[: nb * 64, :784].reshape(1, nb, 64, 784).expand(n, nb, 64, 784)
+                tr.runner.set_persist_gram(gram_table_dp(Xs, 0))
+                if a.algo == 4:
+                    xall = swizzle_inputs(Xs.reshape(n, nb * 64, 784), 64)
+                    tr.runner.set_persist_xall(xall, xall[0].numel())
+                C.mlp_persist_set_probe(True)
             tr.runner.set_persist(tr.pk_buf, tr.pk_err, 5000.0, xs[0], a.algo)
         torch.cuda.synchronize()
 
@@ -75,7 +100,21 @@ def main() -> int:
         run(a.steps)
         tr.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
-        print(json.dumps({"mode": ("pk2" if a.algo else "pk") if n > 1 else "none", "ranks": n,
+        stamps = None
+        if a.stamps:
+            from pk_stamps import decode
+
+            C.mlp_persist_set_stamping(True)
+            run(32)
+            tr.synchronize()
+            C.mlp_persist_set_stamping(False)
+            stamps = decode(C.mlp_persist_stamps(), tr.spec)
+            with open(a.stamps, "a") as f:
+                f.write(json.dumps({"mode": ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo], "ranks": n,
+                                    "stamps": stamps}) + "\n")
+        C.mlp_persist_set_probe(False)
+        name = ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo]
+        print(json.dumps({"mode": name if n > 1 else "none", "ranks": n,
                           "us_per_step": round(dt * 1e6, 2),
                           "bytes_out_per_step": pk_bytes_out(n, a.algo),
                           "bytes_per_peer_per_step": pk_bytes_out(n, a.algo) // max(n - 1, 1)}),

@@ -17,49 +17,58 @@ from hipdsml.ops.native import require_native  # noqa: E402
 from hipdsml.parallel.dist import DistContext  # noqa: E402
 
 C = require_native()
-spec = MlpSpec.parse(sys.argv[2]) if len(sys.argv) > 2 else MlpSpec((784, 128, 64, 10))
-t = MlpTrainer(spec, synthetic_mnist(64 * 100, seed=1), batch=64, lr=0.01,
-               ctx=DistContext(device=torch.device("cuda", 0)))
-assert t.persistent
-t.train_steps(100)
-t.synchronize()
-C.mlp_persist_set_stamping(True)
-t.train_steps(32)
-t.synchronize()
-C.mlp_persist_set_stamping(False)
-v = C.mlp_persist_stamps()
-st = [[[v[(r * 8 + s) * 8 + p] for p in range(8)] for s in range(8)] for r in range(4)]
 L1 = ["fwd+publish", "dZ1 wait", "bwd+update"]
 CH = ["partials flags wait", "partials load+H1, W wait+load", "fwd+softmax", "bwd+dZ1 publish",
       "rows publish"]
 GB = ["rows wait+load", "dW/db MFMAs", "exchange+update", "publish"]
-out = {"model": str(spec), "layer1": {}, "chain": {}, "grad": {}, "step_us": None}
-for name, role, labels in (("layer1", 0, L1), ("chain", 1, CH), ("grad", 2, GB)):
-    for k, lab in enumerate(labels):
-        d = [(st[role][s][k + 1] - st[role][s][k]) / 100.0 for s in range(8)]
-        out[name][lab] = round(statistics.median(d), 3)
-steps = [(st[0][s + 1][0] - st[0][s][0]) / 100.0 for s in range(7)]
-out["step_us"] = round(statistics.median(steps), 3)
-med = lambda xs: round(statistics.median(xs), 3)  # noqa: E731
-# cross-role hand-offs: layer-1 publish -> chain has H1; chain dZ1 publish ->
-# layer-1 has dZ1; chain rows -> gradient block has them; gradient publish ->
-# chain has the next step's weights
-out["l1_publish_to_chain_h1_us"] = med([(st[1][s][2] - st[0][s][1]) / 100.0 for s in range(8)])
-out["chain_dz1_publish_to_l1_ready_us"] = med([(st[0][s][2] - st[1][s][4]) / 100.0 for s in range(8)])
-out["chain_rows_to_grad_ready_us"] = med([(st[2][s][1] - st[1][s][5]) / 100.0 for s in range(8)])
-out["grad_publish_to_chain_w_ready_us"] = med([(st[1][s + 1][1] - st[2][s][4]) / 100.0 for s in range(7)])
-out["chain_flag_wait_us"] = med([(st[1][s][1] - st[1][s][0]) / 100.0 for s in range(8)])
-if spec.dims and all(st[1][s][6] for s in range(8)):
-    # single-replica Gram form: chain step start -> Z1 poll begins (weights
-    # fetched first for 2 layers) -> Z1 seen; layer-1 gk = 0 block: dZ1 ready ->
-    # Z1 = P + C stored; Z1 stored (step s) -> chain sees it (step s+1)
-    out["gram"] = {
-        "chain_start_to_z1_poll_us": med([(st[1][s][6] - st[1][s][0]) / 100.0 for s in range(8)]),
-        "chain_z1_poll_us": med([(st[1][s][1] - st[1][s][6]) / 100.0 for s in range(8)]),
-        "l1_dz1_ready_to_z1_stored_us": med([(st[0][s][4] - st[0][s][2]) / 100.0 for s in range(8)]),
-        "z1_stored_to_chain_seen_us": med([(st[1][s + 1][1] - st[0][s][4]) / 100.0 for s in range(7)]),
-    }
-out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
-print(json.dumps(out, indent=1))
-if len(sys.argv) > 1:
-    json.dump(out, open(sys.argv[1], "w"), indent=1)
+
+
+def decode(v, spec) -> dict:
+    """Phase medians (us) from mlp_persist_stamps() of a stamped launch."""
+    st = [[[v[(r * 8 + s) * 8 + p] for p in range(8)] for s in range(8)] for r in range(4)]
+    out = {"model": str(spec), "layer1": {}, "chain": {}, "grad": {}, "step_us": None}
+    med = lambda xs: round(statistics.median(xs), 3)  # noqa: E731
+    for name, role, labels in (("layer1", 0, L1), ("chain", 1, CH), ("grad", 2, GB)):
+        for k, lab in enumerate(labels):
+            d = [(st[role][s][k + 1] - st[role][s][k]) / 100.0 for s in range(8)
+                 if st[role][s][k + 1] and st[role][s][k]]
+            out[name][lab] = med(d) if d else None
+    out["step_us"] = med([(st[0][s + 1][0] - st[0][s][0]) / 100.0 for s in range(7)])
+    # cross-role hand-offs: layer-1 publish -> chain has H1; chain dZ1 publish ->
+    # layer-1 has dZ1; chain rows -> gradient block has them; gradient publish ->
+    # chain has the next step's weights
+    out["l1_publish_to_chain_h1_us"] = med([(st[1][s][2] - st[0][s][1]) / 100.0 for s in range(8)])
+    out["chain_dz1_publish_to_l1_ready_us"] = med([(st[0][s][2] - st[1][s][4]) / 100.0 for s in range(8)])
+    out["chain_rows_to_grad_ready_us"] = med([(st[2][s][1] - st[1][s][5]) / 100.0 for s in range(8)])
+    out["grad_publish_to_chain_w_ready_us"] = med([(st[1][s + 1][1] - st[2][s][4]) / 100.0 for s in range(7)])
+    out["chain_flag_wait_us"] = med([(st[1][s][1] - st[1][s][0]) / 100.0 for s in range(8)])
+    if all(st[1][s][6] for s in range(8)):
+        # Gram forms: chain step start -> Z1 poll begins (weights fetched first
+        # for 2 layers) -> Z1 seen; layer-1 gk = 0 block: dZ1 ready -> Z1 = P + C
+        # stored; Z1 stored (step s) -> chain sees it (step s+1)
+        out["gram"] = {
+            "chain_start_to_z1_poll_us": med([(st[1][s][6] - st[1][s][0]) / 100.0 for s in range(8)]),
+            "chain_z1_poll_us": med([(st[1][s][1] - st[1][s][6]) / 100.0 for s in range(8)]),
+            "l1_dz1_ready_to_z1_stored_us": med([(st[0][s][4] - st[0][s][2]) / 100.0 for s in range(8)]),
+            "l1_z1_stored_to_step_end_us": med([(st[0][s][3] - st[0][s][4]) / 100.0 for s in range(8)]),
+            "z1_stored_to_chain_seen_us": med([(st[1][s + 1][1] - st[0][s][4]) / 100.0 for s in range(7)]),
+        }
+    out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
+    return out
+
+
+if __name__ == "__main__":
+    spec = MlpSpec.parse(sys.argv[2]) if len(sys.argv) > 2 else MlpSpec((784, 128, 64, 10))
+    t = MlpTrainer(spec, synthetic_mnist(64 * 100, seed=1), batch=64, lr=0.01,
+                   ctx=DistContext(device=torch.device("cuda", 0)))
+    assert t.persistent
+    t.train_steps(100)
+    t.synchronize()
+    C.mlp_persist_set_stamping(True)
+    t.train_steps(32)
+    t.synchronize()
+    C.mlp_persist_set_stamping(False)
+    out = decode(C.mlp_persist_stamps(), spec)
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 1:
+        json.dump(out, open(sys.argv[1], "w"), indent=1)
