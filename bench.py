@@ -136,6 +136,34 @@ def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200,
     return out
 
 
+def _dp_phases(tr) -> dict:
+    """Phase timeline (us) of rank 0's persistent data-parallel step: one
+    stamped launch of 32 steps on every rank (tools/pk_stamps.py decode:
+    layer-1 block 0, chain 0, gradient tile 0, steps 8..15), so the first
+    multi-GPU run records WHERE the step time goes (cross-device hops, pushes,
+    exchanges), not just its total."""
+    import torch
+
+    from hipdsml.ops.native import require_native
+
+    C = require_native()
+    try:
+        tr.synchronize()
+        tr.ctx.barrier()
+        C.mlp_persist_set_stamping(True)
+        tr.train_steps(32)
+        tr.synchronize()
+        C.mlp_persist_set_stamping(False)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        from pk_stamps import decode
+
+        return decode(C.mlp_persist_stamps(), tr.spec)
+    except Exception as e:  # noqa: BLE001 -- diagnostics only, never fail the bench
+        C.mlp_persist_set_stamping(False)
+        torch.cuda.synchronize()
+        return {"error": str(e)[:200]}
+
+
 def _physical_gpus(ctx) -> int:
     """Distinct GPUs (host, device UUID) the job's ranks run on."""
     import torch
@@ -206,6 +234,9 @@ def run(a) -> int:
     # every replica applied the same summed gradient: the parameters must be
     # bit-identical on all ranks after the timed steps (no weight broadcast)
     identical = ctx.replicas_identical(tr.P, "bench/P") if n > 1 else True
+    phases = None
+    if n > 1 and tr.backend == "hip" and tr.persistent and not a.no_stamps:
+        phases = _dp_phases(tr)  # after the timed steps and the identity check
     ar_us = None
     if n > 1 and tr.backend == "hip" and not a.no_allreduce_probe:
         ar_us = allreduce_latency_us(ctx, tr.comm, ring_chunk=a.ring_chunk)
@@ -255,6 +286,7 @@ def run(a) -> int:
             "ring_chunk_bytes": tr._ring_chunk if tr.comm is not None else None,
             "ring_chunk_sweep_us": tr.ring_chunk_sweep_us if tr.backend == "hip" else None,
             "allreduce_1MiB_us": ar_us,
+            "dp_phases_us": phases,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
             "replicas_identical": identical,
@@ -304,6 +336,8 @@ def main(argv=None) -> int:
     ap.add_argument("--samples-per-rank", type=int, default=60032)
     ap.add_argument("--no-allreduce-probe", action="store_true",
                     help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="skip the stamped diagnostic launch of the persistent DP step (N>1)")
     ap.add_argument("--no-sync-sweep", action="store_true",
                     help="skip timing every sync candidate (N>1)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",

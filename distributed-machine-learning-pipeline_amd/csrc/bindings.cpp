@@ -701,8 +701,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
-  m.def("mlp_persist_set_probe", [](bool on) { mlp_persist_set_probe(on); },
-        "testing only: peers' dZ1 rows taken as arrived (lone-replica probe of the Gram forms)");
+  m.def("mlp_persist_set_probe", [](int mode) { mlp_persist_set_probe(mode); },
+        "testing only: 0 off; 1 peers' dZ1 rows taken as arrived (lone-replica probe of the Gram "
+        "forms); 2 mirror: every push loops back into this replica's own buffer in the peer's "
+        "source slot (N-replica step against N - 1 copies of itself)");
   m.def("mlp_persist_set_jitter", [](int ticks) { mlp_persist_set_jitter(ticks); },
         "testing only: every block of the single-replica persistent step sleeps a pseudo-random "
         "0..ticks x 64 cycles before its hand-offs (0 = off)");

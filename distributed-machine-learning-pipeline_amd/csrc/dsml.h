@@ -102,7 +102,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              const struct XchgTab* tab = nullptr, int algo = 0,
                              const float* gram = nullptr, int carry = 0,
                              const float* xsw = nullptr, int64_t xsw_stride = 0);
-void mlp_persist_set_probe(bool on);  // testing only: lone-replica probe of the Gram forms
+void mlp_persist_set_probe(int mode);  // testing only: 0 off, 1 lone-replica probe, 2 mirror
 // Single replica: the Gram table the persistent step reads, float[nbatches][64][64]
 // with G1T[b][m'][m] = X_{b-1}[m'] . X_b[m] + 1 (rows past the batch repeat its
 // last row; b - 1 wraps), and `carry` = 1 when the hand-off buffer still holds

@@ -12,39 +12,53 @@
 // spread over tens of CUs; a three-launch step costs ~18-21 us, almost all of
 // it kernel boundaries, weight reloads and dependent memory round trips.
 //
-// Roles (64 workgroups x 256 threads, one per CU, 1/4 of the chip):
+// Two families of roles share this file.
 //
-//  * 56 layer-1 blocks (gn < 8, gk < 7) own W1[16 gn .. +16][112 gk .. +112]
-//    (and b1[16 gn ..] when gk == 0) in LDS for the whole launch.  Per step:
-//    Z1 partial [64 x 16] = X[:, k slice] . W1 tile^T (v_mfma_f32_16x16x4_f32,
-//    4 k per 16-B LDS read per lane), published with one flag; then, once the
-//    chains have published dZ1, dW1 tile = dZ1[:, n slice]^T . X[:, k slice]
-//    (and db1 = colsum dZ1 when gk == 0) and the SGD update in LDS.  The next
-//    step's X slice is loaded by LDS-DMA while the block waits.
-//  * 4 chain blocks c own batch rows 16c .. 16c+15 and the upper layers'
-//    weights in LDS.  Per step: H1 = relu(sum of the 7 k-partials), upper
-//    layers' forward, softmax + cross-entropy (eps 1e-10, client.go:151),
-//    dLogits = (p - y) / B, backward to dZ1, published to the layer-1 blocks:
-//    the chains hold ONLY this critical path.  Their rows of H1 (H2), dZ2
-//    (dZ3) then go to the gradient blocks, and the next step's upper weights
-//    come back from them.
-//  * 4 gradient blocks g own a quarter of the upper weights (3 layers: W2
-//    rows / W3 columns 16g .. +16, b2 slice, b3 in g = 0; 2 layers: W2
-//    columns 32g .. +32, b2 in g = 0).  Per step: read the 64 rows of the
-//    chains, full-batch dW / db of their slice (fixed summation order), SGD
-//    update, publish the updated slice.  Off the critical path: the chains
-//    pick it up while they wait for the next step's partials.  (Round 2 kept
-//    this work in the chains, which then took 10.4 us per step for 4.7 us of
-//    critical path: profiles/r2_pk_stamps_place1.json.)
+// GRAM FORM (single replica, and the data-parallel pkg / pkg2 / pkx): one
+// launch of 160 workgroups x 256 threads (one per CU), of which 76 work (132
+// with pkx's helpers) and the rest exit at once; placement by blockIdx under
+// round-robin dispatch (block b on XCD b % 8):
+//
+//  * 56 layer-1 blocks (gn < 8, gk < 7) at blockIdx 8 gn + gk + 1 own
+//    W1[16 gn ..][112 gk ..] (b1 slice in gk == 0) in LDS.  SGD gives
+//    Z1(s+1) = P(s+1) + C(s+1) with P(s+1) = X(s+1) W1(s)^T + b1(s) and the
+//    correction C(s+1) = -lr (X(s+1) X(s)^T + 1) dZ1(s) over a per-batch Gram
+//    block tabulated at init (engine/gram.py).  Per step each block publishes
+//    its k-partial of P(s+1) BEFORE dZ1(s) exists; the four blocks gk = c < 4
+//    are the gatherers of chain c: once dZ1(s) arrives they contract the
+//    correction for chain c's 16 rows (K split over the 4 waves), add the 7
+//    partials and publish Z1(s+1) as {value, step-tag} granules.  Then every
+//    block forms its dW1 tile and updates W1 in LDS.
+//  * 4 chain blocks (blockIdx 8 c) hold only the critical path: poll Z1, ReLU,
+//    layers 2 (and 3), softmax-CE (eps 1e-10, client.go:151), backward to
+//    dZ1, published as tagged granules.  Their activation rows go to the
+//    gradient tiles.
+//  * 16 (3 layers) / 8 (2 layers) gradient tiles (blockIdx 8 (4 + g)): the
+//    upper weights' full-batch dW / db and SGD per tile, published back to the
+//    chains.  Chains and tiles share XCD 0.
+//
+//  Data parallel (N replicas): every chain also pushes its dZ1 rows into every
+//  peer's receive buffer (DZR), each correction sums over every replica with
+//  cross-replica Gram blocks [N][64][64], and the upper tiles' gradients are
+//  summed over the replicas inside the launch (one- / two-shot slot exchange).
+//  The layer-1 gradient: pkg / pkg2 sum each wave's dW1 slot over xGMI; pkx
+//  (exchange-free) forms the global-batch dW1 = sum_r dZ1_r^T X_r itself from
+//  the peers' dZ1 rows and the all-gathered, swizzled input shards, with a
+//  helper block per layer-1 tile on an idle CU from 4 replicas on.
+//
+// DIRECT FORM (data-parallel pk / pk2, 64 workgroups): 56 layer-1 blocks
+// publish their k-partials of Z1 = X W1^T + b1, 4 chain blocks sum them and
+// run the upper layers, 4 gradient blocks own a quarter of the upper weights;
+// every wave's weight-gradient fragments are summed over the replicas.
 //
 // Hand-offs (placement-independent, kernels/common.h for the cross-device
-// ones): dZ1 travels as data-tagged 8-byte granules {fp32, step tag} written
-// by single write-through (sc1) stores and read with sc1 loads until the tags
-// match; partials, chain rows and weight slices are plain fp32 stored sc1 by
-// every wave, drained (s_waitcnt vmcnt(0)), then flagged by one lane behind a
-// workgroup barrier, and read with sc1 loads after the flag (MI355X_MICROARCH
-// "Valid forms", row 1).  Tags are the global step number + 1, so buffers need
-// zeroing only when the step counter is rewound (host side).
+// ones): tagged 8-byte granules {fp32, step tag} written by single
+// write-through (sc1) stores and read with sc1 loads until the tags match;
+// plain fp32 payloads stored sc1 by every wave, drained (s_waitcnt vmcnt(0)),
+// then flagged by one lane behind a workgroup barrier, and read with sc1 loads
+// after the flag (MI355X_MICROARCH "Valid forms", row 1).  Tags are the global
+// step number + 1, so buffers need zeroing only when the step counter is
+// rewound (host side).
 //
 // Every wait is bounded (timeout -> error word, checked by the host after the
 // launch) and gives up at once when another block already timed out, so a
@@ -71,9 +85,11 @@ constexpr int kNPart = kNL1;                            // partial slots per par
 // tiles) sit at blockIdx 8 k; layer-1 block (gn, gk) at blockIdx 8 gn + gk + 1.
 template <int NL> struct GTile { static constexpr int kN = NL == 3 ? 16 : 8; };
 template <int NL> constexpr int pk_grid(bool dp) { return dp ? kNBlk : 8 * (kNCH + GTile<NL>::kN); }
-// Whether blockIdx b does work in the single-replica grid (the rest exit).
-template <int NL> __device__ __forceinline__ bool pk_sr_active(int b) {
-  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < kGN;
+// Whether blockIdx b does work in the Gram-form grid (the rest exit); `helpers`:
+// pkx at >= 4 replicas also runs a dW1 helper per layer-1 block at
+// blockIdx 8 (8 + gn) + gk + 1, on its owner's XCD.
+template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, bool helpers = false) {
+  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < (helpers ? 2 * kGN : kGN);
 }
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
@@ -200,7 +216,12 @@ constexpr int64_t kOffCg = kOffWf + 8;
 constexpr int kWXS = kH2 * kD1 + 16 * kH2 + kH2 + 16;   // 9296 floats
 constexpr int64_t kOffWxs = kOffCg + kB * kD1;
 constexpr int64_t kOffWfs = kOffWxs + 2 * kWXS / 2;
-constexpr int64_t kTotalG = kOffWfs + 32;
+// HX[2][56][4 waves][64 lanes][8]: pkx at >= 4 replicas, the helper blocks'
+// half of every layer-1 tile's dW1 (and db1), parity by step, plain fp32; HF[2][64]
+// flags, one per tile.
+constexpr int64_t kOffHx = kOffWfs + 32;
+constexpr int64_t kOffHf = kOffHx + 2 * kNL1 * 4 * 64 * 8 / 2;
+constexpr int64_t kTotalG = kOffHf + 2 * 64;
 static_assert(kCX % 4 == 0 && kWX % 4 == 0 && (kOffCx % 2) == 0 && (kOffWx % 2) == 0,
               "exchange rows travel as 16-B vectors");
 
@@ -312,6 +333,13 @@ __device__ int g_pk_jitter;
 // taken as arrived whatever their tags, so ONE replica can run the N-rank Gram
 // forms with no peer (its flags preset).  0 in production.
 __device__ int g_pk_probe;
+// Testing only, host side: 0 off, 1 the probe above, 2 MIRROR -- a lone replica
+// sends every "peer" push into its OWN receive buffer, in that peer's source
+// slot (dZ1 rows and gradient slots alike, flags included), so it runs the
+// N-replica data-parallel step against N - 1 exact copies of itself: the
+// result must equal single-replica SGD at the same lr (tests/test_gpu_persist.py
+// covers pkx and its helper blocks at N = 4 and 8 on one GPU this way).
+static int g_pk_probe_mode = 0;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;
   uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
@@ -379,6 +407,9 @@ struct PersistArgs {
   const float* xsw;
   int64_t xsw_stride;
   int32_t dzr3;
+  int32_t helpers;  // pkx at >= 4 replicas: replicas [ (nrep+1)/2, nrep ) of dW1 on helper blocks
+  int32_t mirror;   // testing only (g_pk_probe_mode 2): pushes loop back into this replica's buffer
+  int32_t probe;    // testing only (g_pk_probe_mode 1): peers' tagged data taken as arrived
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -432,7 +463,8 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   for (int d = 0; d < a.nrep; ++d) {
     if (d == a.rep) continue;
     const __amdgpu_buffer_rsrc_t r =
-        rsrc(a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
+        rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot + (int64_t)d * per_src
+                      : a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
 #pragma unroll
     for (int j = 0; j < NV; ++j) px_st4(r, (lane * 16 + 4 * j) * 4, v[j]);
   }
@@ -442,8 +474,9 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   if (lane == 0)
     for (int d = 0; d < a.nrep; ++d)
       if (d != a.rep)
-        __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + a.rep * a.pxslots), tag,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store((px_g64*)(a.mirror ? a.xt.flags[a.rep] + slot + d * a.pxslots
+                                              : a.xt.flags[d] + slot + a.rep * a.pxslots),
+                           tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool ok = true;
   if (lane < a.nrep && lane != a.rep)
     ok = poll_flag_ge<1>(a.xt.flags[a.rep] + slot + lane * a.pxslots, tag, a.xerr, a.timeout_ticks);
@@ -564,9 +597,107 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
   return true;
 }
 
+// Tagged one-shot form (the Gram forms' one-shot sums, NV <= 2): every value
+// travels as an 8-B {value, step tag} granule (two per 16-B store), so the
+// sender neither drains its stores (no write-acknowledge round trip over
+// xGMI) nor raises a flag, and the receiver polls the data itself: one
+// one-way hop instead of ack + flag + load.  Stale granules of step s - 2 (the
+// same parity half) carry another tag.  Values are summed in rank order as in
+// px_allreduce_wave (bit-identical replicas).
+template <int NV>
+__device__ __forceinline__ bool px_allreduce_tagged_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV],
+                                                         int slot) {
+  static_assert(NV == 1, "the gradient tiles' slots: one float4 a lane, as 4 granules");
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
+  const uint32_t tag = (uint32_t)(s + 1);
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= a.nrep || d == a.rep) continue;
+    const __amdgpu_buffer_rsrc_t r =
+        rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot + (int64_t)d * per_src
+                      : a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const nu4v lo = {__float_as_uint(v[j].x), tag, __float_as_uint(v[j].y), tag};
+      const nu4v hi = {__float_as_uint(v[j].z), tag, __float_as_uint(v[j].w), tag};
+      __builtin_amdgcn_raw_buffer_store_b128(lo, r, (lane * 16 + 8 * j) * 4, 0, kScSys);
+      __builtin_amdgcn_raw_buffer_store_b128(hi, r, (lane * 16 + 8 * j + 4) * 4, 0, kScSys);
+    }
+  }
+  // every source's granules of this slot, all loads of a round in flight together
+  const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot;
+  nu4v g[kMaxPeers][2 * NV];  // a source's granules, kept once its tags match
+  uint32_t need = 0;
+#pragma unroll
+  for (int src = 0; src < kMaxPeers; ++src)
+    if (src < a.nrep && src != a.rep) need |= 1u << src;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t spins = 0;
+  bool ok = true;
+  while (need != 0u) {
+#pragma unroll
+    for (int src = 0; src < kMaxPeers; ++src) {
+      if (need & (1u << src)) {
+        const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
+#pragma unroll
+        for (int h = 0; h < 2 * NV; ++h) g[src][h] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane * 16 + 4 * h) * 4, 0, kScSys);
+      }
+    }
+#pragma unroll
+    for (int src = 0; src < kMaxPeers; ++src) {
+      if (need & (1u << src)) {
+        bool all = true;
+#pragma unroll
+        for (int h = 0; h < 2 * NV; ++h) all = all && g[src][h].y == tag && g[src][h].w == tag;
+        if (all || a.probe) need &= ~(1u << src);
+      }
+    }
+    if (need == 0u) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      __hip_atomic_fetch_or(a.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok = false;
+      break;
+    }
+    if ((++spins & 63u) == 0u &&
+        __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      ok = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  if (!ok) return false;
+  float4 acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int src = 0; src < kMaxPeers; ++src) {
+    if (src < a.nrep) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float4 y = src == a.rep ? v[j]
+                                      : make_float4(__uint_as_float(g[src][2 * j].x), __uint_as_float(g[src][2 * j].z),
+                                                    __uint_as_float(g[src][2 * j + 1].x),
+                                                    __uint_as_float(g[src][2 * j + 1].z));
+        acc[j].x += y.x; acc[j].y += y.y; acc[j].z += y.z; acc[j].w += y.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = acc[j];
+  return true;
+}
+
 template <int NV>
 __device__ __forceinline__ bool px_sum_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV], int slot) {
   return a.algo ? px_allreduce2_wave<NV>(a, s, v, slot) : px_allreduce_wave<NV>(a, s, v, slot);
+}
+// The Gram forms' sums: tagged one-shot, or the flagged two-shot (pkg2).
+template <int NV>
+__device__ __forceinline__ bool px_sum_wave_g(const PersistArgs& a, uint64_t s, float4 (&v)[NV], int slot) {
+  return a.algo ? px_allreduce2_wave<NV>(a, s, v, slot) : px_allreduce_tagged_wave<NV>(a, s, v, slot);
 }
 
 // A block that gave up leaves a mark in host memory on its way out, so the
@@ -912,7 +1043,7 @@ __device__ __forceinline__ bool pk_l1_gather_rows(__amdgpu_buffer_rsrc_t rb, f4v
 // itself from the swizzled input shards, so no layer-1 gradient crosses xGMI.
 constexpr int kKT = kD0 / 16;  // 49 k tiles of the swizzled shards
 template <int NL, int XMODE>
-__device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
+__device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk) {
   constexpr bool XM = XMODE >= 1, XL = XMODE == 2;
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
@@ -1055,7 +1186,7 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
       Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
       Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
     }
-    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false) && pk_sr_active<NL>(tid) && ok) {
+    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false) && pk_sr_active<NL>(tid, a.helpers) && ok) {
       // hand the step counter on once every block has read it (SF tags)
       const uint32_t t0 = (uint32_t)(s0 + 1);
       poll.start();
@@ -1175,11 +1306,12 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
         }
       };
       float4 xC[2][4];
-      for (int r = 0; r < a.nrep; r += 2) {
-        if (r + 1 < a.nrep) xl_load(xC, r + 1, s);
+      const int hi = a.helpers ? (a.nrep + 1) / 2 : a.nrep;  // the helper sums [hi, nrep)
+      for (int r = 0; r < hi; r += 2) {
+        if (r + 1 < hi) xl_load(xC, r + 1, s);
         pass(xB, r);
-        if (r + 1 < a.nrep) {
-          if (r + 2 < a.nrep) xl_load(xB, r + 2, s);
+        if (r + 1 < hi) {
+          if (r + 2 < hi) xl_load(xB, r + 2, s);
           pass(xC, r + 1);
         }
       }
@@ -1187,6 +1319,22 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
         g[0] = g[0] + g[1];
         db += __shfl_xor(db, 16, 64);
         db += __shfl_xor(db, 32, 64);
+      }
+      if (a.helpers) {
+        // the helper's half (same fragment layout), added in a fixed order
+        bool hok = true;
+        if (lane == 0) hok = wait_flag(rb, kOffHf + (int64_t)(s & 1) * 64 + lb, tag, poll);
+        hok = __builtin_amdgcn_ballot_w64(!hok) == 0;
+        asm volatile("" ::: "memory");
+        const int64_t ho = kOffHx * 2 + ((((int64_t)(s & 1) * kNL1 + lb) * 4 + w) * 64 + lane) * 8;
+        const f4v h0v = ld_f4(rb, ho), h1v = ld_f4(rb, ho + 4);
+        if (hok) {
+          g[0] = g[0] + f32x4{h0v[0], h0v[1], h0v[2], h0v[3]};
+          if (w < 3) g[1] = g[1] + f32x4{h1v[0], h1v[1], h1v[2], h1v[3]};
+          else db += h1v[0];
+        }
+        ok = __syncthreads_and(hok ? 1 : 0) != 0;
+        if (!ok) break;
       }
     } else {
     const float* Xl = xbuf(s);
@@ -1251,6 +1399,144 @@ __device__ void pk_layer1_gram(const PersistArgs& a, float* lds, int lb, int blk
   if (gk == 0 && tid < 16) a.P[a.b_off[0] + n0 + tid] = B1[tid];
   pk_report(a, ok);
   if (lb == 0) PK_EDGE(2);
+}
+
+// pkx helper block (>= 4 replicas): replicas [(nrep + 1) / 2, nrep) of the dW1
+// tile (and db1) of layer-1 block lb, computed exactly as the owner computes
+// its half and handed over through HX[parity] + one flag; the owner adds it to
+// its own half in a fixed order.  Same XCD as the owner, so the shared X
+// slices and the hand-off stay in that XCD's L2.
+__device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, int lb, int blk) {
+  const int gn = lb % kGN, gk = lb / kGN;
+  const int n0 = gn * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  pk_started(a, blk, s0);
+  float* Dh = lds;  // dZ1 tiles of replicas h0 .. nrep - 1: [nrep - h0][64][17]
+  const int probe = g_pk_probe;
+  const int h0 = (a.nrep + 1) / 2;
+  const int kt0 = kKC / 16 * gk + w, kt1 = kKC / 16 * gk + (w < 3 ? w + 4 : w);
+  auto xl_load = [&](float4 (&B)[2][4], int r, uint64_t s) __attribute__((always_inline)) {
+    const float* xr = a.xsw + (int64_t)r * a.xsw_stride +
+                      (int64_t)(s % (uint64_t)a.nbatches) * (kKT * 1024) + lane * 4;
+#pragma unroll
+    for (int wq = 0; wq < 4; ++wq) {
+      B[0][wq] = *reinterpret_cast<const float4*>(xr + kt0 * 1024 + wq * 256);
+      B[1][wq] = *reinterpret_cast<const float4*>(xr + kt1 * 1024 + wq * 256);
+    }
+  };
+  bool ok = true;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);
+    float4 xB[2][4], xC[2][4];
+    xl_load(xB, h0, s);  // data only: in flight during the waits
+    if (probe) {
+      // lone-replica probe: the peers' rows are taken as arrived, so pace this
+      // block on the own replica's dZ1 (the owner's wait) instead of running ahead
+      const int m = tid >> 2, qq = tid & 3;
+      const int64_t gg = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
+      poll.start();
+      for (;;) {
+        const uint4 u0 = ld_gran2(rb, gg), u1 = ld_gran2(rb, gg + 2);
+        if (u0.y == tag && u0.w == tag && u1.y == tag && u1.w == tag) break;
+        if (!poll.again()) { ok = false; break; }
+      }
+    }
+    {
+      // this half's dZ1 tiles: own rows from the local DZ1 region, the peers'
+      // from their DZR slots, every load of a round in flight together
+      const int m = tid >> 2, qq = tid & 3;
+      uint32_t need = 0;
+#pragma unroll
+      for (int r2 = 0; r2 < kMaxPeers; ++r2)
+        if (r2 >= h0 && r2 < a.nrep) need |= 1u << r2;
+      poll.start();
+      while (need != 0u) {
+        nu4v v0[kMaxPeers], v1[kMaxPeers];
+#pragma unroll
+        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
+          if (need & (1u << r2)) {
+            if (r2 == a.rep) {
+              const int64_t gg = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
+              const uint4 u0 = ld_gran2(rb, gg), u1 = ld_gran2(rb, gg + 2);
+              v0[r2] = nu4v{u0.x, u0.y, u0.z, u0.w};
+              v1[r2] = nu4v{u1.x, u1.y, u1.z, u1.w};
+            } else {
+              const __amdgpu_buffer_rsrc_t rr = rsrc(a.xt.buf[a.rep] + pk_dzr_base(a, s, r2));
+              const int off = (m * kD1 + n0 + 4 * qq) * 8;
+              v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
+              v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
+            }
+          }
+        }
+#pragma unroll
+        for (int r2 = 0; r2 < kMaxPeers; ++r2) {
+          if ((need & (1u << r2)) && ((probe && r2 != a.rep) ||
+                                      (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
+            float* d = Dh + (r2 - h0) * (kB * 17) + m * 17 + 4 * qq;
+            d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
+            d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
+            need &= ~(1u << r2);
+          }
+        }
+        if (need != 0u && !poll.again()) { ok = false; break; }
+      }
+      ok = __syncthreads_and(ok ? 1 : 0) != 0;
+      if (!ok) break;
+    }
+    f32x4 g[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float db = 0.f;
+    auto pass = [&](const float4 (&cB)[2][4], int r) __attribute__((always_inline)) {
+      const float* Dr = Dh + (r - h0) * (kB * 17);
+#pragma unroll
+      for (int wq = 0; wq < 4; ++wq) {
+        const float d0 = Dr[(4 * wq + q) * 17 + i], d1 = Dr[(4 * wq + 16 + q) * 17 + i];
+        const float d2 = Dr[(4 * wq + 32 + q) * 17 + i], d3 = Dr[(4 * wq + 48 + q) * 17 + i];
+        if (w < 3) {
+          g[0] = mfma_f32_16x16x4(d0, cB[0][wq].x, g[0]);
+          g[1] = mfma_f32_16x16x4(d0, cB[1][wq].x, g[1]);
+          g[0] = mfma_f32_16x16x4(d1, cB[0][wq].y, g[0]);
+          g[1] = mfma_f32_16x16x4(d1, cB[1][wq].y, g[1]);
+          g[0] = mfma_f32_16x16x4(d2, cB[0][wq].z, g[0]);
+          g[1] = mfma_f32_16x16x4(d2, cB[1][wq].z, g[1]);
+          g[0] = mfma_f32_16x16x4(d3, cB[0][wq].w, g[0]);
+          g[1] = mfma_f32_16x16x4(d3, cB[1][wq].w, g[1]);
+        } else {
+          g[0] = mfma_f32_16x16x4(d0, cB[0][wq].x, g[0]);
+          g[1] = mfma_f32_16x16x4(d1, cB[0][wq].y, g[1]);
+          g[0] = mfma_f32_16x16x4(d2, cB[0][wq].z, g[0]);
+          g[1] = mfma_f32_16x16x4(d3, cB[0][wq].w, g[1]);
+          db += (d0 + d1) + (d2 + d3);
+        }
+      }
+    };
+    for (int r = h0; r < a.nrep; r += 2) {
+      if (r + 1 < a.nrep) xl_load(xC, r + 1, s);
+      pass(xB, r);
+      if (r + 1 < a.nrep) {
+        if (r + 2 < a.nrep) xl_load(xB, r + 2, s);
+        pass(xC, r + 1);
+      }
+    }
+    if (w == 3) {
+      g[0] = g[0] + g[1];
+      db += __shfl_xor(db, 16, 64);
+      db += __shfl_xor(db, 32, 64);
+    }
+    // hand the half over: the owner's fragment layout, plain fp32 drained by
+    // every wave, then one flag
+    const int64_t ho = kOffHx * 2 + ((((int64_t)(s & 1) * kNL1 + lb) * 4 + w) * 64 + lane) * 8;
+    st_f4(rb, ho, f4v{g[0][0], g[0][1], g[0][2], g[0][3]});
+    st_f4(rb, ho + 4, w < 3 ? f4v{g[1][0], g[1][1], g[1][2], g[1][3]} : f4v{db, 0.f, 0.f, 0.f});
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_gran(rb, kOffHf + (int64_t)(s & 1) * 64 + lb, __uint_as_float(tag), tag);
+  }
+  pk_report(a, ok);
 }
 
 // -----------------------------------------------------------------------------
@@ -1431,7 +1717,7 @@ __device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, in
 #pragma unroll
   for (int d = 0; d < kMaxPeers; ++d) {
     if (d >= a.nrep || d == a.rep) continue;
-    const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[d] + base);
+    const __amdgpu_buffer_rsrc_t r = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, d) : a.xt.buf[d] + base);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -1439,6 +1725,24 @@ __device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, in
         const u2 wv = {__float_as_uint(v[tt][k]), tag};
         __builtin_amdgcn_raw_buffer_store_b64(wv, r, ((row0 + k) * kD1 + (tt ? col1 : col0)) * 8, 0, kScSys);
       }
+  }
+}
+
+// Data-parallel Gram forms: the chain's last vector-memory ops of a step are its
+// 8 local dZ1 granules and 8 pushed to each peer; only the rows stored BEFORE
+// them must land before the rows flag.  vmcnt retires in issue order, so
+// waiting down to those 8 n outstanding ops drains the rows without waiting for
+// the peers' write acknowledgements (an xGMI round trip) on the tiles' path.
+__device__ __forceinline__ void pk_drain_rows(int nrep) {
+  switch (nrep) {
+    case 2: __asm__ volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: __asm__ volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 4: __asm__ volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 5: __asm__ volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 6: __asm__ volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 7: __asm__ volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    case 8: __asm__ volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    default: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
@@ -1710,6 +2014,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       // the rest of the rows (H2, dZ2, dZ3) go to the gradient blocks now, ahead
       // of the dZ1 stage; drained and flagged at the end of the step
       pk_chain_rows_out<NL>(rb, lds, par, c, local);
+      asm volatile("" ::: "memory");  // the rows' stores stay ahead of the dZ1 stage's (pk_drain_rows)
       // ---- dZ1 = (dZ2 W2) * (H1 > 0), published to the layer-1 blocks ----
       // wave w: n tiles w and w + 4, four accumulator chains interleaved
       {
@@ -1789,6 +2094,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
       if (tid == 0) st_gran(rb, kOffCxf + par * kNCH + c, __uint_as_float(tag), tag);
       PK_STAMP(1, 3);
       pk_chain_rows_out<NL>(rb, lds, par, c, local);  // dZ2 (the logits' gradient)
+      asm volatile("" ::: "memory");  // the rows' stores stay ahead of the dZ1 stage's (pk_drain_rows)
       // ---- dZ1 = (dZ2 W2) * (H1 > 0), published; wave w: n tiles w, w + 4 ----
       {
         f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -1818,7 +2124,8 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 
     // ---- the rest of the rows (stored before the dZ1 stage): drained by every
     // wave, then flagged behind the barrier ----
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (XM) pk_drain_rows(a.nrep);
+    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     if (tid == 0) st_gran(rb, kOffCxf + 8 + par * kNCH + c, __uint_as_float(tag), tag);
     PK_STAMP(1, 5);
@@ -2159,7 +2466,7 @@ struct GTLay {
 };
 
 template <int NL, bool XM>
-__device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
+__device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
@@ -2296,11 +2603,11 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
         float4 v[1];
         if (w < 2 || (w == 2 && own3)) {
           v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
-          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
           gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
         } else if (w == 3 && (own3 || g == 0)) {
           v[0] = make_float4(sb, sb3, 0.f, 0.f);
-          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
           sb = v[0].x;
           sb3 = v[0].y;
         }
@@ -2328,11 +2635,11 @@ __device__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
         float4 v[1];
         if (w == 0) {
           v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
-          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
           gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
         } else if (w == 1 && g == 0) {
           v[0] = make_float4(sb, 0.f, 0.f, 0.f);
-          xok = px_sum_wave<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
           sb = v[0].x;
         }
         ok = __syncthreads_and(xok ? 1 : 0) != 0;
@@ -2423,12 +2730,14 @@ void mlp_persist_k(PersistArgs a) {
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
     constexpr bool XM = MODE >= 2;
-    if (!pk_sr_active<NL>(b)) return;
+    if (!pk_sr_active<NL>(b, MODE == 3 && a.helpers)) return;
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
       else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
-    } else {
+    } else if (y < kGN) {
       pk_layer1_gram<NL, MODE == 3 ? 2 : MODE == 2 ? 1 : 0>(a, lds, y + kGN * (x - 1), b);
+    } else if constexpr (MODE == 3) {
+      pk_l1_helper(a, lds, y - kGN + kGN * (x - 1), b);
     }
   }
 }
@@ -2441,8 +2750,9 @@ void mlp_persist_set_jitter(int ticks) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_jitter), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
-void mlp_persist_set_probe(bool on) {
-  const int v = on ? 1 : 0;
+void mlp_persist_set_probe(int mode) {
+  g_pk_probe_mode = mode;
+  const int v = mode == 1 ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_probe), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
@@ -2534,6 +2844,9 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     a.algo = algo == 4 ? 0 : (algo & 1);
     a.pxslots = algo >= 2 ? kPxSlotsG : kPxSlots;
     a.dzr_off = px_slots_half(a.nrep, algo, kPxSlotsG);
+    a.mirror = g_pk_probe_mode == 2 ? 1 : 0;
+    a.probe = g_pk_probe_mode == 1 ? 1 : 0;
+    if (a.mirror && (algo & 1) == 1 && algo != 4) return hipErrorInvalidValue;  // one-shot sums only
     if (algo == 4) {
       // the slot regions' parity halves are back to back ([2][slots_half], the
       // parity offset is slots_half, not the buffer's half), then the 3
@@ -2543,6 +2856,8 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
       a.dzr_off = 2 * a.xhalf;
       a.xsw = xsw;
       a.xsw_stride = xsw_stride;
+      // the dW1 sum over >= 4 replicas split with helper blocks on idle CUs
+      a.helpers = a.nrep >= 4 ? 1 : 0;
     }
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)

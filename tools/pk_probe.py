@@ -84,7 +84,7 @@ def main() -> int:
                 if a.algo == 4:
                     xall = swizzle_inputs(Xs.reshape(n, nb * 64, 784), 64)
                     tr.runner.set_persist_xall(xall, xall[0].numel())
-                C.mlp_persist_set_probe(True)
+                C.mlp_persist_set_probe(1)
             tr.runner.set_persist(tr.pk_buf, tr.pk_err, 5000.0, xs[0], a.algo)
         torch.cuda.synchronize()
 
@@ -112,7 +112,7 @@ def main() -> int:
             with open(a.stamps, "a") as f:
                 f.write(json.dumps({"mode": ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo], "ranks": n,
                                     "stamps": stamps}) + "\n")
-        C.mlp_persist_set_probe(False)
+        C.mlp_persist_set_probe(0)
         name = ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo]
         print(json.dumps({"mode": name if n > 1 else "none", "ranks": n,
                           "us_per_step": round(dt * 1e6, 2),
