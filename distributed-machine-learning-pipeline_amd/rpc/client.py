@@ -8,10 +8,13 @@ lr 0.01), print ``Epoch N complete: Avg Loss: x, Accuracy: y%`` and
 Two modes:
 
 ``device`` (MI355X fast path): every device server builds its replica on its
-  GPU (ConfigureModel), the coordinator's CommInit bootstraps an RCCL
-  communicator (backend "rccl"), and each epoch is ONE TrainSteps RPC per device:
-  fused HIP fwd/bwd kernels + RCCL gradient all-reduce + SGD, hipGraph-captured.
-  Only loss / accuracy scalars cross the network.
+  GPU (ConfigureModel) and each epoch is ONE TrainSteps RPC per device.  With
+  several GPU devices the coordinator's CommInit (backend "pg") bootstraps a
+  process group on the device servers over a TCP store it hosts (plus RCCL when
+  every device owns a distinct GPU), so the devices run the framework's fastest
+  self-tested data-parallel step: the persistent step with its in-launch xGMI
+  exchange (pkx / pkg / pk), the fused exchanges, or RCCL.  Only loss /
+  accuracy scalars cross the network.
 
 ``rpc`` (the reference's pipeline, made correct): per step, each device gets
   its own batch by Memcpy, computes gradients on the device (RunForward /
@@ -79,13 +82,17 @@ class TrainingClient:
 
     # ------------------------------------------------------------ device mode --
     def train_device_mode(self, epochs: int, samples_per_rank: int, graph_steps: int = 50,
-                          sync: str = "rccl", eval_samples: int = 10000) -> dict:
+                          sync: str = "", eval_samples: int = 10000, backend: str = "auto") -> dict:
         n = len(self.devs)
-        # GPU device servers sum gradients over RCCL; host (CPU) device servers
-        # over the device-driven gRPC ring (DeviceAllReduce's transfers)
-        backends = {s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata.backend
-                    for s in self.devs}
-        self.comm_init("rccl" if n > 1 and backends == {"hip"} else "rpc")
+        # GPU device servers: a process group (backend "pg") and the framework's
+        # data-parallel choice (sync "" = the server's default, "auto" there);
+        # host (CPU) device servers: the device-driven gRPC ring (DeviceAllReduce's
+        # transfers), or a gloo group with backend="pg"
+        if backend == "auto":
+            backends = {s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata.backend
+                        for s in self.devs}
+            backend = "pg" if n > 1 and backends == {"hip"} else "rpc"
+        self.comm_init(backend)
 
         def cfg(i, s):
             return s.ConfigureModel(pb.ConfigureModelRequest(

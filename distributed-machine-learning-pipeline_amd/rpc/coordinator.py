@@ -66,6 +66,8 @@ class Communicator:
     pending: List[object] = field(default_factory=list)
     lock: threading.Lock = field(default_factory=threading.Lock)
     finalized: bool = False
+    store: object = None        # backend "pg": the TCP store the devices' process group meets on
+    data_backend: str = "rpc"   # what the devices' CommSetup reported ("rccl" when RCCL is up)
 
 
 class CollectiveError(RuntimeError):
@@ -75,7 +77,10 @@ class CollectiveError(RuntimeError):
 class GPUCoordinatorServicer:
     def __init__(self, health_interval: float = 5.0, health_timeout: float = 2.0,
                  connect_timeout: float = 3.0, rpc_timeout: float = 120.0,
-                 sleep: Callable[[float], None] = time.sleep, max_parallel: int = 64):
+                 sleep: Callable[[float], None] = time.sleep, max_parallel: int = 64,
+                 store_host: str = "127.0.0.1"):
+        # host the "pg" communicators' TCP stores bind to (the devices connect to it)
+        self.store_host = store_host
         self._mu = threading.Lock()
         self._next_id = 0
         self.comms: Dict[int, Communicator] = {}
@@ -133,7 +138,7 @@ class GPUCoordinatorServicer:
             comm.error = err
             devices = list(comm.devices)
         log.warning("communicator %d FAILED: %s", comm.id, err)
-        if abort_devices and comm.backend == "rccl":
+        if abort_devices and (comm.backend == "rccl" or comm.data_backend == "rccl"):
             for d in devices:
                 self._pool.submit(self._safe_abort, d, comm.id, err)
 
@@ -165,7 +170,7 @@ class GPUCoordinatorServicer:
                 d.channel.close()
             context.abort(grpc.StatusCode.INTERNAL, "CommInit failed: " + "; ".join(errors))
         backend = request.backend or "rpc"
-        if backend not in ("rpc", "rccl"):
+        if backend not in ("rpc", "rccl", "pg"):
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown backend {backend!r}")
         with self._mu:
             cid = self._next_id
@@ -188,15 +193,30 @@ class GPUCoordinatorServicer:
             return
         peers = [d.address for d in comm.devices]
         uid = b""
+        store_addr = ""
         if comm.backend == "rccl":
             uid = comm.devices[0].stub.GetCommUniqueId(
                 pb.GetCommUniqueIdRequest(commId=comm.id), timeout=self.rpc_timeout).uniqueId
-        # RCCL init is collective: every rank must enter it concurrently.
-        self._parallel([
+        elif comm.backend == "pg" and n > 1:
+            # the devices' process group meets on a TCP store this coordinator
+            # hosts (control plane only: IPC handles, self-test all-reduces,
+            # agreement on the sync mode); the data plane is xGMI / RCCL
+            import datetime
+
+            import torch.distributed as dist
+
+            comm.store = dist.TCPStore(self.store_host, 0, is_master=True, wait_for_workers=False,
+                                       timeout=datetime.timedelta(seconds=self.rpc_timeout))
+            store_addr = f"{self.store_host}:{comm.store.port}"
+        # RCCL init / process-group rendezvous are collective: every rank must
+        # enter them concurrently.
+        rs = self._parallel([
             (lambda d=d: d.stub.CommSetup(pb.CommSetupRequest(
-                commId=comm.id, uniqueId=uid, rank=d.rank, nranks=n, peerAddresses=peers),
-                timeout=self.rpc_timeout))
+                commId=comm.id, uniqueId=uid, rank=d.rank, nranks=n, peerAddresses=peers,
+                storeAddress=store_addr), timeout=self.rpc_timeout))
             for d in comm.devices])
+        if all(r is not None and "rccl" in r.backend for r in rs):
+            comm.data_backend = "rccl"
 
     # -------------------------------------------------------- status / lifecycle --
     def GetCommStatus(self, request, context):
@@ -209,12 +229,18 @@ class GPUCoordinatorServicer:
             c = self.comms.pop(request.commId, None)
         if c is None:
             context.abort(grpc.StatusCode.NOT_FOUND, f"communicator {request.commId} not found")
-        for d in c.devices:
+        # a process group's teardown is collective: every device leaves together
+        tmo = self.rpc_timeout if c.backend == "pg" else self.health_timeout
+        futs = [self._pool.submit(d.stub.CommTeardown, pb.CommTeardownRequest(commId=c.id), timeout=tmo)
+                for d in c.devices]
+        for f in futs:
             try:
-                d.stub.CommTeardown(pb.CommTeardownRequest(commId=c.id), timeout=self.health_timeout)
+                f.result()
             except Exception:
                 pass
+        for d in c.devices:
             d.channel.close()
+        c.store = None
         return pb.CommDestroyResponse(success=True)
 
     def CommFinalize(self, request, context):
@@ -284,7 +310,7 @@ class GPUCoordinatorServicer:
 
     def _run_allreduce(self, c: Communicator, op) -> bool:
         try:
-            if c.backend == "rccl":
+            if c.backend == "rccl" or c.data_backend == "rccl":
                 self._allreduce_rccl(c, op)
             elif op.algo == "coordinator-ring":
                 self._allreduce_rpc_ring(c, op)

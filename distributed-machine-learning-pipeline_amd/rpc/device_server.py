@@ -34,6 +34,7 @@ class GPUDeviceServicer:
         self.name = name or f"device-{device.device_id}"
         self.comms: Dict[int, object] = {}      # commId -> native RcclComm
         self.comm_meta: Dict[int, dict] = {}    # commId -> {"rank", "nranks", "peers"}
+        self.pg_comm: Optional[int] = None      # commId whose process group this process joined
         self._aborted_comms: set = set()        # Abort is sticky for its communicator
         self._peer_stubs: Dict[str, GPUDeviceStub] = {}
         self._lock = threading.Lock()
@@ -241,8 +242,52 @@ class GPUDeviceServicer:
                 context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
             self.comms[cid] = comm
             backend = "rccl"
+        if request.storeAddress:
+            backend = self._join_process_group(cid, request, context)
         self.comm_meta[cid] = meta
         return pb.CommSetupResponse(success=True, backend=backend)
+
+    def _join_process_group(self, cid: int, request, context) -> str:
+        """CommInit backend "pg": join a torch.distributed process group (gloo:
+        control-plane collectives only) on the coordinator's TCP store, then
+        -- when every rank owns a distinct GPU -- an RCCL communicator for the
+        gradient all-reduce candidates.  ConfigureModel can then build the
+        framework's data-parallel trainer (fused xGMI exchanges / persistent
+        steps, self-tested and timed) exactly as a torchrun job would.
+        Collective: the coordinator calls every device at once."""
+        import datetime
+        import socket
+
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                          f"this device server already belongs to process group of comm {self.pg_comm}")
+        host, port = request.storeAddress.rsplit(":", 1)
+        tmo = datetime.timedelta(seconds=120)
+        try:
+            store = dist.TCPStore(host, int(port), request.nranks, is_master=False, timeout=tmo)
+            dist.init_process_group("gloo", store=store, rank=request.rank, world_size=request.nranks,
+                                    timeout=tmo)
+        except Exception as e:
+            context.abort(grpc.StatusCode.INTERNAL, f"process group rendezvous failed: {e}")
+        self.pg_comm = cid
+        if self.dev.backend != "hip":
+            return "pg"
+        from ..parallel.dist import DistContext, make_native_comm
+
+        ctx = DistContext(rank=request.rank, world_size=request.nranks, device=self._torch_device(),
+                          backend="gloo")
+        props = torch.cuda.get_device_properties(self.dev.gpu)
+        ident = f"{socket.gethostname()}/{getattr(props, 'uuid', '')}/{self.dev.gpu}".encode()
+        gpus = ctx.all_gather_bytes(f"hipdsml/pg{cid}/gpu", ident)
+        if len(set(gpus)) < request.nranks:
+            return "pg"  # ranks share a GPU: RCCL refuses; exchanges + gloo fallback only
+        try:
+            self.comms[cid] = make_native_comm(ctx)
+        except Exception as e:
+            context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
+        return "rccl+pg"
 
     @staticmethod
     def _ring_sid(cid: int, seq: int, step: int, src: int) -> int:
@@ -425,6 +470,18 @@ class GPUDeviceServicer:
     def CommTeardown(self, request, context):
         self.comms.pop(request.commId, None)
         self.comm_meta.pop(request.commId, None)
+        if request.commId == self.pg_comm:
+            import torch.distributed as dist
+
+            if self.trainer is not None and getattr(self.trainer, "ctx", None) is not None \
+                    and self.trainer.ctx.is_distributed:
+                self.trainer = None  # its exchanges and self-tests belong to this group
+            torch.cuda.synchronize() if self.dev.backend == "hip" else None
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+            self.pg_comm = None
         return pb.CommTeardownResponse(success=True)
 
     # -------------------------------------------------------------- training --
@@ -459,10 +516,19 @@ class GPUDeviceServicer:
             import numpy as np
 
             params = layout.from_reference(np.frombuffer(raw, dtype=np.float32))
-        ctx = DistContext(rank=rank, world_size=world, device=self._torch_device())
+        pg = world > 1 and request.commId == self.pg_comm
+        ctx = DistContext(rank=rank, world_size=world, device=self._torch_device(),
+                          backend="gloo" if pg else "none")
         comm = self.comms.get(request.commId) if world > 1 else None
         host_ar = None
-        if world > 1 and comm is None:
+        if pg:
+            import torch.distributed as dist
+
+            if dist.get_world_size() != world or dist.get_rank() != rank:
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION,
+                              f"comm {request.commId}'s process group is rank {dist.get_rank()} of "
+                              f"{dist.get_world_size()}, not {rank} of {world}")
+        elif world > 1 and comm is None:
             if self.dev.backend == "hip":
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION,
                               "data-parallel TrainSteps needs an RCCL comm (CommInit backend=rccl)")
@@ -476,16 +542,24 @@ class GPUDeviceServicer:
             except ValueError as e:  # the gradient does not fit the ring scratch window
                 context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         try:
+            # a process group runs the framework's own data-parallel choice
+            # (sync "auto": every fused exchange self-tested and timed, RCCL
+            # or a gloo all-reduce as the fallback)
+            sync = request.sync or ("auto" if pg else "rccl")
+            if pg and self.dev.backend != "hip":
+                sync = "rccl"  # host replicas: the torch step's all-reduce over the group
             self.trainer = MlpTrainer(spec, ds, batch=batch, lr=request.lr or 0.01, ctx=ctx,
                                       seed=request.seed, momentum=request.momentum,
                                       graph_steps=request.graphSteps, params=params,
-                                      external_comm=comm, sync=request.sync or "rccl",
-                                      grad_allreduce=host_ar)
+                                      external_comm=comm, sync=sync, grad_allreduce=host_ar,
+                                      auto_fallback="rccl" if (comm is not None or not pg) else "torch")
         except (ValueError, RuntimeError) as e:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         return pb.ConfigureModelResponse(success=True, numParams=spec.num_params,
                                          batchesPerEpoch=self.trainer.nbatches,
-                                         paramBytes=layout.nparams * 4)
+                                         paramBytes=layout.nparams * 4,
+                                         sync=self.trainer.sync_active,
+                                         syncTimesJson=json.dumps(self.trainer.sync_times or {}))
 
     def _host_grad_allreduce(self, cid: int, n: int, nbytes: int):
         """Gradient sum for host replicas trained by TrainSteps: each step's flat

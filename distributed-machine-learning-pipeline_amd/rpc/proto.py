@@ -12,7 +12,12 @@ numbers and NEW methods:
 * ``AllReduceRingRequest.dtype`` (5), ``algo`` (6): dtype-aware reduction
   instead of the reference's byte-wise uint8 add.
 * ``CommInitRequest.backend`` (3): ``"rpc"`` moves data device->device over
-  gRPC streams; ``"rccl"`` bootstraps an RCCL communicator on the device GPUs.
+  gRPC streams; ``"rccl"`` bootstraps an RCCL communicator on the device GPUs;
+  ``"pg"`` bootstraps a torch.distributed process group on the device servers
+  over a TCP store the coordinator hosts (``CommSetupRequest.storeAddress``, 6),
+  plus an RCCL communicator when every device owns a distinct GPU: data-parallel
+  ``TrainSteps`` then runs the fused xGMI / persistent data-parallel steps
+  (every candidate self-tested and timed, the fastest kept).
 * ``BeginSendRequest.dstAddress`` (4), ``DataChunk.srcRank`` (3): the device
   pushes the data itself (the proto comment's intended semantics,
   ``gpu_sim.proto:32-34``) instead of the coordinator relaying it.
@@ -120,7 +125,8 @@ MESSAGES: M = {
     "GetCommUniqueIdRequest": [("commId", 1, "uint64")],
     "GetCommUniqueIdResponse": [("uniqueId", 1, "bytes")],
     "CommSetupRequest": [("commId", 1, "uint64"), ("uniqueId", 2, "bytes"), ("rank", 3, "uint32"),
-                         ("nranks", 4, "uint32"), ("peerAddresses", 5, "string", "repeated")],
+                         ("nranks", 4, "uint32"), ("peerAddresses", 5, "string", "repeated"),
+                         ("storeAddress", 6, "string")],
     "CommSetupResponse": [("success", 1, "bool"), ("backend", 2, "string")],
     "DeviceAllReduceRequest": [("commId", 1, "uint64"), ("addr", 2, "uint64"), ("count", 3, "uint64"),
                                ("dtype", 4, ".DataType"), ("op", 5, ".ReduceOp"),
@@ -139,7 +145,8 @@ MESSAGES: M = {
                               ("graphSteps", 12, "uint32"), ("sync", 13, "string"),
                               ("dataSeed", 14, "uint64")],
     "ConfigureModelResponse": [("success", 1, "bool"), ("numParams", 2, "uint64"),
-                               ("batchesPerEpoch", 3, "uint64"), ("paramBytes", 4, "uint64")],
+                               ("batchesPerEpoch", 3, "uint64"), ("paramBytes", 4, "uint64"),
+                               ("sync", 5, "string"), ("syncTimesJson", 6, "string")],
     "TrainStepsRequest": [("steps", 1, "uint64")],
     "TrainStepsResponse": [("success", 1, "bool"), ("lossSum", 2, "double"), ("correct", 3, "double"),
                            ("count", 4, "double"), ("elapsedUs", 5, "double"),
