@@ -6,6 +6,12 @@
              vs AllReduceRing(1 MiB), through the gpu_sim API.  Reported both
              "as published" (ring on count = dataSize/4 bytes, uint8, like the
              reference) and apples-to-apples (ring on the full 1 MiB, fp32).
+             The ring is device-driven over ONE long-lived stream per
+             neighbour pair (GPUDevice.RingChannel: one message per ring step);
+             the round-1 form with a StreamSend RPC per segment is reported
+             too.  GPU devices in separate processes also join a "pg"
+             communicator, and AllReduceRing(algo "xgmi") sums the same 1 MiB
+             over xGMI peer memory in one launch per device.
 ``device`` — one process per GPU (torchrun): the native ring (ncclSend/ncclRecv
              reduce-scatter + all-gather with HIP reduce kernels) and RCCL's own
              all-reduce on device buffers, latency (us) and bus bandwidth
@@ -64,7 +70,9 @@ def bench_rpc(a) -> None:
         procs, addrs, caddr = _spawn_cluster(a)
     coord = GPUCoordinatorStub(connect(caddr, timeout=30))
     try:
-        init = coord.CommInit(pb.CommInitRequest(numDevices=a.n, device_addresses=addrs))
+        pg = a.backend == "hip" and not a.inproc and a.n > 1
+        init = coord.CommInit(pb.CommInitRequest(numDevices=a.n, device_addresses=addrs,
+                                                 backend="pg" if pg else ""))
         cid = init.commId
         backend = init.devices[0].backend
         size = a.size
@@ -78,12 +86,17 @@ def bench_rpc(a) -> None:
                 hostSrcData=rng.standard_normal(size // 4).astype(np.float32).tobytes(),
                 dstDeviceId=d.deviceId, dstMemAddr=pb.MemAddr(value=0x1000))))
         res = {}
-        for label, count, dt in (("ring_as_published", size // 4, DT_UINT8), ("ring_full_fp32", size, DT_FLOAT32)):
+        runs = [("ring_as_published", size // 4, DT_UINT8, ""), ("ring_full_fp32", size, DT_FLOAT32, ""),
+                ("ring_per_segment_rpc_fp32", size, DT_FLOAT32, "device-ring")]
+        if pg:
+            runs.append(("xgmi_fp32", size, DT_FLOAT32, "xgmi"))
+        for label, count, dt, algo in runs:
             ts = []
-            for _ in range(a.reps):
+            for k in range(a.reps + 1):
                 t0 = time.perf_counter()
-                coord.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=count, dtype=dt))
-                ts.append((time.perf_counter() - t0) * 1e3)
+                coord.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=count, dtype=dt, algo=algo))
+                if k:  # the first call opens the streams / exchange buffers
+                    ts.append((time.perf_counter() - t0) * 1e3)
             res[label] = ts
         out = {"bench": "allreduce_rpc", "n_devices": a.n, "backend": backend,
                "processes": "in-process" if a.inproc else "one per server",
@@ -91,6 +104,10 @@ def bench_rpc(a) -> None:
                "naive_ms_median": round(statistics.median(naive), 3),
                "ring_as_published_ms_median": round(statistics.median(res["ring_as_published"]), 3),
                "ring_full_fp32_ms_median": round(statistics.median(res["ring_full_fp32"]), 3),
+               "ring_per_segment_rpc_fp32_ms_median": round(statistics.median(res["ring_per_segment_rpc_fp32"]), 3),
+               "xgmi_fp32_ms_median": (round(statistics.median(res["xgmi_fp32"]), 3) if "xgmi_fp32" in res
+                                       else None),
+               "comm_backend": "pg" if pg else "rpc",
                "reference": {"naive_ms": 83, "ring_ms": 8}}
         print(json.dumps(out), flush=True)
     finally:

@@ -314,7 +314,13 @@ class GPUCoordinatorServicer:
                 self._allreduce_rccl(c, op)
             elif op.algo == "coordinator-ring":
                 self._allreduce_rpc_ring(c, op)
-            else:  # "device-ring" (default): devices drive the ring themselves
+            elif op.algo == "xgmi":  # "pg" comms of GPU devices: one launch over peer memory
+                self._parallel([
+                    (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
+                        commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype,
+                        op=op.op, algo="xgmi"), timeout=self.rpc_timeout))
+                    for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
+            else:  # "stream-ring" (default) / "device-ring": devices drive the ring themselves
                 self._allreduce_device_ring(c, op)
         except Exception as e:
             self._fail(c, f"{type(e).__name__}: {e}")
@@ -343,7 +349,8 @@ class GPUCoordinatorServicer:
         self._parallel([
             (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                 commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
-                algo="rpc-ring", chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
+                algo="rpc-ring" if op.algo == "device-ring" else "stream-ring",
+                chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
             for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
 
     def _wait_stream(self, d: DeviceInfo, sid: int) -> None:

@@ -35,6 +35,12 @@ class GPUDeviceServicer:
         self.comms: Dict[int, object] = {}      # commId -> native RcclComm
         self.comm_meta: Dict[int, dict] = {}    # commId -> {"rank", "nranks", "peers"}
         self.pg_comm: Optional[int] = None      # commId whose process group this process joined
+        # RingChannel: per commId, the outgoing queue to the successor (one
+        # long-lived client stream) and the inbox of the predecessor's messages
+        self._ring_out: Dict[int, "queue.Queue"] = {}
+        self._ring_in: Dict[int, dict] = {}
+        self._ring_cv = threading.Condition()
+        self._xgmi_ar: Dict[int, object] = {}   # commId -> XgmiAllReduce (pg comms on GPUs)
         self._aborted_comms: set = set()        # Abort is sticky for its communicator
         self._peer_stubs: Dict[str, GPUDeviceStub] = {}
         self._lock = threading.Lock()
@@ -50,7 +56,8 @@ class GPUDeviceServicer:
     # ------------------------------------------------------ fault injection --
     def arm_fault(self, after_rpcs: int, mode: str = "stop") -> None:
         """BASELINE config 5 hook: die on the `after_rpcs`-th data-plane RPC
-        (BeginSend / BeginReceive / StreamSend / Memcpy / Reduce / DeviceAllReduce).
+        (BeginSend / BeginReceive / StreamSend / Memcpy / Reduce / DeviceAllReduce,
+        and every RingChannel message).
         mode "stop": stop the gRPC server (in-process clusters, like the
         reference test's ``grpcServer.Stop()``, gpu_coordinator_server_test.go:415);
         "exit": terminate the process abruptly (a crashed device server)."""
@@ -313,6 +320,106 @@ class GPUDeviceServicer:
             if time.monotonic() > t_end:
                 return STATUS_FAILED
 
+    # ---- RingChannel: one stream per neighbour pair, one message per ring step --
+    def RingChannel(self, request_iterator, context):
+        """Receiving end of a neighbour's long-lived ring stream: every message
+        (comm, call sequence, step) lands in this comm's inbox until the ring
+        step that needs it takes it."""
+        for msg in request_iterator:
+            self._tick(context)  # every ring step counts as a data-plane RPC (fault injection)
+            with self._ring_cv:
+                self._ring_in.setdefault(msg.commId, {})[(msg.seq, msg.step)] = msg.data
+                self._ring_cv.notify_all()
+            self.counters["stream_bytes_in"] += len(msg.data)
+        return pb.RingAck(success=True)
+
+    def _ring_send(self, cid: int, nxt: str, msg) -> None:
+        """Queue `msg` on this comm's stream to the successor, opening the
+        stream (a background client call fed by the queue) on first use."""
+        import queue
+
+        q = self._ring_out.get(cid)
+        if q is None:
+            q = queue.Queue()
+            self._ring_out[cid] = q
+
+            def gen():
+                while True:
+                    m = q.get()
+                    if m is None:
+                        return
+                    yield m
+
+            def run():
+                try:
+                    self._peer(nxt).RingChannel(gen(), timeout=24 * 3600)
+                except Exception as e:  # peer gone: the waiting step times out / aborts
+                    log.warning("ring channel of comm %d to %s closed: %s", cid, nxt, e)
+
+            threading.Thread(target=run, daemon=True).start()
+        q.put(msg)
+
+    def _ring_recv(self, cid: int, seq: int, step: int, timeout: float = 120.0) -> bytes:
+        t_end = time.monotonic() + timeout
+        with self._ring_cv:
+            while True:
+                box = self._ring_in.get(cid, {})
+                if (seq, step) in box:
+                    return box.pop((seq, step))
+                if cid in self._aborted_comms:
+                    raise RuntimeError(f"communicator {cid} aborted")
+                left = t_end - time.monotonic()
+                if left <= 0:
+                    raise RuntimeError(f"ring step {step} of call {seq}: nothing from the predecessor")
+                self._ring_cv.wait(min(left, 0.05))
+
+    def _ring_close(self, cid: int) -> None:
+        q = self._ring_out.pop(cid, None)
+        if q is not None:
+            q.put(None)
+        with self._ring_cv:
+            self._ring_in.pop(cid, None)
+
+    def _stream_ring(self, cid: int, addr: int, count: int, dtype: int, op: int) -> None:
+        """Device-driven ring all-reduce over the neighbour streams: 2(n-1)
+        steps, each ONE message on the long-lived stream to the successor (no
+        per-step stream setup, no per-step thread), the predecessor's segment
+        reduced in place on the device.  Same segments and order as _rpc_ring."""
+        meta = self.comm_meta[cid]
+        r, n, peers = meta["rank"], meta["nranks"], meta["peers"]
+        seq = meta.setdefault("seq", 0)
+        meta["seq"] = seq + 1
+        es = DT_SIZE[dtype]
+        elems = count // es
+        al = 16 // es
+        seg = (-(-elems // n) + al - 1) // al * al
+        off = [min(i * seg, elems) * es for i in range(n + 1)]
+        nxt = peers[(r + 1) % n]
+        scratch = self.dev.scratch_addr
+        for step in range(2 * (n - 1)):
+            if cid in self._aborted_comms:
+                raise RuntimeError(f"communicator {cid} aborted")
+            s_ = step if step < n - 1 else step - (n - 1)
+            if step < n - 1:  # reduce-scatter
+                si, ri = (r - s_) % n, (r - s_ - 1) % n
+            else:             # all-gather, straight into place
+                si, ri = (r + 1 - s_) % n, (r - s_) % n
+            sl, rl = off[si + 1] - off[si], off[ri + 1] - off[ri]
+            self._ring_send(cid, nxt, pb.RingChunk(commId=cid, seq=seq, step=step, srcRank=r,
+                                                   data=self.dev.read(addr + off[si], sl, internal=True)
+                                                   if sl else b""))
+            self.counters["stream_bytes_out"] += sl
+            data = self._ring_recv(cid, seq, step)
+            if len(data) != rl:
+                raise RuntimeError(f"ring step {step}: {len(data)} B from the predecessor, expected {rl}")
+            if rl:
+                if step < n - 1:
+                    self.dev.write(scratch, data, internal=True, record=False)
+                    self.dev.reduce(addr + off[ri], scratch, rl, dtype, op)
+                else:
+                    self.dev.write(addr + off[ri], data, internal=True, record=False)
+        self.dev.synchronize()
+
     def _rpc_ring(self, cid: int, addr: int, count: int, dtype: int, op: int, chunk: int) -> None:
         """Device-driven ring all-reduce over gRPC streams (CPU / no-RCCL path).
 
@@ -396,8 +503,49 @@ class GPUDeviceServicer:
             step += 1
         del chunk
 
+    def _xgmi_allreduce(self, request, context) -> float:
+        """fp32 sum over xGMI peer memory (parallel/xchg.py XgmiAllReduce,
+        two-shot: reduce-scatter + all-gather in one launch) between the GPU
+        device servers of a "pg" communicator: the exchange buffers' IPC handles
+        travel through the process group's store.  Collective (the coordinator
+        calls every device at once); returns the device time in us."""
+        from ..parallel.dist import DistContext
+        from ..parallel.xchg import XgmiAllReduce
+
+        cid = request.commId
+        if cid != self.pg_comm or self.dev.backend != "hip":
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, "algo 'xgmi' needs GPU devices in a 'pg' comm")
+        if request.dtype != DT_FLOAT32 or request.op != SUM or request.count % 16:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, "algo 'xgmi' sums fp32 buffers of 16-B multiples")
+        n = request.count // 4
+        ar = self._xgmi_ar.get(cid)
+        if ar is None or ar.max_floats < n:
+            meta = self.comm_meta[cid]
+            ctx = DistContext(rank=meta["rank"], world_size=meta["nranks"], device=self._torch_device(),
+                              backend="gloo")
+            with torch.cuda.device(self.dev.gpu):
+                ar = XgmiAllReduce(ctx, max(n, 1 << 18), algo="twoshot")
+            self._xgmi_ar[cid] = ar
+        t = self.dev.tensor(request.addr, request.count, torch.float32, internal=False)
+        torch.cuda.synchronize(self.dev.gpu)
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.dev.gpu):
+            for _ in range(max(1, request.repeat)):
+                ar(t)
+            torch.cuda.synchronize(self.dev.gpu)
+        us = (time.perf_counter() - t0) * 1e6 / max(1, request.repeat)
+        ar.check()
+        return us
+
     def DeviceAllReduce(self, request, context):
         self._tick(context)
+        if request.algo == "xgmi":
+            try:
+                us = self._xgmi_allreduce(request, context)
+            except RuntimeError as e:
+                context.abort(grpc.StatusCode.INTERNAL, f"xGMI all-reduce failed: {e}")
+            self.counters["allreduces"] += max(1, request.repeat)
+            return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
         comm = self.comms.get(request.commId)
         if comm is None and request.commId in self.comm_meta:
             es = DT_SIZE.get(request.dtype, 0)
@@ -410,8 +558,12 @@ class GPUDeviceServicer:
             t0 = time.perf_counter()
             try:
                 for _ in range(max(1, request.repeat)):
-                    self._rpc_ring(request.commId, request.addr, request.count, request.dtype,
-                                   request.op, request.chunkBytes)
+                    if request.algo == "stream-ring":
+                        self._stream_ring(request.commId, request.addr, request.count, request.dtype,
+                                          request.op)
+                    else:
+                        self._rpc_ring(request.commId, request.addr, request.count, request.dtype,
+                                       request.op, request.chunkBytes)
             except Exception as e:
                 context.abort(grpc.StatusCode.INTERNAL, f"device ring failed: {e}")
             self.counters["allreduces"] += max(1, request.repeat)
@@ -468,6 +620,8 @@ class GPUDeviceServicer:
         return pb.AbortResponse(success=True)
 
     def CommTeardown(self, request, context):
+        self._ring_close(request.commId)
+        self._xgmi_ar.pop(request.commId, None)
         self.comms.pop(request.commId, None)
         self.comm_meta.pop(request.commId, None)
         if request.commId == self.pg_comm:

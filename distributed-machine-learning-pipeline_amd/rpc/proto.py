@@ -70,6 +70,11 @@ MESSAGES: M = {
     "BeginReceiveResponse": [("initiated", 1, "bool")],
     "DataChunk": [("data", 1, "bytes"), ("streamId", 2, "uint64"), ("srcRank", 3, "uint32")],
     "StreamSendResponse": [("success", 1, "bool")],
+    # device-driven ring over ONE long-lived client stream per neighbour pair
+    # (GPUDevice.RingChannel): every ring step of every call is one message
+    "RingChunk": [("commId", 1, "uint64"), ("seq", 2, "uint64"), ("step", 3, "uint32"),
+                  ("srcRank", 4, "uint32"), ("data", 5, "bytes")],
+    "RingAck": [("success", 1, "bool")],
     "GetStreamStatusRequest": [("streamId", 1, ".StreamId")],
     "GetStreamStatusResponse": [("status", 1, ".Status")],
     # -- memcpy ------------------------------------------------------------
@@ -167,6 +172,7 @@ SERVICES = {
         ("BeginSend", "BeginSendRequest", "BeginSendResponse", False),
         ("BeginReceive", "BeginReceiveRequest", "BeginReceiveResponse", False),
         ("StreamSend", "DataChunk", "StreamSendResponse", True),
+        ("RingChannel", "RingChunk", "RingAck", True),
         ("GetStreamStatus", "GetStreamStatusRequest", "GetStreamStatusResponse", False),
         ("Memcpy", "MemcpyRequest", "MemcpyResponse", False),
         ("RunForward", "RunForwardRequest", "RunForwardResponse", False),
