@@ -859,6 +859,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return steps;
   }, py::arg("n"), py::arg("rank"), py::arg("count"), py::arg("align") = 4,
      py::arg("chunk") = 0, py::arg("max_rings") = 0);
+  m.def("ring_pipeline", [](int n, int rank, int64_t count, int64_t align, int64_t chunk,
+                            int max_rings) {
+    py::list out;
+    for (const auto& d : ring_pipeline(ring_schedule(n, rank, count, align, chunk, max_rings)))
+      out.append(py::make_tuple(d.wait_reduce, d.slot, d.slot_free));
+    return out;
+  }, py::arg("n"), py::arg("rank"), py::arg("count"), py::arg("align") = 4,
+     py::arg("chunk") = 0, py::arg("max_rings") = 0,
+     "per group of ring_schedule: (wait_reduce, slot, slot_free) of the two-stream pipelined ring");
   m.def("directed_rings", &directed_rings, py::arg("n"), py::arg("max_rings") = 0);
 
   // ---- xGMI peer exchange (gradient all-reduce fused into K_C) -------------

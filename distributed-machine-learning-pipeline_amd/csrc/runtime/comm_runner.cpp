@@ -80,6 +80,26 @@ RcclComm::~RcclComm() {
   }
   if (tmp_) (void)hipFree(tmp_);
   if (one_) (void)hipFree(one_);
+  for (hipEvent_t e : ev_xfer_) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ev_red_) (void)hipEventDestroy(e);
+  if (fork_) (void)hipEventDestroy(fork_);
+  if (join_) (void)hipEventDestroy(join_);
+  if (red_) (void)hipStreamDestroy(red_);
+}
+
+void RcclComm::ensure_pipe(size_t groups) {
+  if (red_ == nullptr) {
+    DSML_HIP_CHECK(hipStreamCreateWithFlags(&red_, hipStreamNonBlocking));
+    DSML_HIP_CHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    DSML_HIP_CHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
+  }
+  while (ev_red_.size() < groups) {
+    hipEvent_t a, b;
+    DSML_HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    DSML_HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    ev_xfer_.push_back(a);
+    ev_red_.push_back(b);
+  }
 }
 
 void RcclComm::check(ncclResult_t r, const char* what) {
@@ -123,7 +143,7 @@ size_t RcclComm::ring_tmp_bytes(int64_t count, int32_t dtype, int64_t chunk_byte
     for (const auto& x : g)
       if (x.reduce) maxr = std::max(maxr, x.recv_len);
   const size_t slot = std::max<size_t>(((size_t)maxr * es + 255) & ~(size_t)255, 256);
-  return slot * (size_t)R;
+  return slot * (size_t)R * 2;  // double buffered (the pipelined form alternates)
 }
 
 void RcclComm::reserve_ring(int64_t count, int32_t dtype, int64_t chunk_bytes, int max_rings) {
@@ -150,7 +170,7 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
   const auto plan = ring_schedule(n, rank_, count, align, chunk, max_rings);
   const size_t need = ring_tmp_bytes(count, dtype, chunk_bytes, max_rings);
   const int R = (int)directed_rings(n, max_rings).size();
-  const size_t slot = need / (size_t)R;
+  const size_t slot = need / (size_t)(2 * R);
   if (need > tmp_bytes_) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
@@ -162,28 +182,61 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
   uint8_t* b = static_cast<uint8_t*>(buf);
   uint8_t* tmp = static_cast<uint8_t*>(tmp_);
   const ncclDataType_t t = to_nccl(dtype);
-  for (const auto& g : plan) {
+  // Pipelined when the schedule has chunk rounds (ring_plan.h ring_pipeline):
+  // the reduces run on red_, each transfer group waits only for the reduce of
+  // the chunk it sends (and of the scratch slot it receives into), so chunk
+  // c's reduce overlaps chunk c+1's transfer.  One round per step leaves
+  // nothing to overlap: the single-stream order is kept (no event overhead).
+  bool pipe = false;
+  for (const auto& g : plan)
+    if (!g.empty() && g[0].round > 0) pipe = true;
+  const auto deps = pipe ? ring_pipeline(plan) : std::vector<RingDeps>(plan.size());
+  if (pipe) {
+    ensure_pipe(plan.size());
+    DSML_HIP_CHECK(hipEventRecord(fork_, s));
+    DSML_HIP_CHECK(hipStreamWaitEvent(red_, fork_, 0));
+  }
+  for (size_t i = 0; i < plan.size(); ++i) {
+    const auto& g = plan[i];
+    const bool rs = !g.empty() && g[0].reduce;
+    if (pipe) {
+      if (deps[i].wait_reduce >= 0) DSML_HIP_CHECK(hipStreamWaitEvent(s, ev_red_[deps[i].wait_reduce], 0));
+      if (rs && deps[i].slot_free >= 0) DSML_HIP_CHECK(hipStreamWaitEvent(s, ev_red_[deps[i].slot_free], 0));
+    }
+    uint8_t* scr = tmp + slot * (size_t)R * (size_t)deps[i].slot;
     check(ncclGroupStart(), "ncclGroupStart");
     for (const auto& x : g) {
       if (x.send_len > 0)
         check(ncclSend(b + x.send_off * es, x.send_len, t, x.send_peer, comm_, s), "ncclSend");
       if (x.recv_len > 0) {
-        void* dst = x.reduce ? (void*)(tmp + slot * x.ring) : (void*)(b + x.recv_off * es);
+        void* dst = x.reduce ? (void*)(scr + slot * x.ring) : (void*)(b + x.recv_off * es);
         check(ncclRecv(dst, x.recv_len, t, x.recv_peer, comm_, s), "ncclRecv");
       }
     }
     check(ncclGroupEnd(), "ncclGroupEnd");
+    if (!rs) continue;
+    hipStream_t rs_s = s;
+    if (pipe) {
+      DSML_HIP_CHECK(hipEventRecord(ev_xfer_[i], s));
+      DSML_HIP_CHECK(hipStreamWaitEvent(red_, ev_xfer_[i], 0));
+      rs_s = red_;
+    }
     // every ring's received segment of this step reduced by ONE launch
     ReduceSegs m{};
     for (const auto& x : g) {
       if (!x.reduce || x.recv_len <= 0) continue;
       if (m.count == kMaxReduceSegs) {
-        DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, s));
+        DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, rs_s));
         m.count = 0;
       }
-      m.seg[m.count++] = ReduceSeg{b + x.recv_off * es, tmp + slot * x.ring, x.recv_len};
+      m.seg[m.count++] = ReduceSeg{b + x.recv_off * es, scr + slot * x.ring, x.recv_len};
     }
-    if (m.count > 0) DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, s));
+    if (m.count > 0) DSML_HIP_CHECK(reduce_multi_inplace(m, dtype, op, rs_s));
+    if (pipe) DSML_HIP_CHECK(hipEventRecord(ev_red_[i], red_));
+  }
+  if (pipe) {  // every reduce done before the caller's next op on s
+    DSML_HIP_CHECK(hipEventRecord(join_, red_));
+    DSML_HIP_CHECK(hipStreamWaitEvent(s, join_, 0));
   }
 }
 

@@ -26,6 +26,8 @@ struct RingXfer {
   int recv_peer;       // -1: nothing to receive
   int64_t recv_off, recv_len;
   bool reduce;         // reduce-scatter (receive into scratch, then reduce) vs all-gather (in place)
+  int step = 0;        // step within its phase (0 .. n-2)
+  int round = 0;       // chunk round within the step
 };
 
 // Undirected edge-disjoint Hamiltonian cycles of K_n (found by exhaustive
@@ -116,13 +118,63 @@ inline std::vector<std::vector<RingXfer>> ring_schedule(int n, int rank, int64_t
           const int64_t rn = std::max<int64_t>(0, std::min(chunk, r_len[k] - o));
           if (sn == 0 && rn == 0) continue;
           g.push_back(RingXfer{k, sn ? nxt[k] : -1, s_off[k] + o, sn, rn ? prv[k] : -1,
-                               r_off[k] + o, rn, phase == 0});
+                               r_off[k] + o, rn, phase == 0, st, (int)c});
         }
         if (!g.empty()) steps.push_back(std::move(g));
       }
     }
   }
   return steps;
+}
+
+// Pipelined execution of a schedule on two streams: the transfers (one
+// ncclGroup per entry, comm stream) and the reduce-scatter's reduces (one
+// launch per group, reduce stream), so chunk c's reduce overlaps chunk c+1's
+// transfer.  Per group i:
+//   wait_reduce: the group whose REDUCE must have finished before i's sends
+//     (a reduce-scatter step sends what the previous step reduced; the first
+//     all-gather step sends what the last reduce-scatter step reduced), -1 none;
+//   slot: scratch slot (0 / 1, double buffered per ring) i's receives land in;
+//   slot_free: the group whose reduce last read that slot, -1 none.
+// Reduces run in issue order on their stream, so waiting for a later group's
+// reduce also covers every earlier one.  Pure index arithmetic: simulated on
+// the CPU against adversarial stream timings (tests/test_ring_plan.py).
+struct RingDeps {
+  int wait_reduce = -1;
+  int slot = 0;
+  int slot_free = -1;
+};
+inline std::vector<RingDeps> ring_pipeline(const std::vector<std::vector<RingXfer>>& plan) {
+  const int G = (int)plan.size();
+  std::vector<RingDeps> out(G);
+  // (phase, step) -> group index of each round
+  std::vector<std::vector<int>> rs, ag;
+  for (int i = 0; i < G; ++i) {
+    if (plan[i].empty()) continue;
+    const RingXfer& x = plan[i][0];
+    auto& tab = x.reduce ? rs : ag;
+    if ((int)tab.size() <= x.step) tab.resize(x.step + 1);
+    tab[x.step].push_back(i);
+  }
+  auto pick = [](const std::vector<int>& rounds, int c) {
+    return rounds.empty() ? -1 : rounds[std::min<int>(c, (int)rounds.size() - 1)];
+  };
+  int last[2] = {-1, -1};
+  int nred = 0;
+  for (int i = 0; i < G; ++i) {
+    if (plan[i].empty()) continue;
+    const RingXfer& x = plan[i][0];
+    if (x.reduce) {
+      if (x.step > 0) out[i].wait_reduce = pick(rs[x.step - 1], x.round);
+      out[i].slot = nred & 1;
+      out[i].slot_free = last[nred & 1];
+      last[nred & 1] = i;
+      ++nred;
+    } else if (x.step == 0 && !rs.empty()) {
+      out[i].wait_reduce = pick(rs.back(), x.round);
+    }
+  }
+  return out;
 }
 
 }  // namespace dsml

@@ -189,6 +189,13 @@ class RcclComm {
   void* tmp_ = nullptr;
   size_t tmp_bytes_ = 0;
   void* one_ = nullptr;  // scratch for barrier
+  // Pipelined ring (ring_plan.h ring_pipeline): the reduce-scatter's reduces run
+  // on their own stream, ordered by events, so chunk c's reduce overlaps chunk
+  // c+1's transfer; scratch is double buffered per ring.
+  void ensure_pipe(size_t groups);
+  hipStream_t red_ = nullptr;
+  hipEvent_t fork_ = nullptr, join_ = nullptr;
+  std::vector<hipEvent_t> ev_xfer_, ev_red_;
 };
 
 // ---------------------------------------------------------------------------

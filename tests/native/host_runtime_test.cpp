@@ -36,7 +36,16 @@ static int g_fail = 0;
 // (src, dst) pair (how ncclSend/ncclRecv pair up).  No progress = deadlock.
 static void ring_sim(int n, int64_t count, int64_t align, int64_t chunk, int max_rings) {
   std::vector<std::vector<std::vector<RingXfer>>> plans(n);
-  for (int r = 0; r < n; ++r) plans[r] = ring_schedule(n, r, count, align, chunk, max_rings);
+  for (int r = 0; r < n; ++r) {
+    plans[r] = ring_schedule(n, r, count, align, chunk, max_rings);
+    // the pipelined form's dependencies only point backwards (ring_pipeline)
+    const auto deps = ring_pipeline(plans[r]);
+    CHECK(deps.size() == plans[r].size());
+    for (size_t i = 0; i < deps.size(); ++i) {
+      CHECK(deps[i].wait_reduce < (int)i && deps[i].slot_free < (int)i);
+      CHECK(deps[i].slot == 0 || deps[i].slot == 1);
+    }
+  }
   std::vector<std::vector<double>> buf(n, std::vector<double>(count > 0 ? count : 0));
   std::vector<double> want(count > 0 ? count : 0, 0.0);
   for (int r = 0; r < n; ++r)
