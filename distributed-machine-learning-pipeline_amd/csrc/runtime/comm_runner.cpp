@@ -8,6 +8,7 @@
 // process owns one GPU and a real ring moves segments GPU->GPU over xGMI.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -187,9 +188,17 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
   // the chunk it sends (and of the scratch slot it receives into), so chunk
   // c's reduce overlaps chunk c+1's transfer.  One round per step leaves
   // nothing to overlap: the single-stream order is kept (no event overhead).
+  // Opt-in (HIPDSML_RING_PIPELINE=1) until a multi-GPU run has validated RCCL
+  // p2p groups waiting on another stream's events: the schedule's dependencies
+  // are verified by simulation only (tests/test_ring_plan.py), and a hang here
+  // would stall every rank's init (the chunk sweep runs this ring).
+  static const bool kPipeEnv = [] {
+    const char* e = std::getenv("HIPDSML_RING_PIPELINE");
+    return e != nullptr && e[0] == '1';
+  }();
   bool pipe = false;
   for (const auto& g : plan)
-    if (!g.empty() && g[0].round > 0) pipe = true;
+    if (kPipeEnv && !g.empty() && g[0].round > 0) pipe = true;
   const auto deps = pipe ? ring_pipeline(plan) : std::vector<RingDeps>(plan.size());
   if (pipe) {
     ensure_pipe(plan.size());
