@@ -53,6 +53,12 @@ def decode(v, spec) -> dict:
             "l1_z1_stored_to_step_end_us": med([(st[0][s][3] - st[0][s][4]) / 100.0 for s in range(8)]),
             "z1_stored_to_chain_seen_us": med([(st[1][s + 1][1] - st[0][s][4]) / 100.0 for s in range(7)]),
         }
+        if all(st[0][s][5] for s in range(8)):
+            # single replica: the correction block of column 0 (chains' XCD)
+            out["gram"]["chain_dz1_publish_to_cb_seen_us"] = med(
+                [(st[0][s][5] - st[1][s][4]) / 100.0 for s in range(8)])
+            out["gram"]["cb_dz1_seen_to_z1_stored_us"] = med(
+                [(st[0][s][4] - st[0][s][5]) / 100.0 for s in range(8)])
     out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
     return out
 
