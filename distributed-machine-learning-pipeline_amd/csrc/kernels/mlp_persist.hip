@@ -84,16 +84,12 @@ constexpr int kNPart = kNL1;                            // partial slots per par
 // ~16 MFMAs instead of a quarter of the update.  All upper blocks (chains +
 // tiles) sit at blockIdx 8 k; layer-1 block (gn, gk) at blockIdx 8 gn + gk + 1.
 template <int NL> struct GTile { static constexpr int kN = NL == 3 ? 16 : 8; };
-// cb: the single replica's 8 correction blocks also sit at blockIdx 8 k (XCD 0)
-template <int NL> constexpr int pk_grid(bool dp, bool cb = false) {
-  return dp ? kNBlk : 8 * (kNCH + GTile<NL>::kN + (cb ? kGN : 0));
-}
+template <int NL> constexpr int pk_grid(bool dp) { return dp ? kNBlk : 8 * (kNCH + GTile<NL>::kN); }
 // Whether blockIdx b does work in the Gram-form grid (the rest exit); `helpers`:
 // pkx at >= 4 replicas also runs a dW1 helper per layer-1 block at
 // blockIdx 8 (8 + gn) + gk + 1, on its owner's XCD.
-template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, bool helpers = false, bool cb = false) {
-  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN + (cb ? kGN : 0)
-                      : (b >> 3) < (helpers ? 2 * kGN : kGN);
+template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, bool helpers = false) {
+  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < (helpers ? 2 * kGN : kGN);
 }
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
@@ -1108,9 +1104,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   // of those rows and sums the 6 others (pk_l1_gather_rows); all 4 waves split
   // the correction's K (wave w: rows m' = 16 w .. +15 of every replica), and
   // wave c adds their partials.  gk >= 4 blocks only publish partials.
-  // (the single replica's correction runs in dedicated blocks on the chains'
-  // XCD instead: pk_corr)
-  const bool gat = XM && gk < kNCH;
+  const bool gat = gk < kNCH;
   const int c = gk;
   float* Red = lds + L1GLay::RED;
   if (!a.carry) {
@@ -1192,8 +1186,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
       Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
     }
-    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false, !XM) &&
-        pk_sr_active<NL>(tid, a.helpers, !XM) && ok) {
+    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false) && pk_sr_active<NL>(tid, a.helpers) && ok) {
       // hand the step counter on once every block has read it (SF tags)
       const uint32_t t0 = (uint32_t)(s0 + 1);
       poll.start();
@@ -1406,101 +1399,6 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   if (gk == 0 && tid < 16) a.P[a.b_off[0] + n0 + tid] = B1[tid];
   pk_report(a, ok);
   if (lb == 0) PK_EDGE(2);
-}
-
-// Correction block (single replica), one per column tile gn, at blockIdx
-// 8 (4 + kN + gn) -- on the chains' XCD, so both critical hops (the chains'
-// dZ1 in, Z1 out) stay in that XCD's L2 instead of crossing XCDs.  Light by
-// design (no X tiles, no W1): wave c gathers P(s+1) for chain c's 16 rows
-// from the column's 7 layer-1 partials, and once dZ1(s) arrives contracts the
-// correction C(s+1) = -lr G1(s+1) dZ1(s) for those rows (16 MFMAs, the Gram
-// fragments prefetched into registers) and publishes Z1(s+1) = P + C as tagged
-// granules.  (Round 3 measured the layer-1 gk = 0 blocks themselves on XCD 0:
-// their X / W1 traffic slowed the chains' loads there.)
-__device__ __forceinline__ void pk_corr(const PersistArgs& a, float* lds, int gn, int blk) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = lane & 15, q = lane >> 4, c = w;
-  const int n0 = 16 * gn;
-  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
-  Poll poll{a.err, a.timeout_ticks, 0, 0};
-  const uint64_t s0 = ld_ctr64(a.ctr + 1);
-  pk_started(a, blk, s0);
-  float* Dz = lds;  // dZ1 tile [64][17]
-  // wave c: P = the column's 7 k-partials of chain c's rows, summed in gk order
-  // (b1 rides in gk = 0's); wave-local flag polls
-  auto gather = [&](f4v& z, int par, uint32_t tg) __attribute__((always_inline)) -> bool {
-    bool ok = true;
-    if (lane < kGK) ok = wait_flag(rb, pk_pf(par, gn + kGN * lane), tg, poll);
-    ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
-    asm volatile("" ::: "memory");
-    if (!ok) return false;
-    f4v v[kGK];
-#pragma unroll
-    for (int g2 = 0; g2 < kGK; ++g2) v[g2] = ld_f4(rb, pk_part_off(par, gn + kGN * g2, c) + i * 16 + 4 * q);
-    z = v[0];
-#pragma unroll
-    for (int g2 = 1; g2 < kGK; ++g2) z += v[g2];
-    return true;
-  };
-  if (!a.carry) {  // no state from a previous launch: step s0's Z1 directly
-    const uint32_t t0 = (uint32_t)(s0 + 1);
-    f4v z;
-    if (!gather(z, (int)(s0 & 1), t0)) {
-      pk_report(a, false);
-      return;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) st_gran(rb, kOffCg + (int64_t)(16 * c + 4 * q + r) * kD1 + n0 + i, z[r], t0);
-  }
-  bool ok = true;
-  const int stamp_on = g_pk_stamp_on && gn == 0;
-  for (int it = 0; it < a.steps && ok; ++it) {
-    const uint64_t s = s0 + (uint64_t)it;
-    const uint32_t tag = (uint32_t)(s + 1), tagn = tag + 1;
-    const int parn = (int)((s + 1) & 1);
-    // Gram fragments of step s+1, data only (in flight during the waits):
-    // lane (i, q) holds G1(s+1)[m = 16 c + i][m' = 4 ks + q] = T[m'][m]
-    float gv[16];
-    {
-      const float* gb = a.gram + (int64_t)((s + 1) % (uint64_t)a.nbatches) * (kB * kB) + 16 * c + i;
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks) gv[ks] = gb[(4 * ks + q) * kB];
-    }
-    f4v zs;
-    if (!gather(zs, parn, tagn)) ok = false;
-    // dZ1(s)[:, n0 .. n0 + 15] of the 4 chains
-    {
-      const int m = tid >> 2, qq = tid & 3;
-      const int64_t g = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
-      uint4 v0, v1;
-      poll.start();
-      for (;;) {
-        v0 = ld_gran2(rb, g);
-        v1 = ld_gran2(rb, g + 2);
-        if (v0.y == tag && v0.w == tag && v1.y == tag && v1.w == tag) break;
-        if (!poll.again()) { ok = false; break; }
-      }
-      Dz[m * 17 + 4 * qq + 0] = __uint_as_float(v0.x);
-      Dz[m * 17 + 4 * qq + 1] = __uint_as_float(v0.z);
-      Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
-      Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
-    }
-    PK_STAMP(0, 5);
-    ok = __syncthreads_and(ok ? 1 : 0) != 0;
-    if (!ok) break;
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < kB / 4; ks += 2) {
-      c0 = mfma_f32_16x16x4(gv[ks], Dz[(4 * ks + q) * 17 + i], c0);
-      c1 = mfma_f32_16x16x4(gv[ks + 1], Dz[(4 * ks + 4 + q) * 17 + i], c1);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      st_gran(rb, kOffCg + (int64_t)(16 * c + 4 * q + r) * kD1 + n0 + i, zs[r] + -a.lr * (c0[r] + c1[r]), tagn);
-    PK_STAMP(0, 4);
-    lds_barrier();  // every wave's Dz reads done before the next step's Dz writes
-  }
-  pk_report(a, ok);
 }
 
 // pkx helper block (>= 4 replicas): replicas [(nrep + 1) / 2, nrep) of the dW1
@@ -2832,11 +2730,10 @@ void mlp_persist_k(PersistArgs a) {
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
     constexpr bool XM = MODE >= 2;
-    if (!pk_sr_active<NL>(b, MODE == 3 && a.helpers, MODE == 0)) return;
+    if (!pk_sr_active<NL>(b, MODE == 3 && a.helpers)) return;
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
-      else if (y < kNCH + GTile<NL>::kN) pk_gtile<NL, XM>(a, lds, y - kNCH, b);
-      else if constexpr (MODE == 0) pk_corr(a, lds, y - kNCH - GTile<NL>::kN, b);
+      else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
     } else if (y < kGN) {
       pk_layer1_gram<NL, MODE == 3 ? 2 : MODE == 2 ? 1 : 0>(a, lds, y + kGN * (x - 1), b);
     } else if constexpr (MODE == 3) {
@@ -2892,11 +2789,10 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return e;
-    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(MODE == 1, MODE == 0)) return hipErrorCooperativeLaunchTooLarge;
+    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(MODE == 1)) return hipErrorCooperativeLaunchTooLarge;
     attr = true;
   }
-  hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(pk_grid<NL>(MODE == 1, MODE == 0)), dim3(kThreads), lds, s,
-                     a);
+  hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(pk_grid<NL>(MODE == 1)), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
