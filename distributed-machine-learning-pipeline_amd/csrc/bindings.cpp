@@ -587,46 +587,87 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("head_set_stamping", &head_set_stamping);
   m.def("head_set_debug", &head_set_debug);
-  m.def("wgrad_sgd_multi", [bf16p](py::list layers, int tile) {
-    // each item: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad); tensors may be None
-    std::vector<WgLayer> v;
+  // one layer of the fused weight-gradient launches:
+  // (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl]); tensors may be None
+  auto wg_layer = [bf16p](py::handle it) -> WgLayer {
     auto opt = [](py::handle h) -> c10::optional<torch::Tensor> {
       if (h.is_none()) return c10::nullopt;
       return h.cast<torch::Tensor>();
     };
-    for (py::handle it : layers) {
-      py::tuple t = it.cast<py::tuple>();
-      TORCH_CHECK(t.size() == 12 || t.size() == 14,
-                  "wgrad_sgd_multi: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl])");
-      torch::Tensor Z = t[0].cast<torch::Tensor>(), X = t[1].cast<torch::Tensor>();
-      const int64_t M = t[2].cast<int64_t>(), N = t[3].cast<int64_t>(), K = t[4].cast<int64_t>();
-      TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
-      TORCH_CHECK(Z.size(0) >= M && X.size(0) >= M && Z.size(1) >= ((N + 7) / 8) * 8 &&
-                  X.size(1) >= ((K + 7) / 8) * 8, "Z / X too small");
-      WgLayer a{};
-      a.Z = bf16p(Z, "Z"); a.ldz = Z.stride(0); a.X = bf16p(X, "X"); a.ldx = X.stride(0);
-      a.M = (int)M; a.N = (int)N; a.K = (int)K;
-      a.alpha = (float)t[5].cast<double>(); a.lr = (float)t[6].cast<double>();
-      auto chk2 = [&](const torch::Tensor& x, const char* nm) {
-        TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= N && x.size(1) >= K, nm, " shape");
-      };
-      if (auto W = opt(t[7])) { chk2(*W, "W"); check_f32(*W, "W"); a.W = W->data_ptr<float>(); a.ldw = W->stride(0); }
-      if (auto Wb = opt(t[8])) { chk2(*Wb, "Wb"); a.Wb = bf16p(*Wb, "Wb"); a.ldwb = Wb->stride(0); }
-      if (auto G = opt(t[9])) { chk2(*G, "G"); check_f32(*G, "G"); a.G = G->data_ptr<float>(); a.ldg = G->stride(0); }
-      if (auto b = opt(t[10])) { check_f32(*b, "bias"); TORCH_CHECK(b->numel() >= N, "bias"); a.bias = b->data_ptr<float>(); }
-      if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
-      if (t.size() == 14) {  // split master: this step's hi words + the int16 remainders
-        if (auto Wh = opt(t[12])) { chk2(*Wh, "Wh"); a.Wh = bf16p(*Wh, "Wh"); a.ldwh = Wh->stride(0); }
-        if (auto Wl = opt(t[13])) {
-          chk2(*Wl, "Wl");
-          TORCH_CHECK(Wl->scalar_type() == torch::kInt16, "Wl must be int16");
-          a.Wl = reinterpret_cast<uint16_t*>(Wl->data_ptr<int16_t>()); a.ldwl = Wl->stride(0);
-        }
+    py::tuple t = it.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 12 || t.size() == 14,
+                "wgrad layer: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl])");
+    torch::Tensor Z = t[0].cast<torch::Tensor>(), X = t[1].cast<torch::Tensor>();
+    const int64_t M = t[2].cast<int64_t>(), N = t[3].cast<int64_t>(), K = t[4].cast<int64_t>();
+    TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
+    TORCH_CHECK(Z.size(0) >= M && X.size(0) >= M && Z.size(1) >= ((N + 7) / 8) * 8 &&
+                X.size(1) >= ((K + 7) / 8) * 8, "Z / X too small");
+    WgLayer a{};
+    a.Z = bf16p(Z, "Z"); a.ldz = Z.stride(0); a.X = bf16p(X, "X"); a.ldx = X.stride(0);
+    a.M = (int)M; a.N = (int)N; a.K = (int)K;
+    a.alpha = (float)t[5].cast<double>(); a.lr = (float)t[6].cast<double>();
+    auto chk2 = [&](const torch::Tensor& x, const char* nm) {
+      TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= N && x.size(1) >= K, nm, " shape");
+    };
+    if (auto W = opt(t[7])) { chk2(*W, "W"); check_f32(*W, "W"); a.W = W->data_ptr<float>(); a.ldw = W->stride(0); }
+    if (auto Wb = opt(t[8])) { chk2(*Wb, "Wb"); a.Wb = bf16p(*Wb, "Wb"); a.ldwb = Wb->stride(0); }
+    if (auto G = opt(t[9])) { chk2(*G, "G"); check_f32(*G, "G"); a.G = G->data_ptr<float>(); a.ldg = G->stride(0); }
+    if (auto b = opt(t[10])) { check_f32(*b, "bias"); TORCH_CHECK(b->numel() >= N, "bias"); a.bias = b->data_ptr<float>(); }
+    if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
+    if (t.size() == 14) {  // split master: this step's hi words + the int16 remainders
+      if (auto Wh = opt(t[12])) { chk2(*Wh, "Wh"); a.Wh = bf16p(*Wh, "Wh"); a.ldwh = Wh->stride(0); }
+      if (auto Wl = opt(t[13])) {
+        chk2(*Wl, "Wl");
+        TORCH_CHECK(Wl->scalar_type() == torch::kInt16, "Wl must be int16");
+        a.Wl = reinterpret_cast<uint16_t*>(Wl->data_ptr<int16_t>()); a.ldwl = Wl->stride(0);
       }
-      v.push_back(a);
     }
+    return a;
+  };
+  m.def("wgrad_sgd_multi", [wg_layer](py::list layers, int tile) {
+    std::vector<WgLayer> v;
+    for (py::handle it : layers) v.push_back(wg_layer(it));
     hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
   }, py::arg("layers"), py::arg("tile") = 0);
+  m.def("wide_bwd", [wg_layer, bf16p](py::list layers, py::object fused, int rows,
+                                      c10::optional<torch::Tensor> dzo_, c10::optional<torch::Tensor> part_,
+                                      c10::optional<torch::Tensor> tick_, c10::optional<torch::Tensor> ready) {
+    // layers as wgrad_sgd_multi; fused: None (plain updates) or the index of the
+    // fused layer (must be 0); its dZ output dzo [M x K] bf16; every later layer
+    // whose Z is dzo waits on `ready` (int32, K / 64 counters, zero)
+    std::vector<WgLayer> v;
+    for (py::handle it : layers) v.push_back(wg_layer(it));
+    std::vector<WbFused> f(v.size());
+    if (!fused.is_none()) {
+      const int j = fused.cast<int>();
+      TORCH_CHECK(j == 0 && !v.empty(), "wide_bwd: the fused layer must be the first");
+      const WgLayer& L = v[0];
+      TORCH_CHECK(dzo_ && part_ && tick_, "wide_bwd: a fused layer needs dzo, part and tick");
+      const torch::Tensor &dzo = *dzo_, &part = *part_, &tick = *tick_;
+      TORCH_CHECK(rows >= 64 && rows % 64 == 0 && L.N % rows == 0, "wide_bwd: rows per slice");
+      TORCH_CHECK(dzo.dim() == 2 && dzo.stride(1) == 1 && dzo.size(0) >= L.M && dzo.size(1) >= L.K, "dzo shape");
+      const int kt = (L.K + 63) / 64, S = L.N / rows;
+      check_f32(part, "part");
+      TORCH_CHECK(part.numel() >= (int64_t)S * kt * 4096, "wide_bwd: partial slab too small");
+      TORCH_CHECK(tick.is_cuda() && tick.scalar_type() == torch::kInt32 && tick.numel() >= kt, "tick");
+      WbFused& F = f[0];
+      F.fused = 1; F.slices = S; F.rows = rows;
+      F.dzo = bf16p(dzo, "dzo"); F.lddo = dzo.stride(0);
+      F.part = part.data_ptr<float>(); F.tick = tick.data_ptr<int32_t>();
+      for (size_t q = 1; q < v.size(); ++q) {
+        if (v[q].Z != F.dzo) continue;
+        TORCH_CHECK(F.ready == nullptr, "wide_bwd: one layer may consume the fused layer's output");
+        TORCH_CHECK(ready && ready->is_cuda() && ready->scalar_type() == torch::kInt32 && ready->numel() >= kt,
+                    "wide_bwd: ready counters");
+        F.ready = ready->data_ptr<int32_t>();
+        F.nready = (v[q].K + 63) / 64;
+        f[q].wait_prev = 1;
+      }
+    }
+    hip_ok(wide_bwd(v.data(), f.data(), (int)v.size(), cur_stream()), "wide_bwd");
+  }, py::arg("layers"), py::arg("fused"), py::arg("rows") = 1024, py::arg("dzo") = py::none(),
+     py::arg("part") = py::none(), py::arg("tick") = py::none(), py::arg("ready") = py::none());
+  m.def("wide_bwd_errors", [](bool clear) { return wide_bwd_errors(clear); }, py::arg("clear") = true);
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

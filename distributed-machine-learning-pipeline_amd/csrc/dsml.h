@@ -319,6 +319,24 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // 64 x 64 everywhere; 0 (auto): 128 for fp32-master layers at M >= 512 rows,
 // else 64.
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
+// Fused backward (kernels/wgrad_sgd.hip wide_bwd): per layer either the plain
+// update tiles, or (fused) the activation gradient dZ_l = (Z . Wh) * (X > 0)
+// folded into the update's pass over W (rows in `slices` slices of `rows`,
+// partials summed in slice order), announcing each 64-column block of dZ_l on
+// `ready` to a following layer with wait_prev (its Z = dzo).  M <= 64.
+struct WbFused {
+  int fused;
+  int slices, rows;
+  uint16_t* dzo;
+  int64_t lddo;
+  float* part;  // >= slices * ceil(K / 64) * 4096 floats
+  int* tick;    // ceil(K / 64), zero, left zero
+  int* ready;   // ceil(K / 64), zero, left zero (nullable)
+  int nready;   // consumers per block: the next layer's k tiles
+  int wait_prev;
+};
+hipError_t wide_bwd(const WgLayer* layers, const WbFused* fused, int n, hipStream_t s);
+uint32_t wide_bwd_errors(bool clear);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 void head_set_debug(int v);

@@ -61,7 +61,8 @@ class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
-                 gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False):
+                 gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False,
+                 fused_bwd: Optional[bool] = None, bwd_rows: int = 0):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -172,6 +173,31 @@ class WideMlpTrainer:
         self._ss = torch.cuda.Stream(dev) if self.overlap_wgrad else None
         # an epoch graph must start at an even step (the Wb parity it baked in)
         self.period = self.nbatches if self.nbatches % 2 == 0 else 2 * self.nbatches
+        # fused_bwd (single replica, 3 layers with the fused head): the dgrad of
+        # layer 1 runs inside its weight-update pass (kernels/wgrad_sgd.hip
+        # wide_bwd) on the W_1 words the update streams anyway -- 32 MB less HBM
+        # traffic and one launch less per step.  Off by default: measured on
+        # MI355X it does not beat the split-K dgrad + update launches (76.6 vs
+        # 75.6 us/step at its best slice height; profiles/r4_wide_fused_bwd_ab.json)
+        if fused_bwd is None:
+            fused_bwd = os.environ.get("HIPDSML_WIDE_FUSED_BWD", "0") == "1"
+        self.fused_bwd = (fused_bwd and not self.ctx.is_distributed and self._ss is None and L == 3 and
+                          self.fused_head and batch <= 64 and d[1] % 64 == 0 and d[2] % 64 == 0)
+        if self.fused_bwd:
+            rows = bwd_rows or int(os.environ.get("HIPDSML_WIDE_BWD_ROWS", "512"))
+            if not bwd_rows:  # the default: the largest multiple of 64 <= rows dividing d[2]
+                rows = max(r for r in range(64, min(rows, d[2]) + 1, 64) if d[2] % r == 0)
+            if rows % 64 or d[2] % rows:
+                raise ValueError(f"bwd_rows={rows} must be a multiple of 64 dividing {d[2]}")
+            self.bwd_rows = rows
+            # layer 0's update in a launch of its own (default): inside the fused
+            # launch its tiles wait for the dZ_1 blocks at the fused tiles' LDS
+            # footprint (2 workgroups per CU), measured slower
+            self.bwd_split = os.environ.get("HIPDSML_WIDE_BWD_SPLIT", "1") == "1"
+            kt = d[1] // 64
+            self.Pd = torch.zeros((d[2] // rows) * kt * 4096, dtype=torch.float32, device=dev)
+            self.wb_tick = torch.zeros(kt, dtype=torch.int32, device=dev)
+            self.wb_ready = torch.zeros(kt, dtype=torch.int32, device=dev)
         if self.xact:
             self._init_xact(batch)
         self._refresh_bf16()
@@ -326,6 +352,21 @@ class WideMlpTrainer:
                                1.0 / n, self.lr, None, nxt[l], None, b, None, cur[l], self.Wlo[l]))
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
+            self.steps_done += 1
+            return
+        if self.fused_bwd:
+            # ONE launch: layer 1's update with its dgrad folded in (dZ_1 out), the
+            # classifier's update, and layer 0's update tiles, which wait for dZ_1
+            lay = []
+            for l in (1, 2, 0):
+                W, b = self.views[l]
+                lay.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l], None, b,
+                            None, cur[l], self.Wlo[l]))
+            if self.bwd_split:  # layer 0's update in a launch of its own (full occupancy)
+                C.wide_bwd(lay[:2], 0, self.bwd_rows, self.dZ[1], self.Pd, self.wb_tick, None)
+                C.wgrad_sgd_multi(lay[2:])
+            else:
+                C.wide_bwd(lay, 0, self.bwd_rows, self.dZ[1], self.Pd, self.wb_tick, self.wb_ready)
             self.steps_done += 1
             return
         if fused_sgd and self._ss is None:

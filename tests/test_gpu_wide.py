@@ -197,7 +197,7 @@ def test_wide_native_evaluate_matches_fp32_forward():
 def test_wide_overlapped_wgrad_is_bit_identical(nb):
     spec = MlpSpec((784, 256, 128, 10))
     ds = synthetic_mnist(64 * nb, seed=11)
-    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True)
+    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, fused_bwd=False)
     b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, overlap_wgrad=True)
     a.train_steps(13)
     b.train_steps(13)
@@ -281,3 +281,58 @@ def test_dw_gemm_fused_sgd_and_bias(M, N):
     torch.cuda.synchronize()
     assert (G.cpu() - gW).abs().max().item() < 1e-3
     assert (gb.cpu() - dZT.float().sum(1)).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("dims,rows,batch,split", [((784, 512, 256, 10), 64, 64, "0"),
+                                                   ((784, 512, 256, 10), 256, 64, "1"),
+                                                   ((784, 4096, 4096, 10), 512, 64, "0"),
+                                                   ((784, 4096, 4096, 10), 512, 64, "1"),
+                                                   ((784, 4096, 4096, 10), 1024, 48, "0")], ids=str)
+def test_wide_fused_backward_matches_separate_dgrad(dims, rows, batch, split, monkeypatch):
+    """The fused backward (layer 1's dgrad folded into its weight-update pass,
+    layer 0's update tiles waiting on the dZ_1 blocks in the same launch)
+    against the split-K dgrad GEMM + update launch: the weight updates of
+    layers 1 and 2 use the same products (bit-identical), dZ_1 sums the same
+    products in another order (bf16 outputs within one rounding), and the run
+    is deterministic."""
+    C = require_native()
+    monkeypatch.setenv("HIPDSML_WIDE_BWD_SPLIT", split)  # "0": layer 0 waits inside the fused launch
+    spec = MlpSpec(dims)
+    ds = synthetic_mnist(batch * 4, seed=12)
+    mk = lambda fused: WideMlpTrainer(spec, ds, batch=batch, lr=0.05, seed=7, graph=False, fused_bwd=fused,
+                                      bwd_rows=rows if fused else 0)
+    a, b, c = mk(True), mk(False), mk(True)
+    assert a.fused_bwd and not b.fused_bwd and a.bwd_rows == rows and a.bwd_split == (split == "1")
+    C.wide_bwd_errors(True)
+    for t in (a, b, c):
+        t.train_steps(1)
+        t.synchronize()
+    assert C.wide_bwd_errors(True) == 0
+    dz_a, dz_b = a.dZ[1].float().cpu(), b.dZ[1].float().cpu()
+    scale = dz_b.abs().max().item()
+    assert (dz_a - dz_b).abs().max().item() <= 2 ** -7 * scale, "dZ_1 beyond one bf16 rounding"
+    for l in (1, 2):
+        assert torch.equal(a.wb(l).cpu(), b.wb(l).cpu()), f"layer {l} update differs"
+        assert torch.equal(a.Wlo[l].cpu(), b.Wlo[l].cpu())
+    P_a, P_b = a.P.cpu(), b.P.cpu()
+    rel = (P_a - P_b).norm().item() / max((P_b - init_params(a.layout, 7, "kaiming")).norm().item(), 1e-30)
+    assert rel < 2e-2, rel
+    for t in (a, b, c):
+        t.train_steps(7)  # epoch wrap, both Wb parities
+        t.synchronize()
+    assert torch.equal(a.P.cpu(), c.P.cpu())  # deterministic: slice-ordered partial sums
+    assert C.wide_bwd_errors(True) == 0
+    sa, sb = a.read_stats(), b.read_stats()
+    assert abs(sa.avg_loss - sb.avg_loss) < 0.02 * max(1.0, sb.avg_loss)
+
+
+def test_wide_fused_backward_in_graph_matches_eager():
+    spec = MlpSpec((784, 512, 256, 10))
+    ds = synthetic_mnist(64 * 4, seed=13)
+    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=False, fused_bwd=True)
+    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, fused_bwd=True)
+    assert a.fused_bwd and b.fused_bwd
+    a.train_steps(12)
+    b.train_steps(12)
+    a.synchronize(); b.synchronize()
+    assert torch.equal(a.P.cpu(), b.P.cpu())
