@@ -367,6 +367,19 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
   }
   const bool vb = n0 + i < N;
   const uint16_t* pb = B + (int64_t)(vb ? n0 + i : N - 1) * ldb;
+  // the epilogue's bias and mask operands fetched up front: their round trip
+  // hides under the K loop instead of following it
+  constexpr int PER = 1024 / NT;  // outputs of the 64x16 tile per thread
+  float bias_v[PER];
+  uint16_t mask_v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + NT * j;
+    const int m = m0 + (e >> 4), n = n0 + (e & 15);
+    const bool ok = m < M && n < N;
+    bias_v[j] = (epi.bias && ok) ? epi.bias[n] : 0.f;
+    mask_v[j] = (epi.mask && ok) ? epi.mask[(int64_t)m * epi.ldm + n] : (uint16_t)0x3f80;  // 1.0
+  }
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
@@ -398,7 +411,6 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) mine[(16 * t + 4 * g + r) * kR64Pad + i] = acc[t][r];
   __syncthreads();
-  constexpr int PER = 1024 / NT;  // outputs of the 64x16 tile per thread
   float v[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -411,9 +423,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
     const int m = m0 + mr, n = n0 + nc;
     x *= epi.alpha;
     if (m < M && n < N) {
-      if (epi.bias) x += epi.bias[n];
+      x += bias_v[j];
       if (epi.relu) x = fmaxf(x, 0.f);
-      if (epi.mask) x = bf16_to_f32(epi.mask[(int64_t)m * epi.ldm + n]) > 0.f ? x : 0.f;
+      if (epi.mask) x = bf16_to_f32(mask_v[j]) > 0.f ? x : 0.f;
     } else {
       x = 0.f;
     }
