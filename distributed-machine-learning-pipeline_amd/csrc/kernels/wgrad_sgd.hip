@@ -691,9 +691,6 @@ __device__ __forceinline__ wb_u2 wb_dstr(uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
   return v;
 }
-__device__ __forceinline__ void wb_dsw128(uint32_t addr, f32x4 v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
-}
 __device__ __forceinline__ uint32_t wb_dsu16(uint32_t addr) {
   uint32_t v;
   asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(addr));
