@@ -489,6 +489,10 @@ class WideMlpTrainer:
 
     def synchronize(self) -> None:
         torch.cuda.synchronize(self.device)
+        if self.fused_bwd and not self.bwd_split and self.C.wide_bwd_errors(True):
+            # a layer-0 update tile gave up waiting for its dZ_1 block (bounded
+            # in-launch hand-off): the step's weights are not valid
+            raise RuntimeError("fused wide backward: an in-launch hand-off timed out")
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         self.synchronize()
