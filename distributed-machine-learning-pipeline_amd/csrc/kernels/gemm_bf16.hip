@@ -741,8 +741,11 @@ __device__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bi
   do {                                                                              \
     if (g_head_stamp_on && t == 0 && m < 64) g_head_stamps[m][(k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-constexpr int kHeadMaxC = 16;
+constexpr int kHeadMaxC = 16;  // classes the head supports (instantiated for <= 10 and <= 16)
 constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
+// MAXC: the class count rounded up to an instantiated size -- register arrays
+// sized for 16 classes spilled into AGPRs at the BASELINE's 10
+template <int MAXC>
 __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
@@ -750,9 +753,9 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats,
     uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt,
     int row_stats) {
-  __shared__ float part[kHeadMaxC][257];  // per-thread partial dot products, per class
-  __shared__ float zsum[kHeadMaxC];
-  __shared__ float gz[kHeadMaxC];         // bf16-rounded dLogits of this row
+  __shared__ float part[MAXC][257];  // per-thread partial dot products, per class
+  __shared__ float zsum[MAXC];
+  __shared__ float gz[MAXC];         // bf16-rounded dLogits of this row
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* hr = H + (int64_t)m * ldh;
   // the softmax's own operands go out with the first loads (not after the reduction)
@@ -767,26 +770,26 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   const bool rst = row_stats && stats && w == 0 && !(g_head_dbg & 1);
   float4 racc = rst ? *reinterpret_cast<const float4*>(stats + 4 * (int64_t)m) : make_float4(0.f, 0.f, 0.f, 0.f);
   // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
-  uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][kHeadMaxC];
+  uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][MAXC];
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
     const int k = (t + 256 * j) * 8;
     const bool kv = k < K;
     hv[j] = kv ? *reinterpret_cast<const uint4*>(hr + k) : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-    for (int c = 0; c < kHeadMaxC; ++c)
+    for (int c = 0; c < MAXC; ++c)
       wv[j][c] = (kv && c < C) ? *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k)
                                : make_uint4(0u, 0u, 0u, 0u);
   }
-  float acc[kHeadMaxC];
+  float acc[MAXC];
 #pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c) acc[c] = 0.f;
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
     const float h[8] = {bf16lo(hv[j].x), bf16hi(hv[j].x), bf16lo(hv[j].y), bf16hi(hv[j].y),
                         bf16lo(hv[j].z), bf16hi(hv[j].z), bf16lo(hv[j].w), bf16hi(hv[j].w)};
 #pragma unroll
-    for (int c = 0; c < kHeadMaxC; ++c) {
+    for (int c = 0; c < MAXC; ++c) {
       const uint4 x = wv[j][c];
       acc[c] += h[0] * bf16lo(x.x) + h[1] * bf16hi(x.x) + h[2] * bf16lo(x.y) + h[3] * bf16hi(x.y) +
                 h[4] * bf16lo(x.z) + h[5] * bf16hi(x.z) + h[6] * bf16lo(x.w) + h[7] * bf16hi(x.w);
@@ -795,15 +798,17 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   HEAD_STAMP(1);
   // block reduction per class: LDS transpose, then one 16-lane DPP row per class
 #pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c) part[c][t] = acc[c];
+  for (int c = 0; c < MAXC; ++c) part[c][t] = acc[c];
   lds_barrier();  // LDS only: no wait for this block's global stores
   {
     const int c = t >> 4, sg = t & 15;  // class c = row of 16 lanes; 16 partials per lane
-    float v = 0.f;
+    if (c < MAXC) {  // whole 16-lane rows: the DPP row sum stays within active lanes
+      float v = 0.f;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v += part[c][16 * sg + u];
-    v = row16_sum(v);
-    if (sg == 0) zsum[c] = v;
+      for (int u = 0; u < 16; ++u) v += part[c][16 * sg + u];
+      v = row16_sum(v);
+      if (sg == 0) zsum[c] = v;
+    }
   }
   lds_barrier();  // LDS only: no wait for this block's global stores
   HEAD_STAMP(2);
@@ -832,7 +837,7 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
       dz[(int64_t)m * ldz + c] = hq;
       if (dzT) dzT[(int64_t)c * ldt + m] = hq;
     }
-    if (c < kHeadMaxC) gz[c] = bf16_to_f32(hq);
+    if (c < MAXC) gz[c] = bf16_to_f32(hq);
     if (c == y && stats && !(g_head_dbg & 1)) {
       if (row_stats) {
         racc.x += -logf(p + 1e-10f);
@@ -852,16 +857,16 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
   // chunks this thread already holds; bf16 row store + transposed copy.
   lds_barrier();  // LDS only: no wait for this block's global stores
-  float g[kHeadMaxC];
+  float g[MAXC];
 #pragma unroll
-  for (int c = 0; c < kHeadMaxC; ++c) g[c] = c < C ? gz[c] : 0.f;
+  for (int c = 0; c < MAXC; ++c) g[c] = c < C ? gz[c] : 0.f;
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
     const int k = (t + 256 * j) * 8;
     if (k >= K) continue;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < kHeadMaxC; ++c) {
+    for (int c = 0; c < MAXC; ++c) {
       const uint4 x = wv[j][c];
       a[0] += g[c] * bf16lo(x.x); a[1] += g[c] * bf16hi(x.x);
       a[2] += g[c] * bf16lo(x.y); a[3] += g[c] * bf16hi(x.y);
@@ -911,9 +916,14 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
       (ldw & 7) ||
       (((uintptr_t)H | (uintptr_t)W) & 15))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_softmax_xent_k, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
-                     labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
-                     ldpt, row_stats);
+  if (C <= 10)
+    hipLaunchKernelGGL(head_softmax_xent_k<10>, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
+                       labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
+                       ldpt, row_stats);
+  else
+    hipLaunchKernelGGL(head_softmax_xent_k<kHeadMaxC>, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K,
+                       C, labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
+                       ldpt, row_stats);
   return hipGetLastError();
 }
 
