@@ -66,8 +66,10 @@ def build_trainer(cfg: TrainConfig, spec: MlpSpec, data: Dataset, ctx: DistConte
             raise ValueError("the wide bf16 engine implements plain SGD")
         return WideMlpTrainer(spec, data, batch=cfg.batch, lr=cfg.lr, ctx=ctx, seed=cfg.seed,
                               init="kaiming" if cfg.init == "auto" else cfg.init,
-                              # the fused exchanges are fp32-MLP kernels; the wide engine syncs by RCCL
-                              sync="rccl" if cfg.sync in ("auto", "xact", "xgmi") else cfg.sync,
+                              # the fused exchanges and the persistent forms are fp32-MLP
+                              # kernels; the wide engine syncs by RCCL
+                              sync="rccl" if cfg.sync in ("auto", "xact", "xgmi", "pk", "pk2", "pkg", "pkg2",
+                                                          "pkx") else cfg.sync,
                               graph=cfg.graph_steps != 0), engine
     from .trainer import MlpTrainer
 

@@ -43,7 +43,7 @@ class TrainConfig:
     data: str = "synthetic"               # synthetic | mnist (idx files under data_dir)
     data_dir: str = ""
     samples: int = 60032                  # synthetic samples per replica
-    sync: str = "auto"                    # auto | xact | xgmi | rccl | ring | torch
+    sync: str = "auto"                    # auto | pkx | pkg | pkg2 | pk | pk2 | xact | xgmi | rccl | ring | torch
     ring_chunk_bytes: int = 1 << 20
     graph_steps: int = 50                 # steps per hipGraph (fused-exchange steps too); 0 = eager
     backend: str = "auto"                 # torch.distributed backend: auto | nccl | gloo
