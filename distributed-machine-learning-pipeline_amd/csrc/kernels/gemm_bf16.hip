@@ -818,18 +818,13 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     float z = -3.402823466e38f;
     if (cv) z = zsum[c] + bc;
     if (cv && logits) logits[(int64_t)m * ldl + c] = z;
+    // every class sits in lanes 0-15 (C <= 16): 16-lane DPP reductions
+    // instead of 64-lane shuffles (each an LDS-path ds_bpermute round trip)
     float mx = z;
     int am = cv ? c : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float om = __shfl_xor(mx, o, 64);
-      const int oa = __shfl_xor(am, o, 64);
-      argmax_combine(mx, am, om, oa);
-    }
+    row16_argmax(mx, am);
     const float e = cv ? expf(z - mx) : 0.f;
-    float se = e;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    const float se = row16_sum(e);
     const float p = e / se;
     const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
     const uint16_t hq = f32_to_bf16(gr);
