@@ -742,6 +742,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
+  m.def("mlp_persist_set_stamp_window", [](int first_step) { mlp_persist_set_stamp_window(first_step); },
+        "stamp steps first_step .. first_step + 7 of a launch (< 0: off)");
   m.def("mlp_persist_set_probe", [](int mode) { mlp_persist_set_probe(mode); },
         "testing only: 0 off; 1 peers' dZ1 rows taken as arrived (lone-replica probe of the Gram "
         "forms); 2 mirror: every push loops back into this replica's own buffer in the peer's "

@@ -93,6 +93,7 @@ hipError_t mlp_f32_wgrad(const float* X, int64_t ldx, float* P, float* G, const 
 bool mlp_persist_supported(const MlpDesc& d);
 hipError_t mlp_persist_read_stamps(uint64_t* host_out);  // [4][8][8] (role, step, phase)
 void mlp_persist_set_stamping(bool on);
+void mlp_persist_set_stamp_window(int first_step);  // stamp steps first..first+7 (< 0: off)
 void mlp_persist_set_jitter(int ticks);  // testing only: uneven-load injection (0 = off)
 int64_t mlp_persist_xbuf_granules();
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,

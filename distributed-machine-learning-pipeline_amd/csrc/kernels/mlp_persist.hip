@@ -354,10 +354,12 @@ __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) 
     if (g_pk_stamp_on && threadIdx.x == 0)                                            \
       g_pk_stamps[3][0][(ph)] = __builtin_amdgcn_s_memrealtime();                     \
   } while (0)
+// g_pk_stamp_on = first stamped step + 1 (mlp_persist_set_stamp_window; the
+// default window is steps 8-15)
 #define PK_STAMP(role, ph)                                                            \
   do {                                                                                \
-    if (stamp_on && threadIdx.x == 0 && it >= 8 && it < 16)                            \
-      g_pk_stamps[(role)][it - 8][(ph)] = __builtin_amdgcn_s_memrealtime();            \
+    if (stamp_on && threadIdx.x == 0 && it >= g_pk_stamp_on - 1 && it < g_pk_stamp_on + 7) \
+      g_pk_stamps[(role)][it - (g_pk_stamp_on - 1)][(ph)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 struct PersistArgs {
@@ -2756,8 +2758,13 @@ void mlp_persist_set_probe(int mode) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_probe), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
+void mlp_persist_set_stamp_window(int first_step) {
+  const int v = first_step < 0 ? 0 : first_step + 1;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
+}
 void mlp_persist_set_stamping(bool on) {
-  const int v = on ? 1 : 0;
+  const int v = on ? 9 : 0;  // steps 8-15
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }

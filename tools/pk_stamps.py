@@ -70,8 +70,15 @@ if __name__ == "__main__":
     assert t.persistent
     t.train_steps(100)
     t.synchronize()
-    C.mlp_persist_set_stamping(True)
-    t.train_steps(32)
+    # STAMP_FIRST=k: steps k .. k+7 of a driver-shaped launch (STAMP_STEPS, default
+    # 20) instead of steps 8-15 of a 32-step one -- k = 0 shows a launch's ramp
+    first = os.environ.get("STAMP_FIRST")
+    if first is not None:
+        C.mlp_persist_set_stamp_window(int(first))
+        t.train_steps(int(os.environ.get("STAMP_STEPS", "20")))
+    else:
+        C.mlp_persist_set_stamping(True)
+        t.train_steps(32)
     t.synchronize()
     C.mlp_persist_set_stamping(False)
     out = decode(C.mlp_persist_stamps(), spec)
