@@ -674,6 +674,43 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("gemm_skinny_set_stamping", &gemm_skinny_set_stamping);
+  m.def("wide_fwd2", [bf16p](torch::Tensor X, torch::Tensor W1, torch::Tensor b1, torch::Tensor H1,
+                             torch::Tensor W2, torch::Tensor b2, torch::Tensor H2, int64_t M, int64_t K1,
+                             torch::Tensor ws, torch::Tensor ctr, torch::Tensor sync) {
+    auto rows = [](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm,
+                  " shape");
+    };
+    rows(X, M, K1, "X");
+    rows(W1, 4096, K1, "W1");
+    rows(H1, M, 4096, "H1");
+    rows(W2, 4096, 4096, "W2");
+    rows(H2, M, 4096, "H2");
+    check_f32(b1, "b1");
+    check_f32(b2, "b2");
+    check_f32(ws, "ws");
+    TORCH_CHECK(b1.numel() >= 4096 && b2.numel() >= 4096, "biases");
+    TORCH_CHECK(ws.numel() >= 4 * 64 * 4096, "ws too small");
+    check_cuda(ctr, "ctr");
+    check_cuda(sync, "sync");
+    TORCH_CHECK(ctr.scalar_type() == torch::kInt32 && ctr.numel() >= 64, "ctr: int32, >= 64");
+    TORCH_CHECK(sync.scalar_type() == torch::kInt32 && sync.numel() >= 259 && sync.is_contiguous(),
+                "sync: int32, >= 259, contiguous");
+    hip_ok(wide_fwd2(bf16p(X, "X"), X.stride(0), bf16p(W1, "W1"), W1.stride(0), b1.data_ptr<float>(),
+                     bf16p(H1, "H1"), H1.stride(0), bf16p(W2, "W2"), W2.stride(0), b2.data_ptr<float>(),
+                     bf16p(H2, "H2"), H2.stride(0), (int)M, (int)K1, ws.data_ptr<float>(),
+                     ctr.data_ptr<int32_t>(), sync.data_ptr<int32_t>(), cur_stream()),
+           "wide_fwd2");
+  }, py::arg("X"), py::arg("W1"), py::arg("b1"), py::arg("H1"), py::arg("W2"), py::arg("b2"), py::arg("H2"),
+     py::arg("M"), py::arg("K1"), py::arg("ws"), py::arg("ctr"), py::arg("sync"));
+  m.def("wide_fwd2_supported", [](int64_t dev) { return wide_fwd2_supported((int)dev); });
+  m.def("wide_fwd2_stamps", []() {
+    std::vector<uint64_t> v(256 * 8);
+    hip_ok(wide_fwd2_read_stamps(v.data()), "wide_fwd2_read_stamps");
+    return v;
+  });
+  m.def("wide_fwd2_set_stamping", &wide_fwd2_set_stamping);
+  m.def("wide_fwd2_set_early_dma", &wide_fwd2_set_early_dma);
   m.def("gemm_skinny_splits", &gemm_skinny_splits, py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("splits") = 0);
   m.def("hilo_split", [bf16p](torch::Tensor W, torch::Tensor hi, torch::Tensor lo) {

@@ -62,7 +62,8 @@ class WideMlpTrainer:
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
                  gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False,
-                 fused_bwd: Optional[bool] = None, bwd_rows: int = 0):
+                 fused_bwd: Optional[bool] = None, bwd_rows: int = 0,
+                 fused_fwd: Optional[bool] = None):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -198,6 +199,22 @@ class WideMlpTrainer:
             self.Pd = torch.zeros((d[2] // rows) * kt * 4096, dtype=torch.float32, device=dev)
             self.wb_tick = torch.zeros(kt, dtype=torch.int32, device=dev)
             self.wb_ready = torch.zeros(kt, dtype=torch.int32, device=dev)
+        # fused_fwd (single replica, 4096-wide hidden layers): both hidden layers'
+        # forward in ONE launch (kernels/wide_fwd.hip): every workgroup streams its
+        # W2 slice into LDS while it computes its layer-1 tile, then waits for the
+        # 64 layer-1 tiles its K slice reads.  Bit-exact with the two launches.
+        # Off by default: measured on MI355X it is slower (25.0 vs 22.2 us,
+        # profiles/r4_wide_fused_fwd_ab.json)
+        if fused_fwd is None:
+            fused_fwd = os.environ.get("HIPDSML_WIDE_FUSED_FWD", "0") == "1"
+        b_al = all(self.views[l][1].data_ptr() % 16 == 0 for l in range(min(L, 2)))
+        self.fused_fwd = bool(fused_fwd and not self.ctx.is_distributed and L == 3 and
+                              d[1] == 4096 and d[2] == 4096 and 512 <= d[0] <= 1024 and
+                              d[0] % 8 == 0 and batch <= 64 and b_al and
+                              self.C.wide_fwd2_supported(dev.index or 0))
+        if self.fused_fwd:
+            # tile flags, launch epoch, done ticket, error word (zeroed once)
+            self.wf_sync = torch.zeros(260, dtype=torch.int32, device=dev)
         if self.xact:
             self._init_xact(batch)
         self._refresh_bf16()
@@ -312,11 +329,15 @@ class WideMlpTrainer:
         cur = [self.Wb[l][p] for l in range(L)]       # this step's weights
         nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
         self.H[0] = self._xb_rows(bi)  # this batch's bf16 rows (a view: no copy)
-        for l in range(L - 1):
-            _, b = self.views[l]
-            self._gemm(f"f{l}", self.H[l], cur[l], bias=b, relu=True, obf=self.H[l + 1])
-            if self.xact:
-                self._gather(self.Hall[l + 1])
+        if self.fused_fwd:
+            C.wide_fwd2(self.H[0], cur[0], self.views[0][1], self.H[1], cur[1], self.views[1][1],
+                        self.H[2], Bt, d[0], self.Cp, self.tctr, self.wf_sync)
+        else:
+            for l in range(L - 1):
+                _, b = self.views[l]
+                self._gemm(f"f{l}", self.H[l], cur[l], bias=b, relu=True, obf=self.H[l + 1])
+                if self.xact:
+                    self._gather(self.Hall[l + 1])
         _, b = self.views[L - 1]
         if self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
             # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
@@ -493,6 +514,11 @@ class WideMlpTrainer:
             # a layer-0 update tile gave up waiting for its dZ_1 block (bounded
             # in-launch hand-off): the step's weights are not valid
             raise RuntimeError("fused wide backward: an in-launch hand-off timed out")
+        if self.fused_fwd and int(self.wf_sync[258].item()):
+            self.wf_sync[258] = 0
+            # a layer-2 workgroup gave up waiting for its layer-1 tiles (the grid
+            # was not co-resident): that step's activations are not valid
+            raise RuntimeError("fused wide forward: an in-launch hand-off timed out")
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         self.synchronize()

@@ -336,3 +336,54 @@ def test_wide_fused_backward_in_graph_matches_eager():
     b.train_steps(12)
     a.synchronize(); b.synchronize()
     assert torch.equal(a.P.cpu(), b.P.cpu())
+
+
+@pytest.mark.parametrize("M,K1", [(64, 784), (40, 784), (64, 1024), (17, 520)])
+def test_wide_fused_forward_matches_two_launches(M, K1):
+    """kernels/wide_fwd.hip: both hidden layers in one launch, bit-exact with
+    gemm_rows64 (layer 1) + gemm_skinny NT (layer 2), over repeated launches
+    (the device-side flag epoch advances) and against fp32 torch."""
+    C = require_native()
+    if not C.wide_fwd2_supported(0):
+        pytest.skip("device cannot hold the 256-workgroup grid")
+    g = torch.Generator().manual_seed(M + K1)
+    X = (0.5 * torch.randn(M, K1, generator=g)).to(torch.bfloat16).to(DEV)
+    W1 = (torch.randn(4096, K1, generator=g) / K1 ** 0.5).to(torch.bfloat16).to(DEV)
+    W2 = (torch.randn(4096, 4096, generator=g) / 64).to(torch.bfloat16).to(DEV)
+    b1 = (0.1 * torch.randn(4096, generator=g)).to(DEV)
+    b2 = (0.1 * torch.randn(4096, generator=g)).to(DEV)
+    ws = torch.zeros(4 * 64 * 4096, device=DEV)
+    ctr = torch.zeros(64, dtype=torch.int32, device=DEV)
+    sync = torch.zeros(260, dtype=torch.int32, device=DEV)
+    bf = dict(dtype=torch.bfloat16, device=DEV)
+    H1r, H2r = torch.zeros(M, 4096, **bf), torch.zeros(M, 4096, **bf)
+    C.gemm_bf16_nt_fused(X, W1, M, 4096, K1, bias=b1, relu=True, obf=H1r, splits=0)
+    C.gemm_skinny(H1r, W2, M, 4096, 4096, bias=b2, relu=True, obf=H2r, ws=ws, ctr=ctr)
+    for it in range(3):
+        H1, H2 = torch.full((M, 4096), 7.0, **bf), torch.full((M, 4096), 7.0, **bf)
+        C.wide_fwd2(X, W1, b1, H1, W2, b2, H2, M, K1, ws, ctr, sync)
+        torch.cuda.synchronize()
+        assert int(sync[258].item()) == 0, "hand-off timed out"
+        assert int(sync[256].item()) == it + 1  # the epoch advanced once per launch
+        assert torch.equal(H1, H1r), it
+        assert torch.equal(H2, H2r), it
+    assert int(ctr.abs().sum().item()) == 0 and int(sync[257].item()) == 0
+    h1 = torch.relu(X.float() @ W1.float().t() + b1)
+    assert (H1.float() - h1).abs().max().item() < 2e-2 * (1 + h1.abs().max().item())
+    h2 = torch.relu(H1.float() @ W2.float().t() + b2)
+    assert (H2.float() - h2).abs().max().item() < 2e-2 * (1 + h2.abs().max().item())
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_wide_fused_forward_engine_is_bit_identical(graph):
+    spec = MlpSpec((784, 4096, 4096, 10))
+    ds = synthetic_mnist(64 * 3, seed=17)
+    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=graph, fused_fwd=False)
+    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=graph, fused_fwd=True)
+    if not b.fused_fwd:
+        pytest.skip("fused forward unavailable on this device")
+    a.train_steps(7)
+    b.train_steps(7)
+    a.synchronize(); b.synchronize()
+    assert torch.equal(a.P.cpu(), b.P.cpu())
+    assert torch.equal(a.H[2].cpu(), b.H[2].cpu())

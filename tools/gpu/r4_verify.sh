@@ -10,3 +10,5 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 for k in 1 2 3; do timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${T}_bench20_$k.json 2>/dev/null; cut -c1-150 gpurun_out/${T}_bench20_$k.json; done
 timeout -k 10 200 python bench.py --gpus 1 --steps 2000 --warmup 200 > gpurun_out/${T}_bench2000.json 2>/dev/null && cut -c1-150 gpurun_out/${T}_bench2000.json
 timeout -k 10 200 python bench.py --gpus 1 --steps 2000 --warmup 200 --model 784-128-10 > gpurun_out/${T}_bench2000_784_128_10.json 2>/dev/null && cut -c1-150 gpurun_out/${T}_bench2000_784_128_10.json
+# the N > 1 bench path end to end: 2 ranks sharing the one GPU (gloo group)
+timeout -k 10 400 python bench.py --gpus 2 --rehearse-one-gpu --steps 2000 --warmup 200 > gpurun_out/${T}_bench2000_reh2.json 2> gpurun_out/${T}_bench2000_reh2.err && cut -c1-200 gpurun_out/${T}_bench2000_reh2.json

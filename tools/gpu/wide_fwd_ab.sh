@@ -1,0 +1,17 @@
+# Fused wide forward (kernels/wide_fwd.hip) against the two-launch forward:
+# its tests, alternating benches, a kernel trace and the phase stamps.
+set -e
+T=${1:-wf}
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wide.py -x -q -k "fused_forward" --timeout 120 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -40 gpurun_out/${T}_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_tests.log
+for e in 0 1; do WF_EARLY_DMA=$e timeout -k 10 120 python tools/wide_fwd_stamps.py > gpurun_out/${T}_stamps_e$e.json && cut -c1-700 gpurun_out/${T}_stamps_e$e.json; done
+for k in 1 2; do
+  for f in 0 1; do
+    HIPDSML_WIDE_FUSED_FWD=$f timeout -k 10 200 python bench_wide.py --steps 200 --warmup 20 2>/dev/null > gpurun_out/${T}_bench_f${f}_$k.json
+    echo "fused_fwd=$f $(cut -c1-110 gpurun_out/${T}_bench_f${f}_$k.json)"
+  done
+done
+export HIPDSML_WIDE_FUSED_FWD=1
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python $GRAFT_REPO_ROOT/bench_wide.py --steps 100 --warmup 10 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 && cd $GRAFT_REPO_ROOT && python tools/rocpd_summary.py gpurun_out/${T}_prof/run_results.db --skip 200 --csv gpurun_out/${T}_kernels.csv | cut -c1-150
