@@ -439,8 +439,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                      c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> ctr,
                                      c10::optional<torch::Tensor> bgrad,
                                      c10::optional<torch::Tensor> bsgd) {
-    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A, B 2-D rows");
-    TORCH_CHECK(A.size(0) >= M && B.size(0) >= N && A.size(1) >= K && B.size(1) >= K, "A/B too small");
+    // A 3-D = k-blocked [K / 32 blocks][rows][32] (rows64 only): element (m, k) at
+    // A[k / 32][m][k % 32]
+    const bool ablk = A.dim() == 3;
+    TORCH_CHECK(!ablk || (splits == 0 && A.stride(2) == 1 && A.stride(1) == 32 && A.size(2) == 32 &&
+                          A.size(0) * 32 >= K && A.size(1) >= M), "k-blocked A: [>= K/32][>= M][32], splits=0");
+    TORCH_CHECK((ablk || (A.dim() == 2 && A.stride(1) == 1)) && B.dim() == 2 && B.stride(1) == 1, "A, B 2-D rows");
+    TORCH_CHECK((ablk || (A.size(0) >= M && A.size(1) >= K)) && B.size(0) >= N && B.size(1) >= K, "A/B too small");
     auto chk2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
       TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
     };
@@ -460,7 +465,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (bsgd) { check_f32(*bsgd, "bsgd"); TORCH_CHECK(bsgd->numel() >= M, "bsgd"); e.bsgd = bsgd->data_ptr<float>(); }
     if (splits == 0) {  // batch-row kernel: full K per block, epilogue fused, no slabs
       hip_ok(gemm_bf16_rows64(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), (int)M, (int)N,
-                              (int)K, e, cur_stream()), "gemm_bf16_rows64");
+                              (int)K, e, cur_stream(), ablk), "gemm_bf16_rows64");
       return 1;
     }
     const int S = gemm_bf16_num_splits((int)K, (int)splits);

@@ -240,8 +240,10 @@ int gemm_bf16_num_splits(int K, int splits);
 // Batch-row GEMM (C = A . B^T with <= 64 rows per block, 16 columns per block,
 // full K per block split across its 4 waves) with the whole epilogue fused
 // (alpha, bias, ReLU, ReLU'-mask, fp32 / bf16 / transposed bf16 outputs).
+// a_blk: A stored k-blocked, element (m, k) at A[(k / 32) * lda + 32 m + k % 32]
+// (one 16-row fragment load = 1 KiB contiguous instead of 16 half lines).
 hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M,
-                            int N, int K, const GemmEpi& epi, hipStream_t s);
+                            int N, int K, const GemmEpi& epi, hipStream_t s, bool a_blk = false);
 // out = epi(alpha * sum_s Cp[s] + bias): relu, ReLU'-mask (bf16 mask > 0), fp32 / bf16 /
 // transposed-bf16 outputs (each nullable).
 hipError_t gemm_epilogue(const float* Cp, int S, int M, int N, float alpha, const float* bias,

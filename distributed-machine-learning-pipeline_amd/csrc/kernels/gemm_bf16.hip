@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 6) void gemm_bf16_nt_k(
 // ---------------------------------------------------------------------------
 constexpr int kR64Pad = 17;  // LDS row stride (floats) of a 16-wide partial tile
 
-template <int U, int WAVES>
+template <int U, int WAVES, bool ABLK = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __restrict__ A, int64_t lda,
                                                      const uint16_t* __restrict__ B, int64_t ldb,
                                                      int M, int N, int K, GemmEpi epi, int vec) {
@@ -392,7 +392,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
       fb[u] = *reinterpret_cast<const uint4*>(pb + kc);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        fa[u][t] = *reinterpret_cast<const uint4*>(A + (int64_t)ra[t] * lda + kc);
+        fa[u][t] = *reinterpret_cast<const uint4*>(
+            ABLK ? A + (int64_t)(kc >> 5) * lda + 32 * ra[t] + (kc & 31) : A + (int64_t)ra[t] * lda + kc);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -482,8 +483,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
 }
 
 hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M,
-                            int N, int K, const GemmEpi& epi, hipStream_t s) {
+                            int N, int K, const GemmEpi& epi, hipStream_t s, bool a_blk) {
   if (M <= 0 || N <= 0 || K <= 0 || (K & 7) || (lda & 7) || (ldb & 7)) return hipErrorInvalidValue;
+  if (a_blk && (lda < 32 * (int64_t)M)) return hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B) & 15) return hipErrorInvalidValue;
   if (epi.sgdW || epi.bgrad || epi.bsgd) return hipErrorInvalidValue;
   // vector stores when every written row run is aligned and whole
@@ -497,6 +499,10 @@ hipError_t gemm_bf16_rows64(const uint16_t* A, int64_t lda, const uint16_t* B, i
   // whole K range (<= 128) is ONE load batch instead of two dependent rounds.
   if (K >= 8 * 32 * 8)
     hipLaunchKernelGGL((gemm_rows64_k<8, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  else if (K >= 4 * 32 * 4 && K <= 8 * 128 && a_blk)
+    hipLaunchKernelGGL((gemm_rows64_k<4, 8, true>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
+  else if (a_blk)
+    return hipErrorInvalidValue;  // k-blocked A: the input-layer shape only
   else if (K >= 4 * 32 * 4 && K <= 8 * 128)
     hipLaunchKernelGGL((gemm_rows64_k<4, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, M, N, K, epi, vec);
   else if (K >= 4 * 32 * 4)

@@ -63,7 +63,7 @@ class WideMlpTrainer:
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
                  gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False,
                  fused_bwd: Optional[bool] = None, bwd_rows: int = 0,
-                 fused_fwd: Optional[bool] = None):
+                 fused_fwd: Optional[bool] = None, xblk: Optional[bool] = None):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -215,6 +215,20 @@ class WideMlpTrainer:
         if self.fused_fwd:
             # tile flags, launch epoch, done ticket, error word (zeroed once)
             self.wf_sync = torch.zeros(260, dtype=torch.int32, device=dev)
+        # xblk: the input-layer GEMM reads a k-blocked copy of the shard
+        # ([K/32][rows][32] bf16): a 16-row MFMA fragment load is then 1 KiB
+        # contiguous instead of 16 half cache lines (gemm_bf16.hip rows64 ABLK).
+        # Same products, same order: bit-identical.
+        if xblk is None:
+            xblk = os.environ.get("HIPDSML_WIDE_XBLK", "1") == "1"
+        self.Xblk = None
+        if xblk and not self.xact and not self.fused_fwd and 512 <= d[0] <= 1024 and batch <= 64 \
+                and (self.gemm == "rows64" or d[0] < 1024):
+            nb = _rup(d[0], 32) // 32
+            xp = torch.zeros(self.Xb.shape[0], nb * 32, **bf)
+            xp[:, :self.Xb.shape[1]] = self.Xb
+            self.Xblk = xp.view(-1, nb, 32).transpose(0, 1).contiguous()
+            del xp
         if self.xact:
             self._init_xact(batch)
         self._refresh_bf16()
@@ -335,7 +349,8 @@ class WideMlpTrainer:
         else:
             for l in range(L - 1):
                 _, b = self.views[l]
-                self._gemm(f"f{l}", self.H[l], cur[l], bias=b, relu=True, obf=self.H[l + 1])
+                A = self.Xblk[:, r0:r0 + Bt] if l == 0 and self.Xblk is not None else self.H[l]
+                self._gemm(f"f{l}", A, cur[l], bias=b, relu=True, obf=self.H[l + 1])
                 if self.xact:
                     self._gather(self.Hall[l + 1])
         _, b = self.views[L - 1]

@@ -387,3 +387,38 @@ def test_wide_fused_forward_engine_is_bit_identical(graph):
     a.synchronize(); b.synchronize()
     assert torch.equal(a.P.cpu(), b.P.cpu())
     assert torch.equal(a.H[2].cpu(), b.H[2].cpu())
+
+
+@pytest.mark.parametrize("M,K", [(64, 784), (40, 520), (64, 1024)])
+def test_gemm_rows64_kblocked_a_is_bit_exact(M, K):
+    """rows64 reading A from a k-blocked [K/32][rows][32] copy: same products
+    in the same order as the row-major A, so bit-identical outputs."""
+    C = require_native()
+    g = torch.Generator().manual_seed(M * K)
+    rows = 3 * M
+    A = torch.randn(rows, K, generator=g).to(torch.bfloat16).to(DEV)
+    B = (torch.randn(4096, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(4096, generator=g).to(DEV)
+    nb = (K + 31) // 32
+    Ap = torch.zeros(rows, nb * 32, dtype=torch.bfloat16, device=DEV)
+    Ap[:, :K] = A
+    Ablk = Ap.view(rows, nb, 32).transpose(0, 1).contiguous()
+    r0 = M  # a batch offset inside the shard
+    o1 = torch.zeros(M, 4096, dtype=torch.bfloat16, device=DEV)
+    o2 = torch.zeros_like(o1)
+    C.gemm_bf16_nt_fused(A[r0:r0 + M], B, M, 4096, K, bias=bias, relu=True, obf=o1, splits=0)
+    C.gemm_bf16_nt_fused(Ablk[:, r0:r0 + M], B, M, 4096, K, bias=bias, relu=True, obf=o2, splits=0)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+
+
+def test_wide_kblocked_input_engine_is_bit_identical():
+    spec = MlpSpec((784, 512, 256, 10))
+    ds = synthetic_mnist(64 * 3, seed=19)
+    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, xblk=False)
+    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, xblk=True)
+    assert b.Xblk is not None
+    a.train_steps(7)
+    b.train_steps(7)
+    a.synchronize(); b.synchronize()
+    assert torch.equal(a.P.cpu(), b.P.cpu())
