@@ -352,6 +352,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
                                                      int M, int N, int K, GemmEpi epi, int vec) {
   constexpr int NT = 64 * WAVES;
   __shared__ float red[WAVES * 64 * kR64Pad];
+  // ABLK: the block's 16 weight rows (K <= 1024), whole, + a tail instruction's overrun
+  __shared__ __attribute__((aligned(16))) char bimg[ABLK ? 16 * 1024 * 2 + 1024 : 16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 64;
@@ -383,26 +385,65 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows64_k(const uint16_t* __re
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kb; k0 < ke; k0 += 32 * U) {
-    uint4 fa[U][4], fb[U];
+  if constexpr (ABLK) {
+    // The input layer (K <= 1024: one U-round per wave).  A (the batch rows) is
+    // k-blocked, so each fragment load is 1 KiB contiguous; B (this block's 16
+    // weight rows, one contiguous run when ldb == K) is copied whole into LDS
+    // by LDS-DMA, 1 KiB whole lines per instruction, instead of 16 half lines
+    // per fragment load.  Same operands, same MFMA order: bit-exact.
+    const int K8 = K / 8, chunks = 16 * K8;
+    uint4 fa[U][4];
+    if (kb < ke) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = k0 + 32 * u + 8 * g;
-      const int kc = kk < ke ? kk : kb;  // per-lane clamp: never past the row
-      fb[u] = *reinterpret_cast<const uint4*>(pb + kc);
+      for (int u = 0; u < U; ++u) {
+        const int kk = kb + 32 * u + 8 * g;
+        const int kc = kk < ke ? kk : kb;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        fa[u][t] = *reinterpret_cast<const uint4*>(
-            ABLK ? A + (int64_t)(kc >> 5) * lda + 32 * ra[t] + (kc & 31) : A + (int64_t)ra[t] * lda + kc);
+        for (int t = 0; t < 4; ++t)
+          fa[u][t] = *reinterpret_cast<const uint4*>(A + (int64_t)(kc >> 5) * lda + 32 * ra[t] + (kc & 31));
+      }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    for (int j = w; 64 * j < chunks; j += WAVES) {
+      const int c = min(64 * j + lane, chunks - 1);  // the tail instruction re-reads the last chunk
+      const int r = c / K8, col = c - r * K8;
+      const int n = min(n0 + r, N - 1);
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(B + (int64_t)n * ldb + 8 * col),
+          (__attribute__((address_space(3))) void*)(bimg + 1024 * j), 16, 0, 0);
+    }
+    __syncthreads();  // every wave's DMA landed (the barrier's vmcnt(0) covers it)
+    if (kb < ke) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool kv = k0 + 32 * u + 8 * g < ke;
-      const uint4 b = (kv && vb) ? fb[u] : zero_u4();
+      for (int u = 0; u < U; ++u) {
+        const int kk = kb + 32 * u + 8 * g;
+        const bool kv = kk < ke;
+        const int kc = kv ? kk : kb;
+        const uint4 bl = *reinterpret_cast<const uint4*>(bimg + 16 * (i * K8 + (kc >> 3)));
+        const uint4 b = (kv && vb) ? bl : zero_u4();
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma_bf16((kv && va[t]) ? fa[u][t] : zero_u4(), b, acc[t]);
+        for (int t = 0; t < 4; ++t) acc[t] = mfma_bf16((kv && va[t]) ? fa[u][t] : zero_u4(), b, acc[t]);
+      }
+    }
+  } else {
+    for (int k0 = kb; k0 < ke; k0 += 32 * U) {
+      uint4 fa[U][4], fb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k0 + 32 * u + 8 * g;
+        const int kc = kk < ke ? kk : kb;  // per-lane clamp: never past the row
+        fb[u] = *reinterpret_cast<const uint4*>(pb + kc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fa[u][t] = *reinterpret_cast<const uint4*>(A + (int64_t)ra[t] * lda + kc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool kv = k0 + 32 * u + 8 * g < ke;
+        const uint4 b = (kv && vb) ? fb[u] : zero_u4();
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] = mfma_bf16((kv && va[t]) ? fa[u][t] : zero_u4(), b, acc[t]);
+      }
     }
   }
   // partials -> LDS, then the fixed-order 4-way sum (deterministic)
