@@ -39,6 +39,7 @@ Reference hot loop replaced: client.go:112-202.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -139,8 +140,6 @@ class WideMlpTrainer:
         # per-layer RCCL all-reduces and updates on the comm stream are
         # captured too (fork/join of the comm stream inside the capture); only
         # the torch.distributed fallback (sync='torch', e.g. gloo) stays eager.
-        import os
-
         self.comm = None
         if self.ctx.is_distributed and (sync in ("rccl", "ring") or
                                         (sync == "xact" and self.ctx.backend == "nccl")):
@@ -226,7 +225,7 @@ class WideMlpTrainer:
                 and (self.gemm == "rows64" or d[0] < 1024):
             nb = _rup(d[0], 32) // 32
             xp = torch.zeros(self.Xb.shape[0], nb * 32, **bf)
-            xp[:, :self.Xb.shape[1]] = self.Xb
+            xp[:, :d[0]] = self.Xb[:, :d[0]]
             self.Xblk = xp.view(-1, nb, 32).transpose(0, 1).contiguous()
             del xp
         if self.xact:
