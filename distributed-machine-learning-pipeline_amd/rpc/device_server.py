@@ -395,7 +395,6 @@ class GPUDeviceServicer:
         seg = (-(-elems // n) + al - 1) // al * al
         off = [min(i * seg, elems) * es for i in range(n + 1)]
         nxt = peers[(r + 1) % n]
-        scratch = self.dev.scratch_addr
         for step in range(2 * (n - 1)):
             if cid in self._aborted_comms:
                 raise RuntimeError(f"communicator {cid} aborted")
@@ -414,8 +413,7 @@ class GPUDeviceServicer:
                 raise RuntimeError(f"ring step {step}: {len(data)} B from the predecessor, expected {rl}")
             if rl:
                 if step < n - 1:
-                    self.dev.write(scratch, data, internal=True, record=False)
-                    self.dev.reduce(addr + off[ri], scratch, rl, dtype, op)
+                    self.dev.reduce_bytes(addr + off[ri], data, dtype, op)
                 else:
                     self.dev.write(addr + off[ri], data, internal=True, record=False)
         self.dev.synchronize()

@@ -202,6 +202,12 @@ class _Device:
     def scale(self, addr: int, nbytes: int, dtype: int, alpha: float) -> None:
         raise NotImplementedError
 
+    def reduce_bytes(self, dst: int, data: bytes, dtype: int, op: int) -> None:
+        """dst <- dst (op) data for bytes that arrived off the wire (a ring
+        step's segment); default: through the private scratch window."""
+        self.write(self.scratch_addr, data, internal=True, record=False)
+        self.reduce(dst, self.scratch_addr, len(data), dtype, op)
+
     def tensor(self, addr: int, nbytes: int, dtype: torch.dtype, internal: bool = True) -> torch.Tensor:
         raise NotImplementedError
 
@@ -251,6 +257,20 @@ class HostDevice(_Device):
         t = self.tensor(addr, nbytes, TORCH_DTYPES[dtype])
         t.copy_((t.float() * alpha).to(t.dtype))
 
+    def reduce_bytes(self, dst, data, dtype, op):
+        # host memory: reduce straight from the received buffer (no scratch copy)
+        from ..ops.functional import reduce_ref
+
+        td = TORCH_DTYPES[dtype]
+        if len(data) % DT_SIZE[dtype]:
+            raise ValueError("byte count is not a multiple of the element size")
+        a = self.tensor(dst, len(data), td)
+        b = torch.frombuffer(bytearray(data) if isinstance(data, bytes) else data, dtype=td)
+        if op == 0 and td not in (torch.uint8, torch.bfloat16, torch.float16):  # SUM
+            a.add_(b)
+        else:
+            a.copy_(reduce_ref(a, b, op))
+
 
 class _CudaArrayView:
     """__cuda_array_interface__ shim so torch can alias arena memory."""
@@ -273,6 +293,7 @@ class HipDevice(_Device):
         torch.cuda.set_device(self.gpu)
         self.arena = C.DeviceArena(self.gpu, mem_size + scratch_size, BASE_ADDR)
         self.copy = C.CopyEngine(self.gpu, staging_bytes)
+        self._views: dict = {}
 
     def write(self, addr, data, internal=False, record=True):
         self.check(addr, len(data), internal)
@@ -293,10 +314,20 @@ class HipDevice(_Device):
 
     def tensor(self, addr, nbytes, dtype, internal=True):
         self.check(addr, nbytes, internal)
+        # views of the (never moving) arena are cached: building one through
+        # __cuda_array_interface__ costs tens of us of Python per RPC
+        key = (addr, nbytes, dtype)
+        t = self._views.get(key)
+        if t is not None:
+            return t
         ptr = self.arena.ptr(addr, nbytes)
         with torch.cuda.device(self.gpu):
             raw = torch.as_tensor(_CudaArrayView(ptr, nbytes), device=f"cuda:{self.gpu}")
-        return raw.view(dtype)
+        t = raw.view(dtype)
+        if len(self._views) >= 256:
+            self._views.clear()
+        self._views[key] = t
+        return t
 
     def scale(self, addr, nbytes, dtype, alpha):
         from ..ops.functional import scale_
