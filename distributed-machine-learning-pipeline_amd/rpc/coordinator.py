@@ -27,7 +27,6 @@ Two data planes for AllReduceRing:
 from __future__ import annotations
 
 import logging
-import os
 import threading
 import time
 from concurrent.futures import FIRST_EXCEPTION, ThreadPoolExecutor, wait
@@ -114,37 +113,6 @@ class GPUCoordinatorServicer:
             done, _ = wait(futs, return_when=FIRST_EXCEPTION)
             if any(f.exception() is not None for f in done):
                 on_error()  # e.g. abort peers still blocked on the failed rank
-        errs, out = [], []
-        for f in futs:
-            try:
-                out.append(f.result())
-            except Exception as e:  # collect every failure
-                errs.append(e)
-                out.append(None)
-        if errs:
-            raise CollectiveError("; ".join(str(e) for e in errs))
-        return out
-
-    def _fanout(self, calls, on_error=None):
-        """One unary RPC per device, all issued at once as gRPC futures (the
-        C core's completion queue, no pool-thread hand-off per call: the
-        collective's dispatch is on the latency path of every AllReduceRing).
-        Same contract as _parallel: every result or every failure collected,
-        and `on_error` runs as soon as the FIRST call fails (a done-callback),
-        so peers blocked on the failed rank are aborted before we wait on them."""
-        if os.environ.get("HIPDSML_COORD_FUTURES", "1") != "1":  # A/B: the thread-pool form
-            return self._parallel([(lambda m=m, r=r: m(r, timeout=self.rpc_timeout)) for m, r in calls],
-                                  on_error=on_error)
-        fired = threading.Event()
-
-        def done(f):
-            if f.exception() is not None and on_error is not None and not fired.is_set():
-                fired.set()
-                threading.Thread(target=on_error, daemon=True).start()
-
-        futs = [m.future(req, timeout=self.rpc_timeout) for m, req in calls]
-        for f in futs:
-            f.add_done_callback(done)
         errs, out = [], []
         for f in futs:
             try:
@@ -347,10 +315,10 @@ class GPUCoordinatorServicer:
             elif op.algo == "coordinator-ring":
                 self._allreduce_rpc_ring(c, op)
             elif op.algo == "xgmi":  # "pg" comms of GPU devices: one launch over peer memory
-                self._fanout([
-                    (d.stub.DeviceAllReduce, pb.DeviceAllReduceRequest(
+                self._parallel([
+                    (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                         commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype,
-                        op=op.op, algo="xgmi"))
+                        op=op.op, algo="xgmi"), timeout=self.rpc_timeout))
                     for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
             else:  # "stream-ring" (default) / "device-ring": devices drive the ring themselves
                 self._allreduce_device_ring(c, op)
@@ -367,10 +335,10 @@ class GPUCoordinatorServicer:
 
     def _allreduce_rccl(self, c: Communicator, op) -> None:
         algo = op.algo if op.algo in ("ring", "rccl") else "ring"
-        self._fanout([
-            (d.stub.DeviceAllReduce, pb.DeviceAllReduceRequest(
+        self._parallel([
+            (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                 commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
-                algo=algo, chunkBytes=op.chunkBytes))
+                algo=algo, chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
             for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
 
     def _abort_all(self, c: Communicator, reason: str) -> None:
@@ -378,11 +346,11 @@ class GPUCoordinatorServicer:
             self._pool.submit(self._safe_abort, d, c.id, reason)
 
     def _allreduce_device_ring(self, c: Communicator, op) -> None:
-        self._fanout([
-            (d.stub.DeviceAllReduce, pb.DeviceAllReduceRequest(
+        self._parallel([
+            (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                 commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype, op=op.op,
                 algo="rpc-ring" if op.algo == "device-ring" else "stream-ring",
-                chunkBytes=op.chunkBytes))
+                chunkBytes=op.chunkBytes), timeout=self.rpc_timeout))
             for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
 
     def _wait_stream(self, d: DeviceInfo, sid: int) -> None:
