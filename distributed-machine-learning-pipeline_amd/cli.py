@@ -54,8 +54,11 @@ def cmd_device_server(a) -> int:
 def cmd_coordinator(a) -> int:
     from .rpc.coordinator import start_coordinator
 
+    # the "pg" communicators' TCP store: devices on other hosts must reach it,
+    # so it binds to the coordinator's own address unless told otherwise
+    store_host = a.store_host or (a.host if a.host not in ("", "0.0.0.0", "::") else "127.0.0.1")
     server, addr, svc = start_coordinator(f"{a.host}:{a.port}", health_interval=a.health_interval,
-                                          health_timeout=a.health_timeout)
+                                          health_timeout=a.health_timeout, store_host=store_host)
     print(f"GPU Coordinator server listening on port {addr.rsplit(':', 1)[1]}", flush=True)
     _serve_forever([svc.stop, lambda: server.stop(1)])
     return 0
@@ -162,6 +165,10 @@ def main(argv=None) -> int:
     c.add_argument("--port", type=int, default=50051)
     c.add_argument("--health-interval", type=float, default=5.0)
     c.add_argument("--health-timeout", type=float, default=2.0)
+    c.add_argument("--store-host", default="",
+                   help="address the process-group store of CommInit backend 'pg' binds to and "
+                        "the device servers connect to (default: --host, or 127.0.0.1 when "
+                        "--host is a wildcard)")
     lo = sub.add_parser("local")
     lo.add_argument("--gpus", type=int, default=1)
     lo.add_argument("--backend", default="hip", choices=["host", "hip"])

@@ -103,6 +103,9 @@ int64_t layout_ws_end(const MlpDesc& d) {
 struct PyMlpRunner {
   MlpDesc d;
   std::vector<torch::Tensor> keep;  // keep tensors alive while the runner exists
+  // persistent-step operands: one slot each, replaced (not appended) on every
+  // set_* call, so a released table is really freed
+  torch::Tensor keep_xbuf, keep_err, keep_gram, keep_xall, keep_xact_in;
   std::unique_ptr<MlpRunner> r;
   hipStream_t stream = nullptr;
   bool own_stream = true;
@@ -634,88 +637,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (py::handle it : layers) v.push_back(wg_layer(it));
     hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
   }, py::arg("layers"), py::arg("tile") = 0);
-  m.def("wide_bwd", [wg_layer, bf16p](py::list layers, py::object fused, int rows,
-                                      c10::optional<torch::Tensor> dzo_, c10::optional<torch::Tensor> part_,
-                                      c10::optional<torch::Tensor> tick_, c10::optional<torch::Tensor> ready) {
-    // layers as wgrad_sgd_multi; fused: None (plain updates) or the index of the
-    // fused layer (must be 0); its dZ output dzo [M x K] bf16; every later layer
-    // whose Z is dzo waits on `ready` (int32, K / 64 counters, zero)
-    std::vector<WgLayer> v;
-    for (py::handle it : layers) v.push_back(wg_layer(it));
-    std::vector<WbFused> f(v.size());
-    if (!fused.is_none()) {
-      const int j = fused.cast<int>();
-      TORCH_CHECK(j == 0 && !v.empty(), "wide_bwd: the fused layer must be the first");
-      const WgLayer& L = v[0];
-      TORCH_CHECK(dzo_ && part_ && tick_, "wide_bwd: a fused layer needs dzo, part and tick");
-      const torch::Tensor &dzo = *dzo_, &part = *part_, &tick = *tick_;
-      TORCH_CHECK(rows >= 64 && rows % 64 == 0 && L.N % rows == 0, "wide_bwd: rows per slice");
-      TORCH_CHECK(dzo.dim() == 2 && dzo.stride(1) == 1 && dzo.size(0) >= L.M && dzo.size(1) >= L.K, "dzo shape");
-      const int kt = (L.K + 63) / 64, S = L.N / rows;
-      check_f32(part, "part");
-      TORCH_CHECK(part.numel() >= (int64_t)S * kt * 4096, "wide_bwd: partial slab too small");
-      TORCH_CHECK(tick.is_cuda() && tick.scalar_type() == torch::kInt32 && tick.numel() >= kt, "tick");
-      WbFused& F = f[0];
-      F.fused = 1; F.slices = S; F.rows = rows;
-      F.dzo = bf16p(dzo, "dzo"); F.lddo = dzo.stride(0);
-      F.part = part.data_ptr<float>(); F.tick = tick.data_ptr<int32_t>();
-      for (size_t q = 1; q < v.size(); ++q) {
-        if (v[q].Z != F.dzo) continue;
-        TORCH_CHECK(F.ready == nullptr, "wide_bwd: one layer may consume the fused layer's output");
-        TORCH_CHECK(ready && ready->is_cuda() && ready->scalar_type() == torch::kInt32 && ready->numel() >= kt,
-                    "wide_bwd: ready counters");
-        F.ready = ready->data_ptr<int32_t>();
-        F.nready = (v[q].K + 63) / 64;
-        f[q].wait_prev = 1;
-      }
-    }
-    hip_ok(wide_bwd(v.data(), f.data(), (int)v.size(), cur_stream()), "wide_bwd");
-  }, py::arg("layers"), py::arg("fused"), py::arg("rows") = 1024, py::arg("dzo") = py::none(),
-     py::arg("part") = py::none(), py::arg("tick") = py::none(), py::arg("ready") = py::none());
-  m.def("wide_bwd_errors", [](bool clear) { return wide_bwd_errors(clear); }, py::arg("clear") = true);
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");
     return v;
   });
   m.def("gemm_skinny_set_stamping", &gemm_skinny_set_stamping);
-  m.def("wide_fwd2", [bf16p](torch::Tensor X, torch::Tensor W1, torch::Tensor b1, torch::Tensor H1,
-                             torch::Tensor W2, torch::Tensor b2, torch::Tensor H2, int64_t M, int64_t K1,
-                             torch::Tensor ws, torch::Tensor ctr, torch::Tensor sync) {
-    auto rows = [](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
-      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm,
-                  " shape");
-    };
-    rows(X, M, K1, "X");
-    rows(W1, 4096, K1, "W1");
-    rows(H1, M, 4096, "H1");
-    rows(W2, 4096, 4096, "W2");
-    rows(H2, M, 4096, "H2");
-    check_f32(b1, "b1");
-    check_f32(b2, "b2");
-    check_f32(ws, "ws");
-    TORCH_CHECK(b1.numel() >= 4096 && b2.numel() >= 4096, "biases");
-    TORCH_CHECK(ws.numel() >= 4 * 64 * 4096, "ws too small");
-    check_cuda(ctr, "ctr");
-    check_cuda(sync, "sync");
-    TORCH_CHECK(ctr.scalar_type() == torch::kInt32 && ctr.numel() >= 64, "ctr: int32, >= 64");
-    TORCH_CHECK(sync.scalar_type() == torch::kInt32 && sync.numel() >= 259 && sync.is_contiguous(),
-                "sync: int32, >= 259, contiguous");
-    hip_ok(wide_fwd2(bf16p(X, "X"), X.stride(0), bf16p(W1, "W1"), W1.stride(0), b1.data_ptr<float>(),
-                     bf16p(H1, "H1"), H1.stride(0), bf16p(W2, "W2"), W2.stride(0), b2.data_ptr<float>(),
-                     bf16p(H2, "H2"), H2.stride(0), (int)M, (int)K1, ws.data_ptr<float>(),
-                     ctr.data_ptr<int32_t>(), sync.data_ptr<int32_t>(), cur_stream()),
-           "wide_fwd2");
-  }, py::arg("X"), py::arg("W1"), py::arg("b1"), py::arg("H1"), py::arg("W2"), py::arg("b2"), py::arg("H2"),
-     py::arg("M"), py::arg("K1"), py::arg("ws"), py::arg("ctr"), py::arg("sync"));
-  m.def("wide_fwd2_supported", [](int64_t dev) { return wide_fwd2_supported((int)dev); });
-  m.def("wide_fwd2_stamps", []() {
-    std::vector<uint64_t> v(256 * 8);
-    hip_ok(wide_fwd2_read_stamps(v.data()), "wide_fwd2_read_stamps");
-    return v;
-  });
-  m.def("wide_fwd2_set_stamping", &wide_fwd2_set_stamping);
-  m.def("wide_fwd2_set_early_dma", &wide_fwd2_set_early_dma);
   m.def("gemm_skinny_splits", &gemm_skinny_splits, py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("splits") = 0);
   m.def("hilo_split", [bf16p](torch::Tensor W, torch::Tensor hi, torch::Tensor lo) {
@@ -875,8 +802,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(x == nullptr || Xall.numel() >= (int64_t)x->nranks() * xstride,
                     "Xall holds fewer than nranks shards");
         s.r->set_act_exchange(x, Xall.data_ptr<float>(), xstride, waves);
+        s.keep_xact_in = Xall;
       }, py::arg("exchange").none(true), py::arg("Xall"), py::arg("xstride"), py::arg("waves") = 0,
-           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+           py::keep_alive<1, 2>())
       .def("set_persist", [](PyMlpRunner& s, c10::optional<torch::Tensor> xbuf,
                              c10::optional<torch::Tensor> err, double timeout_ms, PeerExchange* x,
                              int algo) {
@@ -887,8 +815,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                     mlp_persist_xbuf_granules(), "]");
         TORCH_CHECK(err && err->is_cuda() && err->scalar_type() == torch::kInt32 && err->numel() >= 1,
                     "err: int32[1] on the GPU");
-        s.keep.push_back(*xbuf);
-        s.keep.push_back(*err);
+        s.keep_xbuf = *xbuf;
+        s.keep_err = *err;
         s.r->set_persist(reinterpret_cast<uint64_t*>(xbuf->data_ptr<int64_t>()),
                          reinterpret_cast<uint32_t*>(err->data_ptr<int32_t>()), timeout_ms, x, algo);
       }, py::arg("xbuf").none(true), py::arg("err") = py::none(), py::arg("timeout_ms") = 2000.0,
@@ -906,7 +834,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(g.is_contiguous() && g.numel() >= (int64_t)s.r->desc().nbatches * 64 * 64,
                     "gram: contiguous float[nbatches][64][64]");
         TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr<float>()) & 15) == 0, "gram: 16-B aligned");
-        s.keep.push_back(g);
+        s.keep_gram = g;
         s.r->set_persist_gram(g.data_ptr<float>(), g.numel());
       }, py::arg("gram"),
            "single-replica persistent step: the per-batch Gram table G1T[b][m'][m] = "
@@ -916,11 +844,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         check_f32(x, "xsw");
         TORCH_CHECK(x.is_contiguous() && stride > 0 && stride % 4 == 0, "xsw: contiguous, stride % 4 == 0");
         TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr<float>()) & 15) == 0, "xsw: 16-B aligned");
-        s.keep.push_back(x);
+        s.keep_xall = x;
         s.r->set_persist_xall(x.data_ptr<float>(), stride, x.numel());
       }, py::arg("xsw"), py::arg("stride"),
            "exchange-free data-parallel persistent step (pkx): every replica's input shard in "
            "MFMA fragment order (parallel/xchg.py swizzle_inputs), replica r at r * stride floats")
+      .def("release_xall", [](PyMlpRunner& s) {
+        TORCH_CHECK(s.r->exchange_mode() != 2, "release_xall: the activation exchange still reads Xall");
+        s.r->set_persist_xall(nullptr, 0, 0);
+        s.keep_xall = torch::Tensor();
+        s.keep_xact_in = torch::Tensor();
+      }, "drop the runner's references to the replicated input shards (neither pkx nor xact "
+         "runs any more; the next pkx launch would refuse to start without new ones)")
       .def("persist_carry", [](PyMlpRunner& s) { return s.r->persist_carry(); },
            "the hand-off buffer holds the last launch's pipeline state (next partials + correction)")
       .def("exchange_active", [](PyMlpRunner& s) { return s.r->exchange_active(); })

@@ -278,21 +278,6 @@ void gemm_skinny_set_stamping(bool on);
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N,
                        int K, bool nn, int splits, float* slabs, int* tile_ctr, const GemmEpi& epi,
                        hipStream_t s);
-// Both hidden layers of the wide forward in one launch (kernels/wide_fwd.hip):
-// H1 = relu(X W1^T + b1), H2 = relu(H1 W2^T + b2) for 4096-wide layers, M <= 64
-// rows, 512 <= K1 <= 1024; bit-exact with gemm_bf16_rows64 + gemm_skinny.
-// slabs / tile_ctr as gemm_skinny (4 x 64 tiles); sync: 259 ints, zeroed once
-// (tile flags, launch epoch, done ticket, error word at [258]).  Needs the
-// whole 256-workgroup grid co-resident: wide_fwd2_supported(device).
-bool wide_fwd2_supported(int device);
-int wide_fwd2_lds_bytes();
-hipError_t wide_fwd2_read_stamps(uint64_t* host_out);  // [256][8], profiling only
-void wide_fwd2_set_stamping(bool on);
-void wide_fwd2_set_early_dma(bool on);  // testing: W2 streamed from the start
-hipError_t wide_fwd2(const uint16_t* X, int64_t ldx, const uint16_t* W1, int64_t ldw1, const float* b1,
-                     uint16_t* H1, int64_t ldh1, const uint16_t* W2, int64_t ldw2, const float* b2,
-                     uint16_t* H2, int64_t ldh2, int M, int K1, float* slabs, int* tile_ctr, int* sync,
-                     hipStream_t s);
 // Weight gradient from row-major activations (kernels/wgrad_sgd.hip):
 // G = alpha * Z^T X (Z [M x N], X [M x K] bf16, rows padded to 8 columns), then
 // W -= lr * G (+ bf16 copy Wb) when W is given, else G written out; bias -= lr
@@ -337,24 +322,6 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // 64 x 64 everywhere; 0 (auto): 128 for fp32-master layers at M >= 512 rows,
 // else 64.
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
-// Fused backward (kernels/wgrad_sgd.hip wide_bwd): per layer either the plain
-// update tiles, or (fused) the activation gradient dZ_l = (Z . Wh) * (X > 0)
-// folded into the update's pass over W (rows in `slices` slices of `rows`,
-// partials summed in slice order), announcing each 64-column block of dZ_l on
-// `ready` to a following layer with wait_prev (its Z = dzo).  M <= 64.
-struct WbFused {
-  int fused;
-  int slices, rows;
-  uint16_t* dzo;
-  int64_t lddo;
-  float* part;  // >= slices * ceil(K / 64) * 4096 floats
-  int* tick;    // ceil(K / 64), zero, left zero
-  int* ready;   // ceil(K / 64), zero, left zero (nullable)
-  int nready;   // consumers per block: the next layer's k tiles
-  int wait_prev;
-};
-hipError_t wide_bwd(const WgLayer* layers, const WbFused* fused, int n, hipStream_t s);
-uint32_t wide_bwd_errors(bool clear);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 void head_set_debug(int v);

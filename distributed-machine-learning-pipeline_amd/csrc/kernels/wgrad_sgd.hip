@@ -638,440 +638,6 @@ __global__ __launch_bounds__(256) void wgrad_multi_big_k(WgMultiBig mb) {
   else wgrad_tile(a, kt, nt, lds);
 }
 
-
-// ---------------------------------------------------------------------------
-// Fused backward of the wide step: activation gradient + weight gradient +
-// SGD of a layer in ONE pass over its weights, and the layer below's weight
-// update in the same launch.
-//
-// The dgrad dZ_l = (dZ_{l+1} . W_l) * (H_l > 0) and the update of W_l read the
-// same bf16 words W_l (this step's hi copy): the separate split-K dgrad GEMM
-// streamed the 32 MB of a 4096 x 4096 layer once more just for the product.
-// Here a workgroup owns a 64-column k tile and one slice of R rows of W_l and
-// walks its 64-row subtiles (double-buffered LDS-DMA of the dZ_{l+1} columns,
-// the hi and the lo words): per subtile it contracts
-//   G^T[k][n] = sum_m H_l[m][k] dZ_{l+1}[m][n]     (update of the subtile)
-//   D^T[k][m] += sum_n W_l[n][k] dZ_{l+1}[m][n]    (its share of the dgrad)
-// on MFMA, both with k as the A row, so every lane holds 4 consecutive k of
-// one n (or m): the update runs straight from the accumulators on 8-B words
-// of 4 weights (hi / lo read from the staged images; plain stores, which the
-// L2 merges into whole lines -- 8-B nontemporal stores reached HBM as partial
-// lines and cost 30 %).  The slices' D^T partials are summed in slice order
-// by the last slice to arrive (per-k-tile ticket: deterministic), masked and
-// stored as dZ_l, and the k tile is announced to the layer below, whose 64 x 64
-// update tiles (later in the grid: every producer is already running) wait for
-// their dZ_l column block and read it with sc1 loads (write-through stores,
-// drained before the signal: MI355X_MICROARCH.md, hand-off table row 1).
-// Every LDS access of the subtile loop is inline asm: the compiler cannot see
-// which LDS bytes a DMA writes, and its own waits before LDS accesses would be
-// vmcnt(0), collapsing the ring.  Replaces the dgrad GEMM + update pair of
-// the per-sample backward loop (client.go:112-202).
-// Status (MI355X, 784-4096-4096-10, batch 64): correct (tests/test_gpu_wide.py)
-// but not faster than the split-K dgrad + wgrad_multi launches it replaces --
-// the subtile chain of a workgroup keeps fewer bytes in flight per CU than 5
-// independent 64 x 64 update tiles do -- so the engine keeps it opt-in
-// (profiles/r4_wide_fused_bwd_ab.json).
-// ---------------------------------------------------------------------------
-constexpr int kWbImg = kWgImg;                       // 64 x 64 bf16, 128-B rows
-constexpr int kWbBuf = 3 * kWbImg;                   // Z, hi, lo images of one subtile
-constexpr int kWbMaxSub = 16;                        // rows per slice <= 1024
-constexpr int kWbLds = 3 * kWbBuf + kWbMaxSub * 64 * 4 + 16;
-static_assert(kWbLds >= kWgLdsTot, "the plain update tiles share the launch's LDS");
-__device__ uint32_t g_wb_err;  // a bounded hand-off wait gave up (host-readable)
-
-typedef uint32_t wb_u2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t wb_la(const void* p) { return (uint32_t)(uintptr_t)(wg_lptr)p; }
-__device__ __forceinline__ wg_u4 wb_ds128(uint32_t addr) {
-  wg_u4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ wb_u2 wb_dstr(uint32_t addr) {
-  wb_u2 v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ uint32_t wb_dsu16(uint32_t addr) {
-  uint32_t v;
-  asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ void wb_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// the transposed-read fragment of wg_frag (column c0 + i, rows m0 + 8 g ..), asm form
-__device__ __forceinline__ void wb_frag(uint32_t img, int m0, int c0, int lane, wb_u2& lo, wb_u2& hi) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int chunk = (c0 >> 3) + (p >> 1);
-  const int r0 = m0 + 8 * g + q, r1 = r0 + 4;
-  lo = wb_dstr(img + r0 * 128 + 16 * (chunk ^ wg_swz(r0)) + 8 * (p & 1));
-  hi = wb_dstr(img + r1 * 128 + 16 * (chunk ^ wg_swz(r1)) + 8 * (p & 1));
-}
-__device__ __forceinline__ f32x4 wb_mfma(uint4 a, uint4 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, a), __builtin_bit_cast(wg_bf16x8, b),
-                                                 c, 0, 0, 0);
-}
-__device__ __forceinline__ uint4 wb_cat(wb_u2 lo, wb_u2 hi) { return make_uint4(lo.x, lo.y, hi.x, hi.y); }
-// ReLU' of a packed bf16 pair (the mask of the activation gradient)
-__device__ __forceinline__ bool wb_pos_lo(uint32_t w) { return __uint_as_float(w << 16) > 0.f; }
-__device__ __forceinline__ bool wb_pos_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u) > 0.f; }
-
-// 6 LDS-DMA per wave: rows 16 w' .. of the subtile's Z columns, hi and lo words
-__device__ __forceinline__ void wb_issue(const WgArgs& a, int n0, int k0, char* buf) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int pc = 0; pc < 2; ++pc) {
-    const int piece = 2 * w + pc;
-    const int r = 8 * piece + (lane >> 3), p = lane & 7;
-    const int c8 = 8 * (p ^ wg_swz(r));
-    const int m = min(r, a.M - 1);
-    __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + n0 + c8),
-                                     (wg_lptr)(buf + piece * 1024), 16, 0, 0);
-    const int64_t nr = n0 + r;
-    __builtin_amdgcn_global_load_lds((wg_gptr)(a.Wh + nr * a.ldwh + k0 + c8),
-                                     (wg_lptr)(buf + kWbImg + piece * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((wg_gptr)(a.Wl + nr * a.ldwl + k0 + c8),
-                                     (wg_lptr)(buf + 2 * kWbImg + piece * 1024), 16, 0, 0);
-  }
-}
-
-// LDS: a 3-slot ring of subtiles (Z, hi, lo images: 24 KiB a slot; the X
-// image is staged in slot 2 before the ring reaches it), then the bias
-// gradients of every subtile (k tile 0) and the arrival word: 77 KiB, so two
-// workgroups share a CU, each with two subtiles in flight behind the one it
-// computes.
-__device__ __forceinline__ wb_u2 wb_ds64(uint32_t addr) {
-  wb_u2 v;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-// 4 consecutive weights of the split master: hi / lo as one 8-B word each
-__device__ __forceinline__ void hl_join4(wb_u2 h, wb_u2 l, float (&w)[4]) {
-  w[0] = hl_join(h.x & 0xffffu, l.x & 0xffffu);
-  w[1] = hl_join(h.x >> 16, l.x >> 16);
-  w[2] = hl_join(h.y & 0xffffu, l.y & 0xffffu);
-  w[3] = hl_join(h.y >> 16, l.y >> 16);
-}
-__device__ __forceinline__ void hl_store4(const WgArgs& a, int nr, int kc, const float (&w)[4]) {
-  uint32_t hw[2], lw[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t h0 = hl_hi(w[2 * q]), h1 = hl_hi(w[2 * q + 1]);
-    hw[q] = h0 | (h1 << 16);
-    lw[q] = hl_lo(w[2 * q], h0) | (hl_lo(w[2 * q + 1], h1) << 16);
-  }
-  // plain (write-back) stores: the 4 lanes' 8-B pieces of a line merge in L2
-  // (8-B nontemporal stores went to HBM as partial-line writes: the fused step
-  // ran 40 % slower)
-  *reinterpret_cast<wb_u2*>(a.Wb + (int64_t)nr * a.ldwb + kc) = wb_u2{hw[0], hw[1]};
-  *reinterpret_cast<wb_u2*>(a.Wl + (int64_t)nr * a.ldwl + kc) = wb_u2{lw[0], lw[1]};
-}
-// s_waitcnt vmcnt(n), n wave-uniform (rounded down to even: waiting longer is safe)
-__device__ __forceinline__ void wb_vm_wait(int n) {
-  switch (n < 0 ? 0 : n >> 1) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
-  }
-}
-
-// Fused layer, k tile kt, row slice z (subtiles of 64 rows from z * R).
-// Host-checked: M <= 64, N % 64 == 0, K % 64 == 0, split master.
-__device__ __forceinline__ void wb_fused_tile(const WgArgs& a, const WbFused& f, int kt, int z, int ktiles,
-                                              char* lds) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int k0 = kt * 64;
-  const int nsub = f.rows / 64, nbase = z * f.rows;
-  float* bfin = reinterpret_cast<float*>(lds + 3 * kWbBuf);  // [subtile][64] bias gradients
-  const uint32_t lb0 = wb_la(lds), lbf = wb_la(bfin);
-  char* imx = lds + 2 * kWbBuf;  // slot 2, until subtile 2 is staged there
-  {
-#pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-      const int piece = 2 * w + pc;
-      const int r = 8 * piece + (lane >> 3), p = lane & 7;
-      const int m = min(r, a.M - 1);
-      __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + k0 + 8 * (p ^ wg_swz(r))),
-                                       (wg_lptr)(imx + piece * 1024), 16, 0, 0);
-    }
-  }
-  // vector-memory ops issued by this wave (DMA 6 per subtile, 8 update stores
-  // per subtile), and the count right after each subtile's DMA (ring of 3)
-  int issued = 2, at[3] = {0, 0, 0};
-  wb_issue(a, nbase, k0, lds);
-  issued += 6; at[0] = issued;
-  if (nsub > 1) { wb_issue(a, nbase + 64, k0, lds + kWbBuf); issued += 6; at[1] = issued; }
-  const int kw = (w & 1) * 32, nw = (w >> 1) * 32;  // wave quadrant: k rows kw.., n / m columns nw..
-  uint4 fx[2][2];  // the G product's A operand (X columns k): the same for every subtile
-  f32x4 dacc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) dacc[x][y] = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < nsub; ++s) {
-    // subtile s (and, before it, X) landed: everything issued after it may stay in flight
-    const int slot = s % 3;
-    wb_vm_wait(issued - (slot == 0 ? at[0] : slot == 1 ? at[1] : at[2]));
-    wb_lds_sync();
-    if (s == 0) {
-      wb_u2 l[2][2], h[2][2];
-      const uint32_t lx = wb_la(imx);
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int x = 0; x < 2; ++x) wb_frag(lx, 32 * hh, kw + 16 * x, lane, l[hh][x], h[hh][x]);
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(l[0][0]), "+v"(l[0][1]), "+v"(l[1][0]), "+v"(l[1][1]), "+v"(h[0][0]), "+v"(h[0][1]),
-                     "+v"(h[1][0]), "+v"(h[1][1])::"memory");
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-          fx[hh][x] = wb_cat(l[hh][x], h[hh][x]);
-          if (a.M < 64) {  // batch rows >= M (clamped copies) contribute nothing to G
-            uint32_t* e = reinterpret_cast<uint32_t*>(&fx[hh][x]);
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-              if (32 * hh + 8 * g + t >= a.M) e[t >> 1] &= (t & 1) ? 0x0000ffffu : 0xffff0000u;
-          }
-        }
-      wb_lds_sync();  // every wave holds its X fragments: slot 2 is free
-    }
-    // subtile s + 2 into the slot subtile s - 1 used (every wave is past it)
-    if (s + 2 < nsub) {
-      const int ns = (s + 2) % 3;
-      wb_issue(a, nbase + 64 * (s + 2), k0, lds + ns * kWbBuf);
-      issued += 6;
-      if (ns == 0) at[0] = issued; else if (ns == 1) at[1] = issued; else at[2] = issued;
-    }
-    const int n0 = nbase + 64 * s;
-    const uint32_t bz = lb0 + slot * kWbBuf, bh = bz + kWbImg, bl = bh + kWbImg;
-    f32x4 gacc[2][2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) gacc[x][y] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      wb_u2 zl[2], zh[2], wl[2], wh[2];
-      wg_u4 zr[2];
-#pragma unroll
-      for (int y = 0; y < 2; ++y) wb_frag(bz, 32 * hh, nw + 16 * y, lane, zl[y], zh[y]);  // Z column n
-#pragma unroll
-      for (int x = 0; x < 2; ++x) wb_frag(bh, 32 * hh, kw + 16 * x, lane, wl[x], wh[x]);  // W column k
-#pragma unroll
-      for (int y = 0; y < 2; ++y) {  // Z row m = nw + 16 y + i, n = 32 hh + 8 g ..
-        const int m = nw + 16 * y + i;
-        zr[y] = wb_ds128(bz + m * 128 + 16 * ((4 * hh + g) ^ wg_swz(m)));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(zl[0]), "+v"(zl[1]), "+v"(zh[0]), "+v"(zh[1]), "+v"(wl[0]), "+v"(wl[1]), "+v"(wh[0]),
-                     "+v"(wh[1]), "+v"(zr[0]), "+v"(zr[1])::"memory");
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          gacc[x][y] = wb_mfma(fx[hh][x], wb_cat(zl[y], zh[y]), gacc[x][y]);
-          dacc[x][y] = wb_mfma(wb_cat(wl[x], wh[x]), __builtin_bit_cast(uint4, zr[y]), dacc[x][y]);
-        }
-    }
-    // update straight from the accumulators: lane holds G^T[k = kw + 16 x + 4 g ..+3][n = nw + 16 y + i]
-    {
-      wb_u2 hv[2][2], lv[2][2];
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          const int n = nw + 16 * y + i, kc = kw + 16 * x + 4 * g;
-          const uint32_t o = n * 128 + 16 * ((kc >> 3) ^ wg_swz(n)) + 2 * (kc & 7);
-          hv[x][y] = wb_ds64(bh + o);
-          lv[x][y] = wb_ds64(bl + o);
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(hv[0][0]), "+v"(hv[0][1]), "+v"(hv[1][0]), "+v"(hv[1][1]), "+v"(lv[0][0]), "+v"(lv[0][1]),
-                     "+v"(lv[1][0]), "+v"(lv[1][1])::"memory");
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          float wv[4];
-          hl_join4(hv[x][y], lv[x][y], wv);
-          const f32x4 gv = gacc[x][y];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) wv[r] -= a.lr * (gv[r] * a.alpha);
-          hl_store4(a, n0 + nw + 16 * y + i, k0 + kw + 16 * x + 4 * g, wv);
-        }
-      issued += 8;
-    }
-    // bias (k tile 0, wave 0): column sums of this subtile's Z image, kept in LDS
-    if (kt == 0 && w == 0) {
-      const int ch = lane >> 3, e = lane & 7;
-      float db = 0.f;
-#pragma unroll 1
-      for (int r0 = 0; r0 < 64; r0 += 16) {
-        uint32_t v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          v[r] = wb_dsu16(bz + (r0 + r) * 128 + 16 * (ch ^ wg_swz(r0 + r)) + 2 * e);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
-                       "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),
-                       "+v"(v[14]), "+v"(v[15])::"memory");
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (r0 + r < a.M) db += __uint_as_float(v[r] << 16);
-      }
-      asm volatile("ds_write_b32 %0, %1" ::"v"(lbf + 4 * (64 * s + lane)), "v"(a.alpha * db) : "memory");
-    }
-  }
-  __syncthreads();  // every DMA landed (the last wait was vmcnt(0)-bound), bias sums in LDS
-  if (kt == 0 && tid < 64) {
-    for (int q = 0; q < nsub; ++q) {
-      const float db = bfin[64 * q + tid];
-      const int n = nbase + 64 * q + tid;
-      if (a.bias) a.bias[n] -= a.lr * db;
-      if (a.bgrad) a.bgrad[n] = db;
-    }
-  }
-  // ---- dgrad partial of this slice; the last slice of the k tile finishes it ----
-  // native layout: lane (x, y) of wave w holds D^T[k = kw + 16 x + 4 g ..][m = nw + 16 y + i]
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(f.part, (short)0, 0x7fffffff, 0x00020000);
-  auto poff = [&](int zz, int x, int y) {
-    return (((((zz * ktiles + kt) * 4 + w) * 4 + 2 * x + y) * 64) + lane) * 16;
-  };
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(wg_u4, dacc[x][y]), rp, poff(z, x, y), 0, 16);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* last = reinterpret_cast<int*>(lds + kWbLds - 16);
-  if (tid == 0)
-    *last = __hip_atomic_fetch_add(f.tick + kt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.slices - 1;
-  __syncthreads();
-  if (!*last) return;
-  f32x4 sum[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) sum[x][y] = {0.f, 0.f, 0.f, 0.f};
-  for (int zz = 0; zz < f.slices; ++zz) {  // slice order: deterministic
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-        sum[x][y] += zz == z ? dacc[x][y]
-                             : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, poff(zz, x, y), 0, 16));
-  }
-  // mask by H_l > 0 (= X), bf16, written through (sc1) for the layer below
-  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(f.dzo, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-  for (int y = 0; y < 2; ++y) {
-    const int m = nw + 16 * y + i;
-    if (m >= a.M) continue;
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      const int k = k0 + kw + 16 * x + 4 * g;
-      const uint2 hx = *reinterpret_cast<const uint2*>(a.X + (int64_t)m * a.ldx + k);
-      const f32x4 v = sum[x][y];
-      const uint32_t q0 = (wb_pos_lo(hx.x) ? f32_to_bf16(v[0]) : 0u) |
-                          ((uint32_t)(wb_pos_hi(hx.x) ? f32_to_bf16(v[1]) : 0u) << 16);
-      const uint32_t q1 = (wb_pos_lo(hx.y) ? f32_to_bf16(v[2]) : 0u) |
-                          ((uint32_t)(wb_pos_hi(hx.y) ? f32_to_bf16(v[3]) : 0u) << 16);
-      __builtin_amdgcn_raw_buffer_store_b64(wb_u2{q0, q1}, ro, (int)(((int64_t)m * f.lddo + k) * 2), 0, 16);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(f.tick + kt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f.ready) __hip_atomic_fetch_add(f.ready + kt, f.nready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Update tile of the layer below a fused layer: wait until Z's column block nt
-// (dZ_{l+1} = the fused layer's output) is announced, read it with sc1 loads
-// into the Z image, then the plain 64 x 64 body.  Host-checked: M <= 64.
-__device__ __forceinline__ void wb_dep_tile(const WgArgs& a, int* ready, uint64_t timeout, int kt, int nt,
-                                            char* lds) {
-  const int tid = threadIdx.x;
-  uint4 wr[4];
-  wg_load_hl(a, kt, nt, wr);  // W words first: their round trip overlaps the wait
-  if (tid == 0) {
-    typedef __attribute__((address_space(1))) int g32;
-    const g32* rf = (const g32*)(ready + nt);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool ok = true;
-    while (__hip_atomic_load(rf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (ok) __hip_atomic_fetch_add(ready + nt, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_fetch_or(&g_wb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  // Z[m][nt * 64 ..]: 64 rows x 8 chunks, two per thread, into the swizzled image
-  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.Z), (short)0,
-                                                                      0x7fffffff, 0x00020000);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (tid >> 3) + 32 * j, p = tid & 7;
-    const int m = min(r, a.M - 1);
-    const wg_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rz, (int)(((int64_t)m * a.ldz + nt * 64 + 8 * p) * 2), 0, 16);
-    *reinterpret_cast<wg_u4*>(lds + r * 128 + 16 * (p ^ wg_swz(r))) = v;
-  }
-  wgrad_tile_body(a, kt, nt, lds, wr, true);
-}
-
-// The fused layer (if any) is layer 0 of the launch: the producer of the
-// hand-off precedes its consumers in the grid (every consumer's producers are
-// already running when it waits), and only one WbFused is ever addressed.
-struct WbMulti {
-  WgArgs l[kWgMaxLayers];
-  WbFused f;  // layer 0's, when fused
-  int start[kWgMaxLayers + 1];
-  int ktiles[kWgMaxLayers];
-  int wait[kWgMaxLayers];  // 1: Z is layer 0's dZ output (waits on f.ready)
-  uint64_t timeout;
-  int n, fused0;
-};
-
-__global__ __launch_bounds__(256) void wide_bwd_k(WbMulti m) {
-  extern __shared__ __attribute__((aligned(16))) char wb_lds[];
-  const int b = blockIdx.x;
-  int j = 0;
-#pragma unroll
-  for (int q = 1; q < kWgMaxLayers; ++q)
-    if (q < m.n && b >= m.start[q]) j = q;
-  const int t = b - m.start[j];
-  if (j == 0 && m.fused0) {
-    // the slices of one k tile are adjacent (they finish close together)
-    wb_fused_tile(m.l[0], m.f, t / m.f.slices, t % m.f.slices, m.ktiles[0], wb_lds);
-    return;
-  }
-  // uniform branches select the operands (no dynamic indexing of the argument array)
-  WgArgs a = m.l[0];
-  int kts = m.ktiles[0], wt = m.wait[0];
-#pragma unroll
-  for (int q = 1; q < kWgMaxLayers; ++q)
-    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; wt = m.wait[q]; }
-  int kt, nt;
-  if ((m.start[j] & 7) == 0) wg_tile_xcd(t, kts, (a.N + 63) / 64, kt, nt);
-  else { kt = t % kts; nt = t / kts; }
-  if (wt) wb_dep_tile(a, m.f.ready, m.timeout, kt, nt, wb_lds);
-  else wgrad_tile(a, kt, nt, wb_lds);
-}
-
-
 bool wg_valid(const WgArgs& a) {
   if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
       a.ldz < ((a.N + 7) & ~7) || a.ldx < ((a.K + 7) & ~7) || (((uintptr_t)a.Z | (uintptr_t)a.X) & 15))
@@ -1136,63 +702,6 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile
 }
 
 
-uint32_t wide_bwd_errors(bool clear) {
-  uint32_t v = 0;
-  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_wb_err), sizeof(v), 0, hipMemcpyDeviceToHost);
-  if (clear && v) {
-    const uint32_t z = 0;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wb_err), &z, sizeof(z), 0, hipMemcpyHostToDevice);
-  }
-  return v;
-}
-
-hipError_t wide_bwd(const WgLayer* layers, const WbFused* fused, int n, hipStream_t s) {
-  if (n < 1 || n > kWgMaxLayers) return hipErrorInvalidValue;
-  WbMulti m{};
-  m.n = n;
-  m.timeout = 100000000ull;  // 1 s of s_memrealtime ticks: a hand-off that never comes
-  int t = 0;
-  for (int j = 0; j < n; ++j) {
-    const WgLayer& L = layers[j];
-    const WbFused& F = fused[j];
-    if (!wg_valid(L)) return hipErrorInvalidValue;
-    m.l[j] = L;
-    m.start[j] = t;
-    m.ktiles[j] = (L.K + 63) / 64;
-    if (F.fused) {
-      // layer 0 only; one 64-column k tile x F.rows rows per workgroup; split
-      // master, whole tiles
-      if (j != 0 || L.M > 64 || (L.N & 63) || (L.K & 63) || F.rows < 64 || (F.rows & 63) || L.N % F.rows ||
-          F.rows > 64 * kWbMaxSub ||
-          F.slices != L.N / F.rows || !L.Wl || !F.dzo || !F.part || !F.tick || (F.lddo & 3) ||
-          ((uintptr_t)F.dzo & 7) || (F.ready && F.nready < 1))
-        return hipErrorInvalidValue;
-      m.fused0 = 1;
-      m.f = F;
-      t += m.ktiles[j] * F.slices;
-    } else {
-      if (F.wait_prev) {
-        // Z = layer 0's dZ output, announced per 64-column block
-        if (!m.fused0 || L.M > 64 || (L.N & 63) || m.f.ready == nullptr || m.f.dzo != L.Z ||
-            m.f.nready != m.ktiles[j] || (L.N + 63) / 64 != m.ktiles[0])
-          return hipErrorInvalidValue;
-        m.wait[j] = 1;
-      }
-      t += m.ktiles[j] * ((L.N + 63) / 64);
-    }
-  }
-  for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
-  for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(wide_bwd_k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kWbLds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(wide_bwd_k, dim3(t), dim3(256), kWbLds, s, m);
-  return hipGetLastError();
-}
 
 namespace {
 __global__ void hilo_split_k(const float* __restrict__ W, int N, int K, int64_t ldw, uint16_t* __restrict__ hi,

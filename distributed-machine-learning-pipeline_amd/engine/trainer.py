@@ -58,13 +58,20 @@ class StepStats:
         return 100.0 * self.correct / max(self.count, 1.0)
 
 
-def _xgmi_eligible(ctx: DistContext, need_nccl: bool = True) -> bool:
-    """All ranks on one node, one GPU each, <= 8: the fused exchange applies."""
+def _xgmi_eligible(ctx: DistContext, node_local: Optional[bool] = None) -> bool:
+    """Whether the fused xGMI exchanges apply: GPU replicas, a process group,
+    2..8 ranks, all on this node (IPC peer memory).  The group's backend does
+    not matter -- it carries only the control plane (IPC handles, the
+    self-test all-reduce, agreement on the mode); the data moves over xGMI --
+    so a gloo group with an external RCCL comm (the gpu_sim device servers,
+    rpc/device_server.py ConfigureModel) qualifies like a torchrun RCCL job.
+    `node_local` None: from torchrun's LOCAL_WORLD_SIZE."""
     import os
 
-    local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size))
-    return ctx.device.type == "cuda" and (ctx.backend == "nccl" or not need_nccl) \
-        and 1 < ctx.world_size <= 8 and local == ctx.world_size
+    if node_local is None:
+        node_local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size)) == ctx.world_size
+    return (ctx.device.type == "cuda" and ctx.backend != "none" and 1 < ctx.world_size <= 8
+            and bool(node_local))
 
 
 def _pad_cols(X: torch.Tensor, mult: int = 4) -> torch.Tensor:
@@ -85,7 +92,7 @@ class MlpTrainer:
                  capture_collectives: Optional[bool] = None, xchg_timeout_ms: float = 10000.0,
                  xact_waves: int = 0, auto_fallback: str = "rccl",
                  stream: Optional["torch.cuda.Stream"] = None, persist: Optional[bool] = None,
-                 grad_allreduce=None):
+                 grad_allreduce=None, node_local: Optional[bool] = None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
@@ -134,6 +141,9 @@ class MlpTrainer:
         if auto_fallback not in ("rccl", "torch"):
             raise ValueError("auto_fallback must be 'rccl' or 'torch'")
         self.auto_fallback = auto_fallback
+        # every rank on this node (None: torchrun's LOCAL_WORLD_SIZE says);
+        # the gpu_sim device servers pass what their process group found
+        self._node_local = node_local
         self.sync_active = "none"
         self.sync_times: Dict[str, float] = {}
         # data-only tables built at init, outside any timed region: name -> ms
@@ -227,9 +237,23 @@ class MlpTrainer:
             self.comm.reserve_ring(self.layout.nparams, self._ring_chunk)
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, self._ring_chunk)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
-        if self.sync in EXCHANGE_MODES or (self.sync == "auto" and plain and _xgmi_eligible(
-                self.ctx, need_nccl=not torch_fallback)):
+        if self.exchange_candidates():
             self._init_exchanges()
+
+    def exchange_candidates(self) -> list:
+        """The fused xGMI exchange forms _init_exchanges self-tests, in
+        preference order ([] when none applies: sync='auto' needs plain SGD and
+        an eligible group, see _xgmi_eligible)."""
+        if self.sync in EXCHANGE_MODES:
+            return [self.sync]
+        plain = not (self.momentum or self.weight_decay)
+        if not (self.sync == "auto" and plain and _xgmi_eligible(self.ctx, self._node_local)):
+            return []
+        # pk2 pays one more flag round trip per slot for fewer bytes: a
+        # candidate from 3 replicas on (at 2 it moves the same bytes as pk)
+        two = self.ctx.world_size >= 3
+        return (["pkx", "pkg"] + (["pkg2"] if two else []) + ["pk"] + (["pk2"] if two else [])
+                + ["xact", "xgmi"])
 
     # ------------------------------------------------------ xGMI exchanges --
     def _gather_inputs(self) -> torch.Tensor:
@@ -339,12 +363,7 @@ class MlpTrainer:
         self.Xall = None
         self.pk_gram_dp = None
         strict = self.sync in EXCHANGE_MODES
-        # pk2 pays one more flag round trip per slot for fewer bytes: a
-        # candidate from 3 replicas on (at 2 it moves the same bytes as pk)
-        two = self.ctx.world_size >= 3
-        auto = (["pkx", "pkg"] + (["pkg2"] if two else []) + ["pk"] + (["pk2"] if two else [])
-                + ["xact", "xgmi"])
-        modes = [self.sync] if strict else auto
+        modes = self.exchange_candidates()
         ok = []
         for m in modes:
             err = self._setup_exchange(m)
@@ -364,8 +383,11 @@ class MlpTrainer:
             log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
             self.sync_times = times
         self._set_mode(choice or self.sync_active)
-        if self.sync_active not in XALL_MODES:
-            self.Xall = None  # the replicated inputs are only read by xact / pkx
+        if self.sync_active not in XALL_MODES and self.Xall is not None:
+            # the replicated inputs (N x the shard) are only read by xact / pkx:
+            # free them, the runner's references included
+            self.Xall = None
+            self.runner.release_xall()
 
     @staticmethod
     def runner_module():

@@ -62,9 +62,7 @@ class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
                  sync: str = "rccl", target_wgs: int = 256, graph: bool = True,
-                 gemm: str = "skinny", overlap_wgrad: bool = False, serial_sync: bool = False,
-                 fused_bwd: Optional[bool] = None, bwd_rows: int = 0,
-                 fused_fwd: Optional[bool] = None, xblk: Optional[bool] = None):
+                 gemm: str = "skinny", serial_sync: bool = False, xblk: Optional[bool] = None):
         from ..ops.native import require_native
 
         self.C = require_native()
@@ -105,8 +103,8 @@ class WideMlpTrainer:
         # bf16 W_l with rows padded to 16 (zeros: the dgrad reads a whole K tile of
         # rows), double-buffered by step parity: step s reads Wb[l][s % 2] (forward,
         # dgrad, head) while its weight-gradient kernel writes the updated copy into
-        # Wb[l][(s + 1) % 2] -- so the wgrad kernels can run on a side stream,
-        # concurrently with the dgrad chain that still reads the old weights.
+        # Wb[l][(s + 1) % 2] -- so a replica's comm-stream updates never race the
+        # dgrad chain that still reads the old weights.
         self.Wb = [[torch.zeros(self.pd[l + 1], self.pd[l], **bf) for _ in range(2)]
                    for l in range(L)]
         # the int16 remainders of the split fp32 masters (updated in place)
@@ -164,56 +162,8 @@ class WideMlpTrainer:
         if self.comm is not None and sync == "ring":
             # the in-house ring's reduce scratch, sized once for the largest bucket
             self.comm.reserve_ring(max(hi - lo for lo, hi in self._gspan), 4 << 20)
-        # single replica, overlap_wgrad: the weight-gradient + SGD kernels of layers
-        # >= 1 run on a side stream, concurrently with the dgrad chain.  Off by
-        # default: measured on MI355X the split-K dgrad (one 128 KiB-LDS workgroup
-        # per CU) waits for CUs held by the wgrad workgroups, 14 -> 33 us, and the
-        # step got slower (87.6 -> 99.5 us, profiles/r2_wide_*).
-        self.overlap_wgrad = overlap_wgrad and not self.ctx.is_distributed
-        self._ss = torch.cuda.Stream(dev) if self.overlap_wgrad else None
         # an epoch graph must start at an even step (the Wb parity it baked in)
         self.period = self.nbatches if self.nbatches % 2 == 0 else 2 * self.nbatches
-        # fused_bwd (single replica, 3 layers with the fused head): the dgrad of
-        # layer 1 runs inside its weight-update pass (kernels/wgrad_sgd.hip
-        # wide_bwd) on the W_1 words the update streams anyway -- 32 MB less HBM
-        # traffic and one launch less per step.  Off by default: measured on
-        # MI355X it does not beat the split-K dgrad + update launches (76.6 vs
-        # 75.6 us/step at its best slice height; profiles/r4_wide_fused_bwd_ab.json)
-        if fused_bwd is None:
-            fused_bwd = os.environ.get("HIPDSML_WIDE_FUSED_BWD", "0") == "1"
-        self.fused_bwd = (fused_bwd and not self.ctx.is_distributed and self._ss is None and L == 3 and
-                          self.fused_head and batch <= 64 and d[1] % 64 == 0 and d[2] % 64 == 0)
-        if self.fused_bwd:
-            rows = bwd_rows or int(os.environ.get("HIPDSML_WIDE_BWD_ROWS", "512"))
-            if not bwd_rows:  # the default: the largest multiple of 64 <= rows dividing d[2]
-                rows = max(r for r in range(64, min(rows, d[2]) + 1, 64) if d[2] % r == 0)
-            if rows % 64 or d[2] % rows:
-                raise ValueError(f"bwd_rows={rows} must be a multiple of 64 dividing {d[2]}")
-            self.bwd_rows = rows
-            # layer 0's update in a launch of its own (default): inside the fused
-            # launch its tiles wait for the dZ_1 blocks at the fused tiles' LDS
-            # footprint (2 workgroups per CU), measured slower
-            self.bwd_split = os.environ.get("HIPDSML_WIDE_BWD_SPLIT", "1") == "1"
-            kt = d[1] // 64
-            self.Pd = torch.zeros((d[2] // rows) * kt * 4096, dtype=torch.float32, device=dev)
-            self.wb_tick = torch.zeros(kt, dtype=torch.int32, device=dev)
-            self.wb_ready = torch.zeros(kt, dtype=torch.int32, device=dev)
-        # fused_fwd (single replica, 4096-wide hidden layers): both hidden layers'
-        # forward in ONE launch (kernels/wide_fwd.hip): every workgroup streams its
-        # W2 slice into LDS while it computes its layer-1 tile, then waits for the
-        # 64 layer-1 tiles its K slice reads.  Bit-exact with the two launches.
-        # Off by default: measured on MI355X it is slower (25.0 vs 22.2 us,
-        # profiles/r4_wide_fused_fwd_ab.json)
-        if fused_fwd is None:
-            fused_fwd = os.environ.get("HIPDSML_WIDE_FUSED_FWD", "0") == "1"
-        b_al = all(self.views[l][1].data_ptr() % 16 == 0 for l in range(min(L, 2)))
-        self.fused_fwd = bool(fused_fwd and not self.ctx.is_distributed and L == 3 and
-                              d[1] == 4096 and d[2] == 4096 and 512 <= d[0] <= 1024 and
-                              d[0] % 8 == 0 and batch <= 64 and b_al and
-                              self.C.wide_fwd2_supported(dev.index or 0))
-        if self.fused_fwd:
-            # tile flags, launch epoch, done ticket, error word (zeroed once)
-            self.wf_sync = torch.zeros(260, dtype=torch.int32, device=dev)
         # xblk: the input-layer GEMM reads a k-blocked copy of the shard
         # ([K/32][rows][32] bf16): a 16-row MFMA fragment load is then 1 KiB
         # contiguous instead of 16 half cache lines (gemm_bf16.hip rows64 ABLK).
@@ -221,7 +171,7 @@ class WideMlpTrainer:
         if xblk is None:
             xblk = os.environ.get("HIPDSML_WIDE_XBLK", "1") == "1"
         self.Xblk = None
-        if xblk and not self.xact and not self.fused_fwd and 512 <= d[0] <= 1024 and batch <= 64 \
+        if xblk and not self.xact and 512 <= d[0] <= 1024 and batch <= 64 \
                 and (self.gemm == "rows64" or d[0] < 1024):
             nb = _rup(d[0], 32) // 32
             xp = torch.zeros(self.Xb.shape[0], nb * 32, **bf)
@@ -342,16 +292,12 @@ class WideMlpTrainer:
         cur = [self.Wb[l][p] for l in range(L)]       # this step's weights
         nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
         self.H[0] = self._xb_rows(bi)  # this batch's bf16 rows (a view: no copy)
-        if self.fused_fwd:
-            C.wide_fwd2(self.H[0], cur[0], self.views[0][1], self.H[1], cur[1], self.views[1][1],
-                        self.H[2], Bt, d[0], self.Cp, self.tctr, self.wf_sync)
-        else:
-            for l in range(L - 1):
-                _, b = self.views[l]
-                A = self.Xblk[:, r0:r0 + Bt] if l == 0 and self.Xblk is not None else self.H[l]
-                self._gemm(f"f{l}", A, cur[l], bias=b, relu=True, obf=self.H[l + 1])
-                if self.xact:
-                    self._gather(self.Hall[l + 1])
+        for l in range(L - 1):
+            _, b = self.views[l]
+            A = self.Xblk[:, r0:r0 + Bt] if l == 0 and self.Xblk is not None else self.H[l]
+            self._gemm(f"f{l}", A, cur[l], bias=b, relu=True, obf=self.H[l + 1])
+            if self.xact:
+                self._gather(self.Hall[l + 1])
         _, b = self.views[L - 1]
         if self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
             # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
@@ -389,22 +335,7 @@ class WideMlpTrainer:
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1
             return
-        if self.fused_bwd:
-            # ONE launch: layer 1's update with its dgrad folded in (dZ_1 out), the
-            # classifier's update, and layer 0's update tiles, which wait for dZ_1
-            lay = []
-            for l in (1, 2, 0):
-                W, b = self.views[l]
-                lay.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l], None, b,
-                            None, cur[l], self.Wlo[l]))
-            if self.bwd_split:  # layer 0's update in a launch of its own (full occupancy)
-                C.wide_bwd(lay[:2], 0, self.bwd_rows, self.dZ[1], self.Pd, self.wb_tick, None)
-                C.wgrad_sgd_multi(lay[2:])
-            else:
-                C.wide_bwd(lay, 0, self.bwd_rows, self.dZ[1], self.Pd, self.wb_tick, self.wb_ready)
-            self.steps_done += 1
-            return
-        if fused_sgd and self._ss is None:
+        if fused_sgd:
             # every dgrad first (they read this step's bf16 weights), then ONE
             # launch updates every layer: W -= lr * dZ_{l+1}^T H_l, the next step's
             # bf16 copies, the biases (kernels/wgrad_sgd.hip, flattened tile grid)
@@ -419,33 +350,19 @@ class WideMlpTrainer:
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1
             return
+        # several replicas, gradient all-reduce: per layer, the weight gradient,
+        # then its bucket's all-reduce + SGD on the comm stream while the dgrad
+        # of the layers below continues here
         for l in range(L - 1, -1, -1):
-            W, b = self.views[l]
             gW, gb = self.gviews[l]
-            if fused_sgd:
-                # dW_l = dZ_{l+1}^T H_l with SGD fused: W -= lr*dW, the NEXT step's bf16
-                # copy written, the bias step from the column sums of dZ.  With
-                # overlap_wgrad, layers >= 1 go to the side stream as soon as dZ_{l+1}
-                # exists (fork here) and overlap the dgrad of layer l and below.
-                if l > 0 and self._ss is not None:
-                    self._ss.wait_stream(main)
-                    with torch.cuda.stream(self._ss):
-                        C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale,
-                                    Wb=nxt[l], bias=b, Wh=cur[l], Wl=self.Wlo[l])
-                else:
-                    C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], lr=scale,
-                                Wb=nxt[l], bias=b, Wh=cur[l], Wl=self.Wlo[l])
             if l > 0 and not (self.fused_head and l == L - 1):
                 # activation gradient (reads this step's W_l copy, not the one being written)
                 self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
-            if not fused_sgd:
-                C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], G=gW, bgrad=gb)
-                self._sync_layer(l, scale, cur[l], nxt[l])
+            C.wgrad_sgd(self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], G=gW, bgrad=gb)
+            self._sync_layer(l, scale, cur[l], nxt[l])
         # join: the next step's forward reads every updated layer (and overwrites
-        # the activations the side-stream kernels read)
-        side = self._ss if fused_sgd else self._cs
-        if side is not None:
-            main.wait_stream(side)
+        # the activations the comm-stream updates read)
+        main.wait_stream(self._cs)
         self.steps_done += 1
 
     def _sync_layer(self, l: int, scale: float, wb_cur: torch.Tensor, wb_next: torch.Tensor) -> None:
@@ -524,15 +441,6 @@ class WideMlpTrainer:
 
     def synchronize(self) -> None:
         torch.cuda.synchronize(self.device)
-        if self.fused_bwd and not self.bwd_split and self.C.wide_bwd_errors(True):
-            # a layer-0 update tile gave up waiting for its dZ_1 block (bounded
-            # in-launch hand-off): the step's weights are not valid
-            raise RuntimeError("fused wide backward: an in-launch hand-off timed out")
-        if self.fused_fwd and int(self.wf_sync[258].item()):
-            self.wf_sync[258] = 0
-            # a layer-2 workgroup gave up waiting for its layer-1 tiles (the grid
-            # was not co-resident): that step's activations are not valid
-            raise RuntimeError("fused wide forward: an in-launch hand-off timed out")
 
     def read_stats(self, reset: bool = True, global_: bool = False) -> StepStats:
         self.synchronize()

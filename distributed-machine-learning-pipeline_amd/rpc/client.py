@@ -36,6 +36,7 @@ import numpy as np
 
 from ..models.mlp import MlpLayout, MlpSpec
 from .proto import DT_FLOAT32, SUM, pb
+from .stubs import is_loopback
 from .stubs import GPUCoordinatorStub, GPUDeviceStub, connect
 
 log = logging.getLogger("hipdsml.client")
@@ -91,7 +92,10 @@ class TrainingClient:
         if backend == "auto":
             backends = {s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata.backend
                         for s in self.devs}
-            backend = "pg" if n > 1 and backends == {"hip"} else "rpc"
+            # the process group meets on a store the coordinator hosts; devices on
+            # other hosts take the RCCL bootstrap, whose id travels over gRPC
+            remote = not all(is_loopback(a) for a in self.dev_addrs)
+            backend = ("rccl" if remote else "pg") if n > 1 and backends == {"hip"} else "rpc"
         self.comm_init(backend)
 
         def cfg(i, s):

@@ -37,7 +37,7 @@ import grpc
 import numpy as np
 
 from .proto import DT_SIZE, FAILED, IN_PROGRESS, SUCCESS, pb
-from .stubs import GPUDeviceStub, connect
+from .stubs import GPUDeviceStub, connect, is_loopback
 
 log = logging.getLogger("hipdsml.coordinator")
 
@@ -179,8 +179,9 @@ class GPUCoordinatorServicer:
         try:
             self._setup_devices(comm)
         except Exception as e:
-            for d in devices:
-                d.channel.close()
+            # devices that did join (a process group, an RCCL comm) leave again:
+            # the id was never registered, so CommDestroy could not reach them
+            self._teardown_devices(comm)
             context.abort(grpc.StatusCode.INTERNAL, f"CommInit device setup failed: {e}")
         with self._mu:
             self.comms[cid] = comm
@@ -205,6 +206,11 @@ class GPUCoordinatorServicer:
 
             import torch.distributed as dist
 
+            if is_loopback(self.store_host) and not all(is_loopback(p) for p in peers):
+                raise CollectiveError(
+                    f"backend 'pg': the process-group store would bind to {self.store_host}, which "
+                    f"devices on other hosts cannot reach (start the coordinator with --store-host, "
+                    f"or use backend 'rccl')")
             comm.store = dist.TCPStore(self.store_host, 0, is_master=True, wait_for_workers=False,
                                        timeout=datetime.timedelta(seconds=self.rpc_timeout))
             store_addr = f"{self.store_host}:{comm.store.port}"
@@ -229,6 +235,12 @@ class GPUCoordinatorServicer:
             c = self.comms.pop(request.commId, None)
         if c is None:
             context.abort(grpc.StatusCode.NOT_FOUND, f"communicator {request.commId} not found")
+        self._teardown_devices(c)
+        return pb.CommDestroyResponse(success=True)
+
+    def _teardown_devices(self, c: Communicator) -> None:
+        """CommTeardown on every device (best effort), close the channels and
+        drop the process group's store."""
         # a process group's teardown is collective: every device leaves together
         tmo = self.rpc_timeout if c.backend == "pg" else self.health_timeout
         futs = [self._pool.submit(d.stub.CommTeardown, pb.CommTeardownRequest(commId=c.id), timeout=tmo)
@@ -241,7 +253,6 @@ class GPUCoordinatorServicer:
         for d in c.devices:
             d.channel.close()
         c.store = None
-        return pb.CommDestroyResponse(success=True)
 
     def CommFinalize(self, request, context):
         c = self._get(request.commId, context)
@@ -310,16 +321,19 @@ class GPUCoordinatorServicer:
 
     def _run_allreduce(self, c: Communicator, op) -> bool:
         try:
-            if c.backend == "rccl" or c.data_backend == "rccl":
-                self._allreduce_rccl(c, op)
-            elif op.algo == "coordinator-ring":
-                self._allreduce_rpc_ring(c, op)
-            elif op.algo == "xgmi":  # "pg" comms of GPU devices: one launch over peer memory
+            # an explicit algo "xgmi" runs over peer memory even when RCCL is up
+            # ("pg" comms of GPU devices), so a benchmark asking for it never
+            # gets RCCL's time under that name
+            if op.algo == "xgmi":  # one launch over xGMI peer memory
                 self._parallel([
                     (lambda d=d: d.stub.DeviceAllReduce(pb.DeviceAllReduceRequest(
                         commId=c.id, addr=self._addr(op, d.rank), count=op.count, dtype=op.dtype,
                         op=op.op, algo="xgmi"), timeout=self.rpc_timeout))
                     for d in c.devices], on_error=lambda: self._abort_all(c, "peer failed during all-reduce"))
+            elif c.backend == "rccl" or c.data_backend == "rccl":
+                self._allreduce_rccl(c, op)
+            elif op.algo == "coordinator-ring":
+                self._allreduce_rpc_ring(c, op)
             else:  # "stream-ring" (default) / "device-ring": devices drive the ring themselves
                 self._allreduce_device_ring(c, op)
         except Exception as e:

@@ -35,6 +35,7 @@ class GPUDeviceServicer:
         self.comms: Dict[int, object] = {}      # commId -> native RcclComm
         self.comm_meta: Dict[int, dict] = {}    # commId -> {"rank", "nranks", "peers"}
         self.pg_comm: Optional[int] = None      # commId whose process group this process joined
+        self.pg_node_local = False              # every rank of that group on this node
         # RingChannel: per commId, the outgoing queue to the successor (one
         # long-lived client stream) and the inbox of the predecessor's messages
         self._ring_out: Dict[int, "queue.Queue"] = {}
@@ -279,22 +280,42 @@ class GPUDeviceServicer:
         except Exception as e:
             context.abort(grpc.StatusCode.INTERNAL, f"process group rendezvous failed: {e}")
         self.pg_comm = cid
+        self.pg_node_local = False
         if self.dev.backend != "hip":
             return "pg"
         from ..parallel.dist import DistContext, make_native_comm
 
         ctx = DistContext(rank=request.rank, world_size=request.nranks, device=self._torch_device(),
                           backend="gloo")
-        props = torch.cuda.get_device_properties(self.dev.gpu)
-        ident = f"{socket.gethostname()}/{getattr(props, 'uuid', '')}/{self.dev.gpu}".encode()
-        gpus = ctx.all_gather_bytes(f"hipdsml/pg{cid}/gpu", ident)
-        if len(set(gpus)) < request.nranks:
-            return "pg"  # ranks share a GPU: RCCL refuses; exchanges + gloo fallback only
+        err = None
         try:
+            props = torch.cuda.get_device_properties(self.dev.gpu)
+            ident = f"{socket.gethostname()}/{getattr(props, 'uuid', '')}/{self.dev.gpu}".encode()
+            gpus = ctx.all_gather_bytes(f"hipdsml/pg{cid}/gpu", ident)
+            # the xGMI exchanges need every rank on this node (IPC peer memory)
+            self.pg_node_local = len({g.split(b"/", 1)[0] for g in gpus}) == 1
+            if len(set(gpus)) < request.nranks:
+                return "pg"  # ranks share a GPU: RCCL refuses; exchanges + gloo fallback only
             self.comms[cid] = make_native_comm(ctx)
         except Exception as e:
-            context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {e}")
+            err = e
+        if err is not None:
+            # leave the group again, or every later CommInit('pg') on this server
+            # would fail with "already belongs to process group" 
+            self._leave_process_group()
+            context.abort(grpc.StatusCode.INTERNAL, f"RCCL init failed: {err}")
         return "rccl+pg"
+
+    def _leave_process_group(self) -> None:
+        import torch.distributed as dist
+
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # pragma: no cover
+            pass
+        self.pg_comm = None
+        self.pg_node_local = False
 
     @staticmethod
     def _ring_sid(cid: int, seq: int, step: int, src: int) -> int:
@@ -333,31 +354,49 @@ class GPUDeviceServicer:
             self.counters["stream_bytes_in"] += len(msg.data)
         return pb.RingAck(success=True)
 
+    # an idle ring stream is closed after this many seconds (the next ring step
+    # reopens it): each open stream holds one of the successor's gRPC workers
+    RING_IDLE_S = 60.0
+
     def _ring_send(self, cid: int, nxt: str, msg) -> None:
         """Queue `msg` on this comm's stream to the successor, opening the
-        stream (a background client call fed by the queue) on first use."""
+        stream (a background client call fed by the queue) on first use.  The
+        stream ends when the comm is torn down or aborted, or after
+        RING_IDLE_S without traffic, so a client that never destroys its
+        communicator cannot pin the successor's worker threads."""
         import queue
 
-        q = self._ring_out.get(cid)
-        if q is None:
-            q = queue.Queue()
-            self._ring_out[cid] = q
+        with self._lock:
+            q = self._ring_out.get(cid)
+            if q is None:
+                q = queue.Queue()
+                self._ring_out[cid] = q
 
-            def gen():
-                while True:
-                    m = q.get()
-                    if m is None:
-                        return
-                    yield m
+                def gen(q=q):
+                    while True:
+                        try:
+                            m = q.get(timeout=self.RING_IDLE_S)
+                        except queue.Empty:
+                            with self._lock:  # _ring_send enqueues under this lock
+                                if not q.empty():
+                                    continue
+                                if self._ring_out.get(cid) is q:
+                                    del self._ring_out[cid]
+                            return
+                        if m is None:
+                            return
+                        yield m
 
-            def run():
-                try:
-                    self._peer(nxt).RingChannel(gen(), timeout=24 * 3600)
-                except Exception as e:  # peer gone: the waiting step times out / aborts
-                    log.warning("ring channel of comm %d to %s closed: %s", cid, nxt, e)
+                def run(gen=gen):
+                    try:
+                        # the deadline only bounds a pathological stream; the
+                        # idle close above ends it long before
+                        self._peer(nxt).RingChannel(gen(), timeout=3600)
+                    except Exception as e:  # peer gone: the waiting step times out / aborts
+                        log.warning("ring channel of comm %d to %s closed: %s", cid, nxt, e)
 
-            threading.Thread(target=run, daemon=True).start()
-        q.put(msg)
+                threading.Thread(target=run, daemon=True).start()
+            q.put(msg)
 
     def _ring_recv(self, cid: int, seq: int, step: int, timeout: float = 120.0) -> bytes:
         t_end = time.monotonic() + timeout
@@ -374,7 +413,8 @@ class GPUDeviceServicer:
                 self._ring_cv.wait(min(left, 0.05))
 
     def _ring_close(self, cid: int) -> None:
-        q = self._ring_out.pop(cid, None)
+        with self._lock:
+            q = self._ring_out.pop(cid, None)
         if q is not None:
             q.put(None)
         with self._ring_cv:
@@ -607,6 +647,8 @@ class GPUDeviceServicer:
         # keep failing that communicator's later ring steps (sticky)
         if request.commId in self.comm_meta or request.commId in self.comms:
             self._aborted_comms.add(request.commId)
+            # the comm is dead for good: release the successor's stream worker
+            self._ring_close(request.commId)
         self.dev.fail_pending_streams()
         ids = [request.commId] if request.commId in self.comms else list(self.comms)
         for cid in ids:
@@ -623,17 +665,11 @@ class GPUDeviceServicer:
         self.comms.pop(request.commId, None)
         self.comm_meta.pop(request.commId, None)
         if request.commId == self.pg_comm:
-            import torch.distributed as dist
-
             if self.trainer is not None and getattr(self.trainer, "ctx", None) is not None \
                     and self.trainer.ctx.is_distributed:
                 self.trainer = None  # its exchanges and self-tests belong to this group
             torch.cuda.synchronize() if self.dev.backend == "hip" else None
-            try:
-                dist.destroy_process_group()
-            except Exception:
-                pass
-            self.pg_comm = None
+            self._leave_process_group()
         return pb.CommTeardownResponse(success=True)
 
     # -------------------------------------------------------------- training --
@@ -704,7 +740,10 @@ class GPUDeviceServicer:
                                       seed=request.seed, momentum=request.momentum,
                                       graph_steps=request.graphSteps, params=params,
                                       external_comm=comm, sync=sync, grad_allreduce=host_ar,
-                                      auto_fallback="rccl" if (comm is not None or not pg) else "torch")
+                                      auto_fallback="rccl" if (comm is not None or not pg) else "torch",
+                                      # the exchanges need every server on this node, whatever
+                                      # the group's backend (RCCL stays the fallback candidate)
+                                      node_local=self.pg_node_local if pg else None)
         except (ValueError, RuntimeError) as e:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         return pb.ConfigureModelResponse(success=True, numParams=spec.num_params,

@@ -98,6 +98,13 @@ def serve(service: str, servicer, address: str = "127.0.0.1:0",
     return server, f"{host}:{port}"
 
 
+def is_loopback(address: str) -> bool:
+    """Whether a host[:port] address names this machine's loopback interface."""
+    host = address.rsplit(":", 1)[0] if address.count(":") == 1 or address.startswith("[") else address
+    host = host.strip("[]")
+    return host in ("localhost", "::1") or host.startswith("127.")
+
+
 def connect(address: str, timeout: Optional[float] = None) -> grpc.Channel:
     """Insecure channel; with `timeout`, wait until it is READY (an explicit
     connect, unlike the reference's lazy grpc.Dial retry loop)."""

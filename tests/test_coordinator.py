@@ -309,3 +309,61 @@ def test_crashed_device_process_detected(tmp_path):
                 p.wait(timeout=10)
             except subprocess.TimeoutExpired:
                 p.kill()
+
+
+def test_ring_streams_close_when_idle_and_on_abort():
+    """every comm's long-lived RingChannel holds one of the
+    successor's gRPC workers; it must end when idle (and reopen on the next
+    ring step) and when the comm is aborted, not live for a day."""
+    n = 3
+    with cluster(n_devices=n, mem_size=1 << 14) as c:
+        for _, _, svc in c.devices:
+            svc.RING_IDLE_S = 0.3
+        cid = c.comm_init().commId
+        arrays = [np.full(64, float(r + 1), dtype=np.float32) for r in range(n)]
+        _fill(c, n, arrays)
+        assert c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=256, dtype=DT_FLOAT32)).success
+        assert all(cid in svc._ring_out for _, _, svc in c.devices)
+        t_end = time.time() + 10
+        while any(cid in svc._ring_out for _, _, svc in c.devices) and time.time() < t_end:
+            time.sleep(0.05)
+        assert not any(cid in svc._ring_out for _, _, svc in c.devices)  # idle: closed
+        assert c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=256, dtype=DT_FLOAT32)).success
+        np.testing.assert_array_equal(_read(c, 0, 256, np.float32), np.full(64, 18.0, np.float32))
+        svc0 = c.devices[0][2]
+        assert cid in svc0._ring_out  # reopened by the second call
+        svc0.Abort(pb.AbortRequest(commId=cid, reason="test"), None)
+        assert cid not in svc0._ring_out
+
+
+def test_xgmi_algo_is_never_answered_by_rccl():
+    """an explicit algo 'xgmi' on a comm whose data plane is RCCL
+    must run (or fail as) the xGMI path, never report RCCL's time under that name."""
+    with cluster(n_devices=2, mem_size=1 << 14) as c:
+        cid = c.comm_init().commId
+        c.coord.comms[cid].data_backend = "rccl"
+        with pytest.raises(grpc.RpcError) as e:  # host devices: the xGMI path refuses
+            c.stub.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=64, dtype=DT_FLOAT32, algo="xgmi"))
+        assert "xgmi" in e.value.details().lower() or "xGMI" in e.value.details()
+
+
+def test_pg_comm_with_loopback_store_and_remote_devices_is_refused_and_torn_down():
+    """a 'pg' store bound to 127.0.0.1 is unreachable from devices
+    on other hosts -- CommInit fails at once with a pointer to --store-host
+    instead of every device waiting out its rendezvous timeout; the devices
+    that were set up leave again (CommTeardown)."""
+    from hipdsml.rpc import coordinator as C
+
+    with cluster(n_devices=2, mem_size=1 << 14) as c:
+        torn = []
+        orig = c.coord._teardown_devices
+        c.coord._teardown_devices = lambda comm: (torn.append(comm.id), orig(comm))
+        real = C.is_loopback
+        C.is_loopback = lambda a: a == "127.0.0.1" or (real(a) and a != c.addresses[1])
+        try:
+            with pytest.raises(grpc.RpcError) as e:
+                c.comm_init(backend="pg")
+        finally:
+            C.is_loopback = real
+        assert e.value.code() == grpc.StatusCode.INTERNAL and "--store-host" in e.value.details()
+        assert torn == [0]

@@ -193,19 +193,6 @@ def test_wide_native_evaluate_matches_fp32_forward():
     assert abs(got["loss"] - loss) <= 0.02 * max(1.0, loss), (got, loss)
 
 
-@pytest.mark.parametrize("nb", [4, 3])  # odd epochs: the graph covers two (Wb parity)
-def test_wide_overlapped_wgrad_is_bit_identical(nb):
-    spec = MlpSpec((784, 256, 128, 10))
-    ds = synthetic_mnist(64 * nb, seed=11)
-    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, fused_bwd=False)
-    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, overlap_wgrad=True)
-    a.train_steps(13)
-    b.train_steps(13)
-    a.synchronize(); b.synchronize()
-    assert torch.equal(a.P.cpu(), b.P.cpu())
-    assert torch.equal(a.wb(1).cpu(), b.wb(1).cpu())
-
-
 def test_wide_graph_matches_eager():
     spec = MlpSpec((784, 256, 128, 10))
     ds = synthetic_mnist(64 * 4, seed=5)
@@ -281,112 +268,6 @@ def test_dw_gemm_fused_sgd_and_bias(M, N):
     torch.cuda.synchronize()
     assert (G.cpu() - gW).abs().max().item() < 1e-3
     assert (gb.cpu() - dZT.float().sum(1)).abs().max().item() < 1e-4
-
-
-@pytest.mark.parametrize("dims,rows,batch,split", [((784, 512, 256, 10), 64, 64, "0"),
-                                                   ((784, 512, 256, 10), 256, 64, "1"),
-                                                   ((784, 4096, 4096, 10), 512, 64, "0"),
-                                                   ((784, 4096, 4096, 10), 512, 64, "1"),
-                                                   ((784, 4096, 4096, 10), 1024, 48, "0")], ids=str)
-def test_wide_fused_backward_matches_separate_dgrad(dims, rows, batch, split, monkeypatch):
-    """The fused backward (layer 1's dgrad folded into its weight-update pass,
-    layer 0's update tiles waiting on the dZ_1 blocks in the same launch)
-    against the split-K dgrad GEMM + update launch: the weight updates of
-    layers 1 and 2 use the same products (bit-identical), dZ_1 sums the same
-    products in another order (bf16 outputs within one rounding), and the run
-    is deterministic."""
-    C = require_native()
-    monkeypatch.setenv("HIPDSML_WIDE_BWD_SPLIT", split)  # "0": layer 0 waits inside the fused launch
-    spec = MlpSpec(dims)
-    ds = synthetic_mnist(batch * 4, seed=12)
-    mk = lambda fused: WideMlpTrainer(spec, ds, batch=batch, lr=0.05, seed=7, graph=False, fused_bwd=fused,
-                                      bwd_rows=rows if fused else 0)
-    a, b, c = mk(True), mk(False), mk(True)
-    assert a.fused_bwd and not b.fused_bwd and a.bwd_rows == rows and a.bwd_split == (split == "1")
-    C.wide_bwd_errors(True)
-    for t in (a, b, c):
-        t.train_steps(1)
-        t.synchronize()
-    assert C.wide_bwd_errors(True) == 0
-    dz_a, dz_b = a.dZ[1].float().cpu(), b.dZ[1].float().cpu()
-    scale = dz_b.abs().max().item()
-    assert (dz_a - dz_b).abs().max().item() <= 2 ** -7 * scale, "dZ_1 beyond one bf16 rounding"
-    for l in (1, 2):
-        assert torch.equal(a.wb(l).cpu(), b.wb(l).cpu()), f"layer {l} update differs"
-        assert torch.equal(a.Wlo[l].cpu(), b.Wlo[l].cpu())
-    P_a, P_b = a.P.cpu(), b.P.cpu()
-    rel = (P_a - P_b).norm().item() / max((P_b - init_params(a.layout, 7, "kaiming")).norm().item(), 1e-30)
-    assert rel < 2e-2, rel
-    for t in (a, b, c):
-        t.train_steps(7)  # epoch wrap, both Wb parities
-        t.synchronize()
-    assert torch.equal(a.P.cpu(), c.P.cpu())  # deterministic: slice-ordered partial sums
-    assert C.wide_bwd_errors(True) == 0
-    sa, sb = a.read_stats(), b.read_stats()
-    assert abs(sa.avg_loss - sb.avg_loss) < 0.02 * max(1.0, sb.avg_loss)
-
-
-def test_wide_fused_backward_in_graph_matches_eager():
-    spec = MlpSpec((784, 512, 256, 10))
-    ds = synthetic_mnist(64 * 4, seed=13)
-    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=False, fused_bwd=True)
-    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=True, fused_bwd=True)
-    assert a.fused_bwd and b.fused_bwd
-    a.train_steps(12)
-    b.train_steps(12)
-    a.synchronize(); b.synchronize()
-    assert torch.equal(a.P.cpu(), b.P.cpu())
-
-
-@pytest.mark.parametrize("M,K1", [(64, 784), (40, 784), (64, 1024), (17, 520)])
-def test_wide_fused_forward_matches_two_launches(M, K1):
-    """kernels/wide_fwd.hip: both hidden layers in one launch, bit-exact with
-    gemm_rows64 (layer 1) + gemm_skinny NT (layer 2), over repeated launches
-    (the device-side flag epoch advances) and against fp32 torch."""
-    C = require_native()
-    if not C.wide_fwd2_supported(0):
-        pytest.skip("device cannot hold the 256-workgroup grid")
-    g = torch.Generator().manual_seed(M + K1)
-    X = (0.5 * torch.randn(M, K1, generator=g)).to(torch.bfloat16).to(DEV)
-    W1 = (torch.randn(4096, K1, generator=g) / K1 ** 0.5).to(torch.bfloat16).to(DEV)
-    W2 = (torch.randn(4096, 4096, generator=g) / 64).to(torch.bfloat16).to(DEV)
-    b1 = (0.1 * torch.randn(4096, generator=g)).to(DEV)
-    b2 = (0.1 * torch.randn(4096, generator=g)).to(DEV)
-    ws = torch.zeros(4 * 64 * 4096, device=DEV)
-    ctr = torch.zeros(64, dtype=torch.int32, device=DEV)
-    sync = torch.zeros(260, dtype=torch.int32, device=DEV)
-    bf = dict(dtype=torch.bfloat16, device=DEV)
-    H1r, H2r = torch.zeros(M, 4096, **bf), torch.zeros(M, 4096, **bf)
-    C.gemm_bf16_nt_fused(X, W1, M, 4096, K1, bias=b1, relu=True, obf=H1r, splits=0)
-    C.gemm_skinny(H1r, W2, M, 4096, 4096, bias=b2, relu=True, obf=H2r, ws=ws, ctr=ctr)
-    for it in range(3):
-        H1, H2 = torch.full((M, 4096), 7.0, **bf), torch.full((M, 4096), 7.0, **bf)
-        C.wide_fwd2(X, W1, b1, H1, W2, b2, H2, M, K1, ws, ctr, sync)
-        torch.cuda.synchronize()
-        assert int(sync[258].item()) == 0, "hand-off timed out"
-        assert int(sync[256].item()) == it + 1  # the epoch advanced once per launch
-        assert torch.equal(H1, H1r), it
-        assert torch.equal(H2, H2r), it
-    assert int(ctr.abs().sum().item()) == 0 and int(sync[257].item()) == 0
-    h1 = torch.relu(X.float() @ W1.float().t() + b1)
-    assert (H1.float() - h1).abs().max().item() < 2e-2 * (1 + h1.abs().max().item())
-    h2 = torch.relu(H1.float() @ W2.float().t() + b2)
-    assert (H2.float() - h2).abs().max().item() < 2e-2 * (1 + h2.abs().max().item())
-
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_wide_fused_forward_engine_is_bit_identical(graph):
-    spec = MlpSpec((784, 4096, 4096, 10))
-    ds = synthetic_mnist(64 * 3, seed=17)
-    a = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=graph, fused_fwd=False)
-    b = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=3, graph=graph, fused_fwd=True)
-    if not b.fused_fwd:
-        pytest.skip("fused forward unavailable on this device")
-    a.train_steps(7)
-    b.train_steps(7)
-    a.synchronize(); b.synchronize()
-    assert torch.equal(a.P.cpu(), b.P.cpu())
-    assert torch.equal(a.H[2].cpu(), b.H[2].cpu())
 
 
 @pytest.mark.parametrize("M,K", [(64, 784), (40, 520), (64, 1024)])
