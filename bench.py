@@ -164,6 +164,34 @@ def _dp_phases(tr) -> dict:
         return {"error": str(e)[:200]}
 
 
+def _e2e_10epoch(a, ctx, spec) -> dict:
+    """The reference's only training number as ONE wall-clock span: a 60,000-row
+    training set and a 10,000-row test set generated on the host, trainer
+    construction (upload, Gram table), 10 epochs of 937 batches of 64 (the
+    last partial batch dropped, client.go:596) and the evaluation -- the
+    counterpart of the reference's 732 s (README.md:199-203: 599,680 samples,
+    about 819 samples/s end to end, init included)."""
+    import torch
+
+    from hipdsml.data.mnist import synthetic_mnist
+    from hipdsml.engine.trainer import MlpTrainer
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    train = synthetic_mnist(60000, seed=77, dim=spec.dims[0])
+    test = synthetic_mnist(10000, seed=78, dim=spec.dims[0])
+    tr = MlpTrainer(spec, train, batch=64, lr=a.lr, ctx=ctx, seed=1)
+    t1 = time.perf_counter()
+    res = tr.fit(10, log_fn=lambda _s: None, test=test)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    samples = 10 * tr.nbatches * 64
+    return {"s": round(t2 - t0, 4), "init_s": round(t1 - t0, 4), "train_eval_s": round(t2 - t1, 4),
+            "samples": samples, "steps": 10 * tr.nbatches, "samples_per_s": round(samples / (t2 - t0), 1),
+            "precompute_ms": dict(tr.precompute_ms), "test_accuracy": round(res["test_accuracy"], 2),
+            "reference_s": 732.0, "vs_reference": round(732.0 / (t2 - t0), 1)}
+
+
 def _physical_gpus(ctx) -> int:
     """Distinct GPUs (host, device UUID) the job's ranks run on."""
     import torch
@@ -241,6 +269,9 @@ def run(a) -> int:
     if n > 1 and tr.backend == "hip" and not a.no_allreduce_probe:
         ar_us = allreduce_latency_us(ctx, tr.comm, ring_chunk=a.ring_chunk)
     phys = _physical_gpus(ctx)
+    e2e = None
+    if n == 1 and not a.no_e2e and ctx.device.type == "cuda":
+        e2e = _e2e_10epoch(a, ctx, spec)
     samples = a.batch * n * a.steps
     value = samples / elapsed
     if tr.comm is not None:
@@ -286,6 +317,7 @@ def run(a) -> int:
             "ring_chunk_bytes": tr._ring_chunk if tr.comm is not None else None,
             "ring_chunk_sweep_us": tr.ring_chunk_sweep_us if tr.backend == "hip" else None,
             "allreduce_1MiB_us": ar_us,
+            "e2e_10epoch": e2e,
             "dp_phases_us": phases,
             "train_loss": round(st.avg_loss, 4),
             "train_acc": round(st.accuracy, 2),
@@ -338,6 +370,8 @@ def main(argv=None) -> int:
                     help="skip the 1 MiB all-reduce latency probe that follows the timed steps (N>1)")
     ap.add_argument("--no-stamps", action="store_true",
                     help="skip the stamped diagnostic launch of the persistent DP step (N>1)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end 10-epoch run (data, init, 9,370 steps, eval; N=1)")
     ap.add_argument("--no-sync-sweep", action="store_true",
                     help="skip timing every sync candidate (N>1)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",

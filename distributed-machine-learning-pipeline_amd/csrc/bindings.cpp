@@ -713,6 +713,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_persist_set_stamping", [](bool on) { mlp_persist_set_stamping(on); });
   m.def("mlp_persist_set_stamp_window", [](int first_step) { mlp_persist_set_stamp_window(first_step); },
         "stamp steps first_step .. first_step + 7 of a launch (< 0: off)");
+  m.def("gram_table", [](torch::Tensor Xs, torch::Tensor Xc, int64_t nb, int64_t B, int64_t K) {
+    // Xs: one source [rows][ld] (-> T [nb][64][64]) or [nsrc][rows][ld]
+    // (-> T [nb][nsrc][64][64]); Xc [rows][ld]: the batches the table is for
+    check_cuda_strided(Xs, "Xs");
+    check_cuda_strided(Xc, "Xc");
+    TORCH_CHECK(Xs.scalar_type() == torch::kFloat32 && Xc.scalar_type() == torch::kFloat32,
+                "gram_table: float32 operands");
+    TORCH_CHECK(Xs.dim() == 2 || Xs.dim() == 3, "Xs: [rows][ld] or [nsrc][rows][ld]");
+    TORCH_CHECK(Xc.dim() == 2 && Xc.stride(1) == 1 && Xs.stride(-1) == 1, "rows must be contiguous");
+    TORCH_CHECK(nb >= 1 && B >= 1 && B <= 64 && K >= 1, "gram_table: nb >= 1, 1 <= B <= 64, K >= 1");
+    const int64_t rows = nb * B;
+    const int64_t nsrc = Xs.dim() == 3 ? Xs.size(0) : 1;
+    TORCH_CHECK(Xs.size(-2) >= rows && Xc.size(0) >= rows && Xs.size(-1) >= K && Xc.size(1) >= K,
+                "gram_table: operands hold fewer than nb * B rows or K columns");
+    TORCH_CHECK(Xs.get_device() == Xc.get_device(), "gram_table: operands on one GPU");
+    const int64_t sstride = Xs.dim() == 3 ? Xs.stride(0) : 0;
+    auto T = torch::empty(Xs.dim() == 3 ? std::vector<int64_t>{nb, nsrc, 64, 64} : std::vector<int64_t>{nb, 64, 64},
+                          Xc.options());
+    hip_ok(gram_table(Xs.data_ptr<float>(), sstride, Xs.stride(-2), Xc.data_ptr<float>(), Xc.stride(0), (int)nb,
+                      (int)B, (int)K, (int)nsrc, T.data_ptr<float>(), cur_stream()),
+           "gram_table");
+    return T;
+  }, py::arg("Xs"), py::arg("Xc"), py::arg("nb"), py::arg("B"), py::arg("K"),
+     "Gram tables of the persistent step's Gram form (kernels/gram.hip; engine/gram.py is the "
+     "float64 torch oracle)");
+  m.def("mlp_persist_set_pkx_helpers", [](int h) { mlp_persist_set_pkx_helpers(h); }, py::arg("helpers"),
+        "pkx dW1 helper blocks per layer-1 block: -1 default (3 from 4 replicas on), 0, 1 or 3");
   m.def("mlp_persist_set_probe", [](int mode) { mlp_persist_set_probe(mode); },
         "testing only: 0 off; 1 peers' dZ1 rows taken as arrived (lone-replica probe of the Gram "
         "forms); 2 mirror: every push loops back into this replica's own buffer in the peer's "

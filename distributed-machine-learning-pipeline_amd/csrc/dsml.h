@@ -96,6 +96,13 @@ void mlp_persist_set_stamping(bool on);
 void mlp_persist_set_stamp_window(int first_step);  // stamp steps first..first+7 (< 0: off)
 void mlp_persist_set_jitter(int ticks);  // testing only: uneven-load injection (0 = off)
 int64_t mlp_persist_xbuf_granules();
+// Gram tables of the persistent step's Gram form (kernels/gram.hip):
+// T[b][r][m'][m] = Xs_r(b-1)[m'] . Xc(b)[m] + 1 over K features, fp64
+// accumulation rounded to fp32; source r at Xs + r * src_stride floats, rows
+// of ld_src / ldc floats (multiples of 4, 16-B aligned bases); batches of B
+// <= 64 rows padded to 64 by repeating the last row; T [nb][nsrc][64][64].
+hipError_t gram_table(const float* Xs, int64_t src_stride, int64_t ld_src, const float* Xc, int64_t ldc, int nb,
+                      int B, int K, int nsrc, float* T, hipStream_t s);
 hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels, float* P,
                              int64_t* ctr, const MlpDesc& d, float lr, int steps, uint64_t* xb,
                              float* stats, uint32_t* err, uint32_t* herr, uint64_t timeout_ticks,
@@ -104,6 +111,9 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              const float* gram = nullptr, int carry = 0,
                              const float* xsw = nullptr, int64_t xsw_stride = 0);
 void mlp_persist_set_probe(int mode);  // testing only: 0 off, 1 lone-replica probe, 2 mirror
+// pkx dW1 helper blocks per layer-1 block: -1 the default (3 from 4 replicas on,
+// else 0; HIPDSML_PKX_HELPERS overrides it), 0, 1 or 3 (tuning / testing)
+void mlp_persist_set_pkx_helpers(int helpers);
 // Single replica: the Gram table the persistent step reads, float[nbatches][64][64]
 // with G1T[b][m'][m] = X_{b-1}[m'] . X_b[m] + 1 (rows past the batch repeat its
 // last row; b - 1 wraps), and `carry` = 1 when the hand-off buffer still holds

@@ -63,6 +63,8 @@
 // Every wait is bounded (timeout -> error word, checked by the host after the
 // launch) and gives up at once when another block already timed out, so a
 // fault ends the launch instead of hanging the GPU.
+#include <cstdlib>
+
 #include "common.h"
 #include "../dsml.h"
 
@@ -84,13 +86,21 @@ constexpr int kNPart = kNL1;                            // partial slots per par
 // ~16 MFMAs instead of a quarter of the update.  All upper blocks (chains +
 // tiles) sit at blockIdx 8 k; layer-1 block (gn, gk) at blockIdx 8 gn + gk + 1.
 template <int NL> struct GTile { static constexpr int kN = NL == 3 ? 16 : 8; };
-template <int NL> constexpr int pk_grid(bool dp) { return dp ? kNBlk : 8 * (kNCH + GTile<NL>::kN); }
-// Whether blockIdx b does work in the Gram-form grid (the rest exit); `helpers`:
-// pkx at >= 4 replicas also runs a dW1 helper per layer-1 block at
-// blockIdx 8 (8 + gn) + gk + 1, on its owner's XCD.
-template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, bool helpers = false) {
-  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < (helpers ? 2 * kGN : kGN);
+constexpr int cmax0(int a, int b) { return a > b ? a : b; }
+// pkx: up to 3 dW1 helper blocks per layer-1 block (helper h = 1..3 of block
+// (gn, gk) at blockIdx 8 (8 h + gn) + gk + 1, on its owner's XCD: with 3 the
+// layer-1 roles fill XCDs 1-7, 32 CUs each).
+constexpr int kMaxHelpers = 3;
+template <int NL> constexpr int pk_grid(bool dp, int helpers = 0) {
+  return dp ? kNBlk : 8 * cmax0(kNCH + GTile<NL>::kN, (1 + helpers) * kGN);
 }
+// Whether blockIdx b does work in the Gram-form grid (the rest exit).
+template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, int helpers = 0) {
+  return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < (1 + helpers) * kGN;
+}
+// Replicas [pk_hlo(N, H, k), pk_hlo(N, H, k + 1)) of the global-batch dW1 go to
+// part k of a layer-1 tile (k = 0: the owner, k = h: helper h), rank order.
+__host__ __device__ constexpr int pk_hlo(int n, int helpers, int k) { return k * n / (1 + helpers); }
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
 
@@ -216,12 +226,18 @@ constexpr int64_t kOffCg = kOffWf + 8;
 constexpr int kWXS = kH2 * kD1 + 16 * kH2 + kH2 + 16;   // 9296 floats
 constexpr int64_t kOffWxs = kOffCg + kB * kD1;
 constexpr int64_t kOffWfs = kOffWxs + 2 * kWXS / 2;
-// HX[2][56][4 waves][64 lanes][8]: pkx at >= 4 replicas, the helper blocks'
-// half of every layer-1 tile's dW1 (and db1), parity by step, plain fp32; HF[2][64]
-// flags, one per tile.
+// HX[2][3][56][4 waves][64 lanes][8]: pkx with helpers, helper h's share of
+// every layer-1 tile's dW1 (and db1) at [parity][h - 1], plain fp32;
+// HF[2][3][64] flags, one per tile and helper.
 constexpr int64_t kOffHx = kOffWfs + 32;
-constexpr int64_t kOffHf = kOffHx + 2 * kNL1 * 4 * 64 * 8 / 2;
-constexpr int64_t kTotalG = kOffHf + 2 * 64;
+constexpr int64_t kOffHf = kOffHx + 2 * kMaxHelpers * kNL1 * 4 * 64 * 8 / 2;
+constexpr int64_t kTotalG = kOffHf + 2 * kMaxHelpers * 64;
+__device__ __forceinline__ int64_t pk_hx_off(uint64_t s, int h, int lb, int w, int lane) {  // floats
+  return kOffHx * 2 + (((((int64_t)(s & 1) * kMaxHelpers + (h - 1)) * kNL1 + lb) * 4 + w) * 64 + lane) * 8;
+}
+__device__ __forceinline__ int64_t pk_hf(uint64_t s, int h, int lb) {
+  return kOffHf + ((int64_t)(s & 1) * kMaxHelpers + (h - 1)) * 64 + lb;
+}
 static_assert(kCX % 4 == 0 && kWX % 4 == 0 && (kOffCx % 2) == 0 && (kOffWx % 2) == 0,
               "exchange rows travel as 16-B vectors");
 
@@ -293,9 +309,21 @@ __device__ __forceinline__ bool wait_flag(__amdgpu_buffer_rsrc_t r, int64_t g, u
   return true;
 }
 
+// The wave's index in its workgroup, provably wave-uniform (threadIdx.x >> 6 is
+// uniform per wave, but the compiler's divergence analysis cannot see it):
+// slot numbers and descriptors derived from it then stay in SGPRs.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// The launch's first step, made wave-uniform: every lane loads the same word,
+// and a value the compiler can prove uniform keeps every step-derived offset
+// (parity halves, DZR slots, tags) in SGPRs -- otherwise each buffer access
+// through a descriptor built from it runs in a readfirstlane waterfall loop
+// (r5: the pkx exchange loads and pushes, 0.2-0.3 us apiece).
 __device__ __forceinline__ uint64_t ld_ctr64(const int64_t* p) {
-  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // ---- replica exchange (nrep > 1): 16-B vector accesses at system scope
@@ -340,6 +368,9 @@ __device__ int g_pk_probe;
 // result must equal single-replica SGD at the same lr (tests/test_gpu_persist.py
 // covers pkx and its helper blocks at N = 4 and 8 on one GPU this way).
 static int g_pk_probe_mode = 0;
+// pkx helper count override (-1: the default by replica count; set from
+// HIPDSML_PKX_HELPERS at the first data-parallel launch)
+static int g_pkx_helpers = -2;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;
   uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
@@ -409,7 +440,8 @@ struct PersistArgs {
   const float* xsw;
   int64_t xsw_stride;
   int32_t dzr3;
-  int32_t helpers;  // pkx at >= 4 replicas: replicas [ (nrep+1)/2, nrep ) of dW1 on helper blocks
+  int32_t helpers;  // pkx: dW1 helper blocks per layer-1 block (0..3); part k sums replicas
+                    // [pk_hlo(nrep, helpers, k), pk_hlo(.., k + 1))
   int32_t mirror;   // testing only (g_pk_probe_mode 2): pushes loop back into this replica's buffer
   int32_t probe;    // testing only (g_pk_probe_mode 1): peers' tagged data taken as arrived
 };
@@ -462,8 +494,12 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint64_t tag = s + 1;
-  for (int d = 0; d < a.nrep; ++d) {
-    if (d == a.rep) continue;
+  // peers unrolled to compile-time indices: a.xt.buf[d] is then a kernarg
+  // (scalar) load, not a vector load + vmcnt(0) (which would wait for the
+  // previous peer's pushes) + a readfirstlane waterfall per store
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= a.nrep || d == a.rep) continue;
     const __amdgpu_buffer_rsrc_t r =
         rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot + (int64_t)d * per_src
                       : a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
@@ -473,12 +509,14 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   // every peer's memory acknowledged the slot before its flag: the
   // system-scope release of this protocol (common.h, "Cross-device release")
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0)
-    for (int d = 0; d < a.nrep; ++d)
-      if (d != a.rep)
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kMaxPeers; ++d)
+      if (d < a.nrep && d != a.rep)
         __hip_atomic_store((px_g64*)(a.mirror ? a.xt.flags[a.rep] + slot + d * a.pxslots
                                               : a.xt.flags[d] + slot + a.rep * a.pxslots),
                            tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   bool ok = true;
   if (lane < a.nrep && lane != a.rep)
     ok = poll_flag_ge<1>(a.xt.flags[a.rep] + slot + lane * a.pxslots, tag, a.xerr, a.timeout_ticks);
@@ -531,9 +569,10 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const int64_t ag = (int64_t)n * per_src;  // all-gather region of a parity half
   const uint64_t tag = s + 1;
-  // ---- reduce-scatter: values to their owner ----
-  for (int d = 0; d < n; ++d) {
-    if (d == me) continue;
+  // ---- reduce-scatter: values to their owner (peers unrolled: scalar buf[d]) ----
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= n || d == me) continue;
     const __amdgpu_buffer_rsrc_t r =
         rsrc(a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)me * per_src);
     if (own == d) {
@@ -542,11 +581,13 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // system-scope release (common.h)
-  if (lane == 0)
-    for (int d = 0; d < n; ++d)
-      if (d != me)
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kMaxPeers; ++d)
+      if (d < n && d != me)
         __hip_atomic_store((px_g64*)(a.xt.flags[d] + slot + me * a.pxslots), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   bool ok = true;
   if (lane < n && lane != me)
     ok = poll_flag_ge<1>(a.xt.flags[me] + slot + lane * a.pxslots, tag, a.xerr, a.timeout_ticks);
@@ -570,8 +611,9 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
     for (int j = 0; j < NV; ++j) v[j] = acc[j];
   }
   // ---- all-gather: the owner's sums to every peer ----
-  for (int d = 0; d < n; ++d) {
-    if (d == me) continue;
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= n || d == me) continue;
     const __amdgpu_buffer_rsrc_t r = rsrc(a.xt.buf[d] + poff + ag + (int64_t)slot * kPxSlot);
     if (own == me) {
 #pragma unroll
@@ -579,11 +621,13 @@ __device__ __forceinline__ bool px_allreduce2_wave(const PersistArgs& a, uint64_
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0)
-    for (int d = 0; d < n; ++d)
-      if (d != me)
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kMaxPeers; ++d)
+      if (d < n && d != me)
         __hip_atomic_store((px_g64*)(a.xt.flags[d] + n * a.pxslots + me * a.pxslots + slot), tag,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   ok = true;
   if (lane < n && lane != me)
     ok = poll_flag_ge<1>(a.xt.flags[me] + n * a.pxslots + lane * a.pxslots + slot, tag, a.xerr,
@@ -692,6 +736,90 @@ __device__ __forceinline__ bool px_allreduce_tagged_wave(const PersistArgs& a, u
   return true;
 }
 
+// The same tagged one-shot sum split over two waves (the Gram forms' gradient
+// tiles): vmcnt retires loads and stores in issue order, so a wave that polls
+// after pushing waits for every push's write acknowledgement -- a round trip
+// to the peers' (uncached) memory per poll, 6.4 us a step at 8 replicas in the
+// lone-replica probe (profiles/r5_pkx_stamps_base.jsonl).  One wave pushes
+// every slot of its block (px_tagged_push, never drained here); the slots'
+// own waves poll and sum (px_tagged_gather) with no store outstanding.
+__device__ __forceinline__ void px_tagged_push(const PersistArgs& a, uint64_t s, float4 v, int slot) {
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
+  const uint32_t tag = (uint32_t)(s + 1);
+  const nu4v lo = {__float_as_uint(v.x), tag, __float_as_uint(v.y), tag};
+  const nu4v hi = {__float_as_uint(v.z), tag, __float_as_uint(v.w), tag};
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= a.nrep || d == a.rep) continue;
+    const __amdgpu_buffer_rsrc_t r =
+        rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot + (int64_t)d * per_src
+                      : a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
+    __builtin_amdgcn_raw_buffer_store_b128(lo, r, (lane * 16) * 4, 0, kScSys);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, r, (lane * 16 + 4) * 4, 0, kScSys);
+  }
+}
+// v (this replica's value) <- the rank-ordered sum of every replica's `slot`;
+// false: a source did not arrive in time (error word raised).
+__device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t s, float4& v, int slot) {
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
+  const uint32_t tag = (uint32_t)(s + 1);
+  const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot;
+  nu4v g[kMaxPeers][2];
+  uint32_t need = 0;
+#pragma unroll
+  for (int src = 0; src < kMaxPeers; ++src)
+    if (src < a.nrep && src != a.rep) need |= 1u << src;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t spins = 0;
+  bool ok = true;
+  while (need != 0u) {
+#pragma unroll
+    for (int src = 0; src < kMaxPeers; ++src) {
+      if (need & (1u << src)) {
+        const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
+        g[src][0] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane * 16) * 4, 0, kScSys);
+        g[src][1] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane * 16 + 4) * 4, 0, kScSys);
+      }
+    }
+#pragma unroll
+    for (int src = 0; src < kMaxPeers; ++src) {
+      if ((need & (1u << src)) &&
+          ((g[src][0].y == tag && g[src][0].w == tag && g[src][1].y == tag && g[src][1].w == tag) || a.probe))
+        need &= ~(1u << src);
+    }
+    if (__builtin_amdgcn_ballot_w64(need != 0u) == 0) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      __hip_atomic_fetch_or(a.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok = false;
+      break;
+    }
+    if ((++spins & 63u) == 0u &&
+        __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      ok = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  if (!ok) return false;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int src = 0; src < kMaxPeers; ++src) {
+    if (src < a.nrep) {
+      const float4 y = src == a.rep ? v
+                                    : make_float4(__uint_as_float(g[src][0].x), __uint_as_float(g[src][0].z),
+                                                  __uint_as_float(g[src][1].x), __uint_as_float(g[src][1].z));
+      acc.x += y.x; acc.y += y.y; acc.z += y.z; acc.w += y.w;
+    }
+  }
+  v = acc;
+  return true;
+}
+
 template <int NV>
 __device__ __forceinline__ bool px_sum_wave(const PersistArgs& a, uint64_t s, float4 (&v)[NV], int slot) {
   return a.algo ? px_allreduce2_wave<NV>(a, s, v, slot) : px_allreduce_wave<NV>(a, s, v, slot);
@@ -774,7 +902,7 @@ template <bool DP>
 __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int lb, int blk) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
@@ -1049,7 +1177,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   constexpr bool XM = XMODE >= 1, XL = XMODE == 2;
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16, k0 = gk * kKC;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
@@ -1164,9 +1292,16 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
         }
       }
     }
-    // pkx: replica 0's dW1 operands are data only -- in flight during the waits
-    float4 xB[2][4];
-    if constexpr (XL) xl_load(xB, 0, s);
+    // pkx: the dW1 operands of this block's first (up to 3) replicas are data
+    // only -- all in flight during the waits, so the dW1 passes find them in
+    // registers instead of waiting one load latency per replica
+    float4 xP[3][2][4];
+    const int own_hi = XL ? pk_hlo(a.nrep, a.helpers, 1) : 0;
+    if constexpr (XL) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (j < own_hi) xl_load(xP[j], j, s);
+    }
     if (gat && w == c && !pk_l1_gather_rows(rb, zs, parn, gn, c, tagn, poll, lane, i, q)) ok = false;
     PK_STAMP(0, 1);
     pk_jit(jit, blk, s, 2);
@@ -1188,7 +1323,8 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
       Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
     }
-    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false) && pk_sr_active<NL>(tid, a.helpers) && ok) {
+    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false, a.helpers) && pk_sr_active<NL>(tid, a.helpers) &&
+        ok) {
       // hand the step counter on once every block has read it (SF tags)
       const uint32_t t0 = (uint32_t)(s0 + 1);
       poll.start();
@@ -1307,14 +1443,13 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
           }
         }
       };
-      float4 xC[2][4];
-      const int hi = a.helpers ? (a.nrep + 1) / 2 : a.nrep;  // the helper sums [hi, nrep)
-      for (int r = 0; r < hi; r += 2) {
-        if (r + 1 < hi) xl_load(xC, r + 1, s);
-        pass(xB, r);
-        if (r + 1 < hi) {
-          if (r + 2 < hi) xl_load(xB, r + 2, s);
-          pass(xC, r + 1);
+      // replicas [0, own_hi) here, rank order; a set is reloaded for replica
+      // j + 3 once pass j has consumed it (only with fewer helpers than the default)
+#pragma unroll
+      for (int j = 0; j < kMaxPeers; ++j) {
+        if (j < own_hi) {
+          pass(xP[j % 3], j);
+          if (j + 3 < own_hi) xl_load(xP[j % 3], j + 3, s);
         }
       }
       if (w == 3) {
@@ -1323,17 +1458,29 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
         db += __shfl_xor(db, 32, 64);
       }
       if (a.helpers) {
-        // the helper's half (same fragment layout), added in a fixed order
+        // the helpers' parts (same fragment layout), added in helper order
         bool hok = true;
-        if (lane == 0) hok = wait_flag(rb, kOffHf + (int64_t)(s & 1) * 64 + lb, tag, poll);
+        if (lane < a.helpers) hok = wait_flag(rb, pk_hf(s, lane + 1, lb), tag, poll);
         hok = __builtin_amdgcn_ballot_w64(!hok) == 0;
         asm volatile("" ::: "memory");
-        const int64_t ho = kOffHx * 2 + ((((int64_t)(s & 1) * kNL1 + lb) * 4 + w) * 64 + lane) * 8;
-        const f4v h0v = ld_f4(rb, ho), h1v = ld_f4(rb, ho + 4);
+        f4v hv[kMaxHelpers][2];
+#pragma unroll
+        for (int h = 0; h < kMaxHelpers; ++h) {
+          if (h < a.helpers) {
+            const int64_t ho = pk_hx_off(s, h + 1, lb, w, lane);
+            hv[h][0] = ld_f4(rb, ho);
+            hv[h][1] = ld_f4(rb, ho + 4);
+          }
+        }
         if (hok) {
-          g[0] = g[0] + f32x4{h0v[0], h0v[1], h0v[2], h0v[3]};
-          if (w < 3) g[1] = g[1] + f32x4{h1v[0], h1v[1], h1v[2], h1v[3]};
-          else db += h1v[0];
+#pragma unroll
+          for (int h = 0; h < kMaxHelpers; ++h) {
+            if (h < a.helpers) {
+              g[0] = g[0] + f32x4{hv[h][0][0], hv[h][0][1], hv[h][0][2], hv[h][0][3]};
+              if (w < 3) g[1] = g[1] + f32x4{hv[h][1][0], hv[h][1][1], hv[h][1][2], hv[h][1][3]};
+              else db += hv[h][1][0];
+            }
+          }
         }
         ok = __syncthreads_and(hok ? 1 : 0) != 0;
         if (!ok) break;
@@ -1403,23 +1550,25 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   if (lb == 0) PK_EDGE(2);
 }
 
-// pkx helper block (>= 4 replicas): replicas [(nrep + 1) / 2, nrep) of the dW1
-// tile (and db1) of layer-1 block lb, computed exactly as the owner computes
-// its half and handed over through HX[parity] + one flag; the owner adds it to
-// its own half in a fixed order.  Same XCD as the owner, so the shared X
+// pkx helper block h (1..a.helpers) of layer-1 block lb: replicas
+// [pk_hlo(N, H, h), pk_hlo(N, H, h + 1)) of the tile's dW1 (and db1), computed
+// exactly as the owner computes its part, operands prefetched at step start,
+// and handed over through HX[parity][h - 1] + one flag; the owner adds the
+// helpers' parts in helper order.  Same XCD as the owner, so the shared X
 // slices and the hand-off stay in that XCD's L2.
-__device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, int lb, int blk) {
+__device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, int lb, int h, int blk) {
   const int gn = lb % kGN, gk = lb / kGN;
   const int n0 = gn * 16;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
   const uint64_t s0 = ld_ctr64(a.ctr + 1);
   pk_started(a, blk, s0);
-  float* Dh = lds;  // dZ1 tiles of replicas h0 .. nrep - 1: [nrep - h0][64][17]
+  float* Dh = lds;  // dZ1 tiles of replicas h0 .. h1 - 1: [h1 - h0][64][17]
   const int probe = g_pk_probe;
-  const int h0 = (a.nrep + 1) / 2;
+  const int h0 = pk_hlo(a.nrep, a.helpers, h), h1 = pk_hlo(a.nrep, a.helpers, h + 1);
+  const int cnt = h1 - h0;
   const int kt0 = kKC / 16 * gk + w, kt1 = kKC / 16 * gk + (w < 3 ? w + 4 : w);
   auto xl_load = [&](float4 (&B)[2][4], int r, uint64_t s) __attribute__((always_inline)) {
     const float* xr = a.xsw + (int64_t)r * a.xsw_stride +
@@ -1434,8 +1583,10 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
   for (int it = 0; it < a.steps && ok; ++it) {
     const uint64_t s = s0 + (uint64_t)it;
     const uint32_t tag = (uint32_t)(s + 1);
-    float4 xB[2][4], xC[2][4];
-    xl_load(xB, h0, s);  // data only: in flight during the waits
+    float4 xP[3][2][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j < cnt) xl_load(xP[j], h0 + j, s);  // data only: in flight during the waits
     if (probe) {
       // lone-replica probe: the peers' rows are taken as arrived, so pace this
       // block on the own replica's dZ1 (the owner's wait) instead of running ahead
@@ -1449,13 +1600,13 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
       }
     }
     {
-      // this half's dZ1 tiles: own rows from the local DZ1 region, the peers'
+      // this part's dZ1 tiles: own rows from the local DZ1 region, the peers'
       // from their DZR slots, every load of a round in flight together
       const int m = tid >> 2, qq = tid & 3;
       uint32_t need = 0;
 #pragma unroll
       for (int r2 = 0; r2 < kMaxPeers; ++r2)
-        if (r2 >= h0 && r2 < a.nrep) need |= 1u << r2;
+        if (r2 >= h0 && r2 < h1) need |= 1u << r2;
       poll.start();
       while (need != 0u) {
         nu4v v0[kMaxPeers], v1[kMaxPeers];
@@ -1516,12 +1667,11 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
         }
       }
     };
-    for (int r = h0; r < a.nrep; r += 2) {
-      if (r + 1 < a.nrep) xl_load(xC, r + 1, s);
-      pass(xB, r);
-      if (r + 1 < a.nrep) {
-        if (r + 2 < a.nrep) xl_load(xB, r + 2, s);
-        pass(xC, r + 1);
+#pragma unroll
+    for (int j = 0; j < kMaxPeers; ++j) {
+      if (j < cnt) {
+        pass(xP[j % 3], h0 + j);
+        if (j + 3 < cnt) xl_load(xP[j % 3], h0 + j + 3, s);
       }
     }
     if (w == 3) {
@@ -1529,14 +1679,14 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
       db += __shfl_xor(db, 16, 64);
       db += __shfl_xor(db, 32, 64);
     }
-    // hand the half over: the owner's fragment layout, plain fp32 drained by
+    // hand the part over: the owner's fragment layout, plain fp32 drained by
     // every wave, then one flag
-    const int64_t ho = kOffHx * 2 + ((((int64_t)(s & 1) * kNL1 + lb) * 4 + w) * 64 + lane) * 8;
+    const int64_t ho = pk_hx_off(s, h, lb, w, lane);
     st_f4(rb, ho, f4v{g[0][0], g[0][1], g[0][2], g[0][3]});
     st_f4(rb, ho + 4, w < 3 ? f4v{g[1][0], g[1][1], g[1][2], g[1][3]} : f4v{db, 0.f, 0.f, 0.f});
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) st_gran(rb, kOffHf + (int64_t)(s & 1) * 64 + lb, __uint_as_float(tag), tag);
+    if (tid == 0) st_gran(rb, pk_hf(s, h, lb), __uint_as_float(tag), tag);
   }
   pk_report(a, ok);
 }
@@ -1751,7 +1901,7 @@ __device__ __forceinline__ void pk_drain_rows(int nrep) {
 template <int NL, bool DP, bool XM = false>
 __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c, int blk) {
   using L = ChLay<NL>;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const int rb0 = 16 * c;  // first batch row of this chain
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
@@ -2151,7 +2301,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 template <int NL, bool DP>
 __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g, int blk) {
   using L = GLay<NL>;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
@@ -2464,12 +2614,15 @@ struct GTLay {
   static constexpr int W2 = DZ3T + 16 * kST;    // tile [16][33]
   static constexpr int W3 = W2 + 16 * 33;       // [16 o][17]
   static constexpr int B = W3 + 16 * 17;        // b2 slice [16], b3 [16]
-  static constexpr int TOTAL = B + 32;
+  static constexpr int STG = B + 32;            // data parallel: the slots' values [3][64 lanes] f4
+  static constexpr int BST = STG + 3 * 256;     // data parallel: bias partials [2][16]
+  static constexpr int TOTAL = BST + 32;
 };
+static_assert(GTLay::STG % 4 == 0, "slot stage: 16-B aligned");
 
 template <int NL, bool XM>
 __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g, int blk) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int i = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
@@ -2482,6 +2635,10 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
   float* W2 = lds + GTLay::W2;
   float* W3 = lds + GTLay::W3;
   float* Bs = lds + GTLay::B;
+  float4* Stg = reinterpret_cast<float4*>(lds + GTLay::STG);
+  float* Bst = lds + GTLay::BST;
+  __shared__ uint32_t s_xfail;  // a wave's exchange gave up (set once: the loop then ends)
+  if (tid == 0) s_xfail = 0u;
   // tile geometry: W2 rows r0 .. r0 + 15 (3 layers: h; 2 layers: class o),
   // columns n0 .. n0 + nw - 1
   constexpr int nw = NL == 3 ? 32 : 16;
@@ -2602,19 +2759,47 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
       PK_STAMP(2, 2);
       if constexpr (XM) {  // data parallel: this wave's gradients summed over the replicas
         bool xok = true;
-        float4 v[1];
-        if (w < 2 || (w == 2 && own3)) {
-          v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
-          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
-          gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
-        } else if (w == 3 && (own3 || g == 0)) {
-          v[0] = make_float4(sb, sb3, 0.f, 0.f);
-          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
-          sb = v[0].x;
-          sb3 = v[0].y;
+        if (a.algo == 0) {
+          // tagged one-shot, pushes on wave 3 (px_tagged_push): the bias
+          // partials ride in the dW3 slot's padding rows o = 12, 13 (q == 3),
+          // so a tile has 2 slots (3 with W3), and wave 3 -- which only
+          // pushes -- never polls behind its own stores
+          if (w == 3 && q == 0) { Bst[i] = sb; Bst[16 + i] = sb3; }
+          lds_barrier();
+          const int nslot = own3 ? 3 : 2;
+          if (w == 2 && own3 && q == 3) { gw[0] = Bst[i]; gw[1] = Bst[16 + i]; }
+          if (w < nslot) Stg[w * 64 + lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+          lds_barrier();
+          PK_STAMP(2, 5);
+          if (w == 3) {
+            for (int sl = 0; sl < nslot; ++sl) px_tagged_push(a, s, Stg[sl * 64 + lane], kNL1 * 4 + 4 * g + sl);
+          } else if (w < nslot) {
+            float4 v = make_float4(gw[0], gw[1], gw[2], gw[3]);
+            xok = px_tagged_gather(a, s, v, kNL1 * 4 + 4 * g + w);
+            gw = f32x4{v.x, v.y, v.z, v.w};
+            if (w == 2 && q == 3) { sb = gw[0]; sb3 = gw[1]; }
+          }
+          PK_STAMP(2, 6);
+          // agreed without a vector-memory drain (wave 3's pushes stay in flight)
+          if (!xok) s_xfail = 1u;
+          lds_barrier();
+          PK_STAMP(2, 7);
+          if (s_xfail != 0u) { ok = false; break; }
+        } else {
+          float4 v[1];
+          if (w < 2 || (w == 2 && own3)) {
+            v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+            xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+            gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
+          } else if (w == 3 && (own3 || g == 0)) {
+            v[0] = make_float4(sb, sb3, 0.f, 0.f);
+            xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+            sb = v[0].x;
+            sb3 = v[0].y;
+          }
+          ok = __syncthreads_and(xok ? 1 : 0) != 0;
+          if (!ok) break;
         }
-        ok = __syncthreads_and(xok ? 1 : 0) != 0;
-        if (!ok) break;
       }
       // ---- SGD on the resident tile ----
       if (w < 2) {
@@ -2624,7 +2809,11 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (4 * q + r < kNC) W3[(4 * q + r) * 17 + i] -= a.lr * gw[r];
-      } else if (w == 3 && q == 0) {
+        if (XM && a.algo == 0 && q == 3) {  // the summed bias partials (packed rows 12, 13)
+          Bs[i] -= a.lr * sb;
+          if (g == 0 && i < kNC) Bs[16 + i] -= a.lr * sb3;
+        }
+      } else if (w == 3 && q == 0 && !(XM && a.algo == 0)) {
         if (own3) Bs[i] -= a.lr * sb;
         if (g == 0 && i < kNC) Bs[16 + i] -= a.lr * sb3;
       }
@@ -2634,55 +2823,81 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
       PK_STAMP(2, 2);
       if constexpr (XM) {
         bool xok = true;
-        float4 v[1];
-        if (w == 0) {
-          v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
-          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
-          gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
-        } else if (w == 1 && g == 0) {
-          v[0] = make_float4(sb, 0.f, 0.f, 0.f);
-          xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
-          sb = v[0].x;
+        if (a.algo == 0) {
+          // tagged one-shot, pushes on wave 3: the b2 partial rides in the dW2
+          // slot's padding row o = 12 (q == 3)
+          if (w == 1 && q == 0) Bst[i] = sb;
+          lds_barrier();
+          if (w == 0 && q == 3) gw[0] = Bst[i];
+          if (w == 0) Stg[lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+          lds_barrier();
+          if (w == 3) {
+            px_tagged_push(a, s, Stg[lane], kNL1 * 4 + 4 * g);
+          } else if (w == 0) {
+            float4 v = make_float4(gw[0], gw[1], gw[2], gw[3]);
+            xok = px_tagged_gather(a, s, v, kNL1 * 4 + 4 * g);
+            gw = f32x4{v.x, v.y, v.z, v.w};
+            if (q == 3) sb = gw[0];
+          }
+          if (!xok) s_xfail = 1u;
+          lds_barrier();
+          if (s_xfail != 0u) { ok = false; break; }
+        } else {
+          float4 v[1];
+          if (w == 0) {
+            v[0] = make_float4(gw[0], gw[1], gw[2], gw[3]);
+            xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+            gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
+          } else if (w == 1 && g == 0) {
+            v[0] = make_float4(sb, 0.f, 0.f, 0.f);
+            xok = px_sum_wave_g<1>(a, s, v, kNL1 * 4 + 4 * g + w);
+            sb = v[0].x;
+          }
+          ok = __syncthreads_and(xok ? 1 : 0) != 0;
+          if (!ok) break;
         }
-        ok = __syncthreads_and(xok ? 1 : 0) != 0;
-        if (!ok) break;
       }
       if (w == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (4 * q + r < kNC) W2[(4 * q + r) * 33 + i] -= a.lr * gw[r];
-      } else if (w == 1 && g == 0 && q == 0 && i < kNC) {
+        if (XM && a.algo == 0 && q == 3 && g == 0 && i < kNC) Bs[i] -= a.lr * sb;
+      } else if (w == 1 && g == 0 && q == 0 && i < kNC && !(XM && a.algo == 0)) {
         Bs[i] -= a.lr * sb;
       }
     }
-    __syncthreads();
+    lds_barrier();  // no vector-memory drain: wave 3's pushes (data parallel) stay in flight
     PK_STAMP(2, 3);
     pk_jit(jit, blk, s, 5);
-    // ---- publish the tile into WXS[par] (the chains' order) ----
-    {
+    // ---- publish the tile into WXS[par] (the chains' order), by waves 0-2:
+    // W2 tile f4 0 .. kT4-1, then (W3 owners) 64 W3 f4 and 4 b2 f4, then (tile 0) 4 b3 f4 ----
+    if (w < 3) {
       const int64_t base = kOffWxs * 2 + (int64_t)par * kWXS;
       constexpr int kT4 = 16 * nw / 4;  // f4 of the W2 tile
-      if (tid < kT4) {
-        const int r = tid / (nw / 4), c4 = tid - r * (nw / 4);
-        const float* src = W2 + r * 33 + 4 * c4;
-        st_up4(rb, base + (int64_t)(r0 + r) * kD1 + n0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
-      } else if (NL == 3 && own3 && tid < kT4 + 64) {
-        const int x = tid - kT4, o = x >> 2, c4 = x & 3;
-        const float* src = W3 + o * 17 + 4 * c4;
-        st_up4(rb, base + kH2 * kD1 + o * kH2 + r0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
-      } else if (NL == 3 && own3 && tid < kT4 + 68) {
-        const int c4 = tid - kT4 - 64;
-        st_up4(rb, base + kH2 * kD1 + 16 * kH2 + r0 + 4 * c4,
-               f4v{Bs[4 * c4], Bs[4 * c4 + 1], Bs[4 * c4 + 2], Bs[4 * c4 + 3]}, local);
-      } else if (g == 0 && tid >= 200 && tid < 204) {
-        const int c4 = tid - 200;
-        const float* src = Bs + (NL == 3 ? 16 : 0) + 4 * c4;
-        st_up4(rb, base + (NL == 3 ? kH2 * kD1 + 16 * kH2 + kH2 : 16 * kD1) + 4 * c4,
-               f4v{src[0], src[1], src[2], src[3]}, local);
+      const int nitem = kT4 + (NL == 3 && own3 ? 68 : 0) + (g == 0 ? 4 : 0);
+      for (int x = tid; x < nitem; x += 192) {
+        if (x < kT4) {
+          const int r = x / (nw / 4), c4 = x - r * (nw / 4);
+          const float* src = W2 + r * 33 + 4 * c4;
+          st_up4(rb, base + (int64_t)(r0 + r) * kD1 + n0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
+        } else if (NL == 3 && own3 && x < kT4 + 64) {
+          const int y = x - kT4, o = y >> 2, c4 = y & 3;
+          const float* src = W3 + o * 17 + 4 * c4;
+          st_up4(rb, base + kH2 * kD1 + o * kH2 + r0 + 4 * c4, f4v{src[0], src[1], src[2], src[3]}, local);
+        } else if (NL == 3 && own3 && x < kT4 + 68) {
+          const int c4 = x - kT4 - 64;
+          st_up4(rb, base + kH2 * kD1 + 16 * kH2 + r0 + 4 * c4,
+                 f4v{Bs[4 * c4], Bs[4 * c4 + 1], Bs[4 * c4 + 2], Bs[4 * c4 + 3]}, local);
+        } else {  // tile 0: b3 (3 layers) / b2 (2 layers)
+          const int c4 = x - (nitem - 4);
+          const float* src = Bs + (NL == 3 ? 16 : 0) + 4 * c4;
+          st_up4(rb, base + (NL == 3 ? kH2 * kD1 + 16 * kH2 + kH2 : 16 * kD1) + 4 * c4,
+                 f4v{src[0], src[1], src[2], src[3]}, local);
+        }
       }
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) st_gran(rb, kOffWfs + par * 16 + g, __uint_as_float(tag), tag);
     PK_STAMP(2, 4);
   }
@@ -2732,14 +2947,14 @@ void mlp_persist_k(PersistArgs a) {
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
     constexpr bool XM = MODE >= 2;
-    if (!pk_sr_active<NL>(b, MODE == 3 && a.helpers)) return;
+    if (!pk_sr_active<NL>(b, MODE == 3 ? a.helpers : 0)) return;
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
       else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
     } else if (y < kGN) {
       pk_layer1_gram<NL, MODE == 3 ? 2 : MODE == 2 ? 1 : 0>(a, lds, y + kGN * (x - 1), b);
     } else if constexpr (MODE == 3) {
-      pk_l1_helper(a, lds, y - kGN + kGN * (x - 1), b);
+      pk_l1_helper(a, lds, y % kGN + kGN * (x - 1), y / kGN, b);
     }
   }
 }
@@ -2758,6 +2973,7 @@ void mlp_persist_set_probe(int mode) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_probe), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
+void mlp_persist_set_pkx_helpers(int helpers) { g_pkx_helpers = helpers < 0 ? -1 : helpers; }
 void mlp_persist_set_stamp_window(int first_step) {
   const int v = first_step < 0 ? 0 : first_step + 1;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
@@ -2783,6 +2999,7 @@ template <int NL, int MODE>
 static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
   const size_t lds = (size_t)lds_floats<NL>() * sizeof(float);
   static bool attr = false;
+  static int slots = 0;  // co-resident workgroups (occupancy x CUs)
   if (!attr) {
     const void* f = reinterpret_cast<const void*>(mlp_persist_k<NL, MODE>);
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2796,10 +3013,13 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
       return e;
-    if (per_cu < 1 || per_cu * cus < pk_grid<NL>(MODE == 1)) return hipErrorCooperativeLaunchTooLarge;
+    if (per_cu < 1) return hipErrorCooperativeLaunchTooLarge;
+    slots = per_cu * cus;
     attr = true;
   }
-  hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(pk_grid<NL>(MODE == 1)), dim3(kThreads), lds, s, a);
+  const int grid = pk_grid<NL>(MODE == 1, MODE == 3 ? a.helpers : 0);
+  if (slots < grid) return hipErrorCooperativeLaunchTooLarge;
+  hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -2863,8 +3083,18 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
       a.dzr_off = 2 * a.xhalf;
       a.xsw = xsw;
       a.xsw_stride = xsw_stride;
-      // the dW1 sum over >= 4 replicas split with helper blocks on idle CUs
-      a.helpers = a.nrep >= 4 ? 1 : 0;
+      // the dW1 sum over the replicas split with helper blocks on idle CUs
+      // (pk_hlo): 3 from 4 replicas on, none below (HIPDSML_PKX_HELPERS overrides,
+      // testing / tuning: 0, 1 or 3)
+      if (g_pkx_helpers == -2) {
+        const char* e = getenv("HIPDSML_PKX_HELPERS");
+        g_pkx_helpers = e != nullptr && *e ? atoi(e) : -1;
+      }
+      int h = g_pkx_helpers >= 0 ? g_pkx_helpers : a.nrep >= 4 ? 3 : 0;
+      if (h >= 3 && a.nrep >= 4) h = 3;        // every part gets >= 1 replica
+      else if (h >= 1 && a.nrep >= 2) h = 1;
+      else h = 0;
+      a.helpers = h;
     }
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)

@@ -383,6 +383,7 @@ class MlpTrainer:
             log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
             self.sync_times = times
         self._set_mode(choice or self.sync_active)
+        self._plain = None  # the all-gathered fp32 shards: only the tables' builds read them
         if self.sync_active not in XALL_MODES and self.Xall is not None:
             # the replicated inputs (N x the shard) are only read by xact / pkx:
             # free them, the runner's references included
@@ -475,10 +476,9 @@ class MlpTrainer:
     def _gram_table(self) -> torch.Tensor:
         """Per-batch Gram blocks of the single-replica persistent step
         (engine/gram.py gram_table: float[nbatches][64][64], 16 KB a batch)."""
-        from .gram import gram_table
-
         nb, B, d0 = self.nbatches, self.batch, self.spec.dims[0]
-        return gram_table(self.X[: nb * B, :d0].reshape(nb, B, d0)).contiguous()
+        # one launch of kernels/gram.hip (fp64 MFMA); engine/gram.py is its oracle
+        return self.runner_module().gram_table(self.X, self.X, nb, B, d0)
 
     def _gather_plain(self) -> torch.Tensor:
         """Every rank's input rows (fp32 [world][rows][d0], rank order) on this
@@ -487,6 +487,8 @@ class MlpTrainer:
 
         from ..parallel.xchg import ExchangeUnavailable
 
+        if getattr(self, "_plain", None) is not None:  # gathered once per _init_exchanges
+            return self._plain
         ctx = self.ctx
         rows = self.nbatches * self.batch
         lo = ctx.all_reduce_scalars(float(rows), op="min")[0]
@@ -497,10 +499,12 @@ class MlpTrainer:
         if ctx.backend == "nccl":
             out = torch.empty((ctx.world_size,) + tuple(own.shape), dtype=own.dtype, device=self.device)
             dist.all_gather_into_tensor(out, own)
-            return out
-        parts = [torch.empty(own.shape, dtype=own.dtype) for _ in range(ctx.world_size)]
-        dist.all_gather(parts, own.cpu())
-        return torch.stack(parts).to(self.device)
+        else:
+            parts = [torch.empty(own.shape, dtype=own.dtype) for _ in range(ctx.world_size)]
+            dist.all_gather(parts, own.cpu())
+            out = torch.stack(parts).to(self.device)
+        self._plain = out
+        return out
 
     def _replicas_per_gpu(self) -> int:
         """How many ranks share this rank's GPU (1 on a node, one process per
@@ -517,11 +521,10 @@ class MlpTrainer:
         """Cross-replica Gram blocks of the data-parallel persistent step in Gram
         form (sync pkg / pkg2; engine/gram.py gram_table_dp:
         float[nbatches][world][64][64]).  Collective (all-gathers the shards)."""
-        from .gram import gram_table_dp
-
-        nb, B, d0, N = self.nbatches, self.batch, self.spec.dims[0], self.ctx.world_size
+        nb, B, d0 = self.nbatches, self.batch, self.spec.dims[0]
         t0 = time.perf_counter()
-        T = gram_table_dp(self._gather_plain().view(N, nb, B, d0), self.ctx.rank)
+        # every source's batches against this rank's, one launch (kernels/gram.hip)
+        T = self.runner_module().gram_table(self._gather_plain(), self.X, nb, B, d0)
         torch.cuda.synchronize(self.device)
         self.precompute_ms["gram_table_dp"] = round(1e3 * (time.perf_counter() - t0), 2)
         return T

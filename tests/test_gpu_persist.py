@@ -171,9 +171,10 @@ def test_persistent_uneven_load_is_bit_exact(spec):
     assert torch.equal(a.P, b.P)
 
 
-@pytest.mark.parametrize("algo,n", [(4, 2), (4, 4), (4, 8), (2, 4), (2, 8), (0, 4)],
+@pytest.mark.parametrize("algo,n,helpers", [(4, 2, -1), (4, 3, -1), (4, 4, -1), (4, 8, -1), (4, 8, 1), (4, 6, -1),
+                                            (4, 2, 1), (4, 4, 0), (2, 4, -1), (2, 8, -1), (0, 4, -1)],
                          ids=lambda v: str(v))
-def test_data_parallel_forms_mirrored_replicas(algo, n):
+def test_data_parallel_forms_mirrored_replicas(algo, n, helpers):
     """One GPU runs the n-replica persistent step (pk = 0, pkg = 2, pkx = 4)
     against n - 1 exact copies of itself: in the kernel's mirror test mode every
     push to peer d lands in this replica's OWN receive buffer, in d's source
@@ -182,7 +183,6 @@ def test_data_parallel_forms_mirrored_replicas(algo, n):
     match single-replica SGD.  This is the only way one GPU runs pkx at n >= 4,
     where the dW1 sum is split with the helper blocks (the Gram grid of more
     than 2 real replicas cannot share one GPU)."""
-    from hipdsml.engine.gram import gram_table_dp
     from hipdsml.ops.native import require_native
     from hipdsml.parallel.xchg import make_local_group, swizzle_inputs
 
@@ -195,11 +195,12 @@ def test_data_parallel_forms_mirrored_replicas(algo, n):
     nb = t.nbatches
     Xs = t.X[: nb * 64, :784].reshape(1, nb, 64, 784).expand(n, nb, 64, 784).contiguous()
     if algo >= 2:
-        t.runner.set_persist_gram(gram_table_dp(Xs, 0))
+        t.runner.set_persist_gram(C.gram_table(Xs.reshape(n, nb * 64, 784), t.X, nb, 64, 784))
     if algo == 4:
         xall = swizzle_inputs(Xs.reshape(n, nb * 64, 784), 64)
         t.runner.set_persist_xall(xall, xall[0].numel())
     C.mlp_persist_set_probe(2)
+    C.mlp_persist_set_pkx_helpers(helpers)  # pkx: the dW1 split over 0 / 1 / 3 helper blocks
     try:
         t.runner.set_persist(t.pk_buf, t.pk_err, 5000.0, xs[0], algo)
         for k in (5, 1, 9):  # launch splits: carried state, parity and slot reuse
@@ -207,6 +208,7 @@ def test_data_parallel_forms_mirrored_replicas(algo, n):
         t.synchronize()
     finally:
         C.mlp_persist_set_probe(0)
+        C.mlp_persist_set_pkx_helpers(-1)
     want, _ = _ref(ds, 15)
     err = (t.P.cpu() - want).abs().max().item()
     assert err < 2e-5, err

@@ -29,14 +29,15 @@ def pk_bytes_out(n: int, algo: int = 0) -> int:
     floats per lane (3 layers: wave 0 four float4, waves 1-3 two).  Gram forms
     (pkg / pkg2 / pkx): the 224 layer-1 slots (not in pkx), the 16 gradient
     tiles' slots (3 layers: 2 dW2 waves of 4 floats a lane each, the 4 W3
-    owners a dW3 wave and a bias wave: 40 slots of 1 KiB) and this replica's
+    owners a dW3 wave carrying the bias partials in its padding rows: 36
+    slots of 1 KiB of values) and this replica's
     dZ1 rows as 8-B granules (64 x 128 x 8 = 64 KiB) to every peer.  One-shot:
     every slot to every peer; two-shot: (n-1)/n of each slot to its owners,
     then the owners' (n-1)/n share to every peer."""
     if algo <= 1:
         slot_bytes = 224 * 64 * 8 * 4 + 4 * (64 * 16 * 4 + 3 * 64 * 8 * 4)
     else:
-        slot_bytes = (224 * 64 * 8 * 4 if algo < 4 else 0) + 40 * 1024
+        slot_bytes = (224 * 64 * 8 * 4 if algo < 4 else 0) + (36 if algo != 3 else 40) * 1024
     out = (n - 1) * slot_bytes if algo in (0, 2, 4) else 2 * (n - 1) * slot_bytes // n
     if algo >= 2:
         out += (n - 1) * 64 * 128 * 8
@@ -49,6 +50,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--launch", type=int, default=0, help="steps per launch (0: all in one)")
     ap.add_argument("--stamps", default="", help="also write the phase stamps of each N (JSON lines)")
+    ap.add_argument("--helpers", type=int, default=-1,
+                    help="pkx dW1 helper blocks per layer-1 block (-1: the default by N)")
     ap.add_argument("--algo", type=int, default=0,
                     help="0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx (exchange-free layer 1)")
     a = ap.parse_args()
@@ -62,6 +65,7 @@ def main() -> int:
     from hipdsml.parallel.xchg import make_local_group
 
     C = require_native()
+    C.mlp_persist_set_pkx_helpers(a.helpers)
     dev = torch.device("cuda", 0)
     for n in [int(x) for x in a.ranks.split(",")]:
         tr = MlpTrainer(MlpSpec((784, 128, 64, 10)), synthetic_mnist(64 * 100, seed=0),
@@ -75,12 +79,12 @@ def main() -> int:
                 x.fill_flags(1 << 62)
             tr.runner.set_world_size(n)
             if a.algo >= 2:
-                from hipdsml.engine.gram import gram_table_dp
                 from hipdsml.parallel.xchg import swizzle_inputs
 
                 nb = tr.nbatches
                 Xs = tr.X[: nb * 64, :784].reshape(1, nb, 64, 784).expand(n, nb, 64, 784)
-                tr.runner.set_persist_gram(gram_table_dp(Xs, 0))
+                tr.runner.set_persist_gram(C.gram_table(Xs.reshape(n, nb * 64, 784).contiguous(),
+                                                        tr.X, nb, 64, 784))
                 if a.algo == 4:
                     xall = swizzle_inputs(Xs.reshape(n, nb * 64, 784), 64)
                     tr.runner.set_persist_xall(xall, xall[0].numel())

@@ -59,6 +59,14 @@ def decode(v, spec) -> dict:
                 [(st[0][s][5] - st[1][s][4]) / 100.0 for s in range(8)])
             out["gram"]["cb_dz1_seen_to_z1_stored_us"] = med(
                 [(st[0][s][4] - st[0][s][5]) / 100.0 for s in range(8)])
+    if all(st[2][s][5] and st[2][s][6] and st[2][s][7] for s in range(8)):
+        # data-parallel Gram forms: the gradient tile's exchange, split (tile 0, wave 0)
+        out["grad_xchg"] = {
+            "stage_us": med([(st[2][s][5] - st[2][s][2]) / 100.0 for s in range(8)]),
+            "gather_us": med([(st[2][s][6] - st[2][s][5]) / 100.0 for s in range(8)]),
+            "gathered_to_all_waves_us": med([(st[2][s][7] - st[2][s][6]) / 100.0 for s in range(8)]),
+            "update_us": med([(st[2][s][3] - st[2][s][7]) / 100.0 for s in range(8)]),
+        }
     out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
     return out
 
