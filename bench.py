@@ -89,8 +89,8 @@ def allreduce_latency_us(ctx, comm, nbytes: int = 1 << 20, iters: int = 200,
         from hipdsml.parallel.ring_tune import tune_ring_chunk
 
         try:
-            res = tune_ring_chunk(ctx, comm, t)
-            ring_chunk, sweep = int(res["best"]), res["sweep_us"]
+            res = tune_ring_chunk(ctx, comm, t)  # both schedules, the faster kept
+            ring_chunk, sweep = int(res["best"]), {k: v for k, v in res.items() if k != "best"}
         except Exception as e:  # noqa: BLE001
             ring_chunk, sweep = 1 << 20, {"error": str(e)[:200]}
     out = {"bytes": nbytes, "ring_chunk_bytes": ring_chunk, "ring_chunk_sweep_us": sweep}

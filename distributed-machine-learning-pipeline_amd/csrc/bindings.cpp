@@ -990,13 +990,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         s.c->allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, cur_stream());
       }, py::arg("t"), py::arg("op") = 0)
       .def("ring_allreduce_", [](PyComm& s, torch::Tensor t, int op, int64_t chunk_bytes,
-                                 int max_rings) {
+                                 int max_rings, int pipe) {
         check_cuda(t, "t");
         TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "tensor must be 16 B aligned");
         s.c->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream(),
-                            max_rings);
+                            max_rings, pipe);
       }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20,
-         py::arg("max_rings") = 0)
+         py::arg("max_rings") = 0, py::arg("pipe") = -1,
+         "pipe: 1 pipelined schedule, 0 single-stream, -1 the communicator's default")
+      .def("set_ring_pipeline", [](PyComm& s, int mode) { s.c->set_ring_pipeline(mode); }, py::arg("mode"))
+      .def_property_readonly("ring_pipeline", [](PyComm& s) { return s.c->pipeline_mode(); })
       .def("reserve_ring", [](PyComm& s, int64_t count, int64_t chunk_bytes, int max_rings) {
         s.c->reserve_ring(count, kF32, chunk_bytes, max_rings);
       }, py::arg("count"), py::arg("chunk_bytes") = 1 << 20, py::arg("max_rings") = 0,

@@ -1350,9 +1350,13 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       const int off = (m * kD1 + n0 + 4 * qq) * 8;
       const float* rbase = a.xt.buf[a.rep];
       uint32_t need = 0;  // peers whose rows this thread still waits for
+      // gatherers: every replica (the correction); other pkx owners: only the
+      // replicas of their own dW1 part (the helpers read theirs) -- the exchange
+      // memory is uncached, and every redundant poll is HBM traffic
+      const int rhi = gat ? a.nrep : own_hi;
 #pragma unroll
       for (int r2 = 0; r2 < kMaxPeers; ++r2)
-        if (r2 < a.nrep && r2 != a.rep) need |= 1u << r2;
+        if (r2 < rhi && r2 != a.rep) need |= 1u << r2;
       bool pok = true;
       poll.start();
       while (need != 0u) {
@@ -1857,43 +1861,69 @@ __device__ __forceinline__ void pk_chain_rows_out(__amdgpu_buffer_rsrc_t rb, con
   }
 }
 
-// Data-parallel Gram form: a chain's dZ1 rows also go to every peer's DZR
-// region (this replica's slot, parity by step), as system-scope granules.
-// The lane's 8 values (rows row0 + r, r = 0..3, of columns col0 and col1), one
-// buffer descriptor per peer (built once, not once per value), every peer's
-// stores issued back to back.
-__device__ __forceinline__ void pk_push_dz1(const PersistArgs& a, uint64_t s, int row0, int col0, int col1,
-                                            const float (&v)[2][4], uint32_t tag) {
-  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  const int64_t base = pk_dzr_base(a, s, a.rep);
+// A chain's dZ1 rows as {value, step tag} granule PAIRS: lane (i, q) computes
+// rows 4 q .. +3 of columns 16 (w + 4 tt) + i; lanes i and i ^ 1 swap halves
+// (one DPP swap per value), so each lane owns two rows of an adjacent column
+// pair and publishes each row as ONE 16-B store -- 4 stores a lane instead of
+// 8 single granules, to the local DZ1 region (g0: its granule base) and, in the
+// data-parallel Gram forms (XM), to every peer's DZR slot (system scope).
+// Readers check both tags of a pair as before.
+template <bool XM>
+__device__ __forceinline__ void pk_publish_dz1(const PersistArgs& a, __amdgpu_buffer_rsrc_t rb, int64_t g0,
+                                               uint64_t s, int rb0, int q, int w, int i, const float (&dzv)[2][4],
+                                               uint32_t tag) {
+  const bool odd = (i & 1) != 0;
+  nu4v pr[2][2];
+  int off[2][2];  // granule index in the [64][128] image
 #pragma unroll
-  for (int d = 0; d < kMaxPeers; ++d) {
-    if (d >= a.nrep || d == a.rep) continue;
-    const __amdgpu_buffer_rsrc_t r = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, d) : a.xt.buf[d] + base);
+  for (int tt = 0; tt < 2; ++tt) {
+    // each lane sends what its partner keeps (odd -> rows 0, 1; even -> rows
+    // 2, 3) by one quad_perm [1, 0, 3, 2] DPP move apiece, no indexing by lane
+    const float s0 = odd ? dzv[tt][0] : dzv[tt][2], s1 = odd ? dzv[tt][1] : dzv[tt][3];
+    const float x0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xF, 0xF, false));
+    const float x1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xF, 0xF, false));
+    const int nb = 16 * (w + 4 * tt) + (i & ~1);
+    const float lo0 = odd ? x0 : dzv[tt][0], hi0 = odd ? dzv[tt][2] : x0;
+    const float lo1 = odd ? x1 : dzv[tt][1], hi1 = odd ? dzv[tt][3] : x1;
+    pr[tt][0] = nu4v{__float_as_uint(lo0), tag, __float_as_uint(hi0), tag};
+    pr[tt][1] = nu4v{__float_as_uint(lo1), tag, __float_as_uint(hi1), tag};
+    off[tt][0] = (rb0 + 4 * q + (odd ? 2 : 0)) * kD1 + nb;
+    off[tt][1] = (rb0 + 4 * q + (odd ? 3 : 1)) * kD1 + nb;
+  }
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+  for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const u2 wv = {__float_as_uint(v[tt][k]), tag};
-        __builtin_amdgcn_raw_buffer_store_b64(wv, r, ((row0 + k) * kD1 + (tt ? col1 : col0)) * 8, 0, kScSys);
-      }
+    for (int k = 0; k < 2; ++k)
+      __builtin_amdgcn_raw_buffer_store_b128(pr[tt][k], rb, (int)((g0 + off[tt][k]) * 8), 0, kSc1);
+  if constexpr (XM) {
+    const int64_t base = pk_dzr_base(a, s, a.rep);
+#pragma unroll
+    for (int d = 0; d < kMaxPeers; ++d) {
+      if (d >= a.nrep || d == a.rep) continue;
+      const __amdgpu_buffer_rsrc_t r = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, d) : a.xt.buf[d] + base);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) __builtin_amdgcn_raw_buffer_store_b128(pr[tt][k], r, off[tt][k] * 8, 0, kScSys);
+    }
   }
 }
 
 // Data-parallel Gram forms: the chain's last vector-memory ops of a step are its
-// 8 local dZ1 granules and 8 pushed to each peer; only the rows stored BEFORE
-// them must land before the rows flag.  vmcnt retires in issue order, so
-// waiting down to those 8 n outstanding ops drains the rows without waiting for
-// the peers' write acknowledgements (an xGMI round trip) on the tiles' path.
+// 4 local dZ1 pair stores and 4 pushed to each peer (pk_publish_dz1); only the
+// rows stored BEFORE them must land before the rows flag.  vmcnt retires in
+// issue order, so waiting down to those 4 n outstanding ops drains the rows
+// without waiting for the peers' write acknowledgements (an xGMI round trip)
+// on the tiles' path.
 __device__ __forceinline__ void pk_drain_rows(int nrep) {
   switch (nrep) {
-    case 2: __asm__ volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 3: __asm__ volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 4: __asm__ volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 5: __asm__ volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-    case 6: __asm__ volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-    case 7: __asm__ volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-    case 8: __asm__ volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    case 2: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: __asm__ volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 4: __asm__ volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 5: __asm__ volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 6: __asm__ volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 7: __asm__ volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 8: __asm__ volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
     default: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -2192,10 +2222,9 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? a0[tt][r] + a1[tt][r] : 0.f;
             dzv[tt][r] = v;
-            st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
           }
         }
-        if constexpr (XM) pk_push_dz1(a, s, rb0 + 4 * q, 16 * w + i, 16 * (w + 4) + i, dzv, tag);
+        pk_publish_dz1<XM>(a, rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)), s, rb0, q, w, i, dzv, tag);
       }
     } else {
       // ---- logits = H1 W2^T + b2: K = 128 split over the 4 waves ----
@@ -2266,10 +2295,9 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
             const int m = 4 * q + r;
             const float v = H1[m * kS1 + n] > 0.f ? acc[tt][r] : 0.f;
             dzv[tt][r] = v;
-            st_gran(rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)) + (int64_t)(rb0 + m) * kD1 + n, v, tag);
           }
         }
-        if constexpr (XM) pk_push_dz1(a, s, rb0 + 4 * q, 16 * w + i, 16 * (w + 4) + i, dzv, tag);
+        pk_publish_dz1<XM>(a, rb, kOffDz1 + (DP ? 0 : (int64_t)par * (kB * kD1)), s, rb0, q, w, i, dzv, tag);
       }
     }
     PK_STAMP(1, 4);

@@ -157,8 +157,16 @@ void RcclComm::allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, hi
         "ncclAllReduce");
 }
 
+int RcclComm::pipeline_mode() const {
+  static const bool kPipeEnv = [] {
+    const char* e = std::getenv("HIPDSML_RING_PIPELINE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return pipe_default_ >= 0 ? pipe_default_ : (kPipeEnv ? 1 : 0);
+}
+
 void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op,
-                              int64_t chunk_bytes, hipStream_t s, int max_rings) {
+                              int64_t chunk_bytes, hipStream_t s, int max_rings, int pipe_mode) {
   if (aborted_) throw std::runtime_error("ring_allreduce on aborted communicator");
   const int n = nranks_;
   if (n < 2 || count == 0) return;
@@ -188,17 +196,14 @@ void RcclComm::ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t o
   // the chunk it sends (and of the scratch slot it receives into), so chunk
   // c's reduce overlaps chunk c+1's transfer.  One round per step leaves
   // nothing to overlap: the single-stream order is kept (no event overhead).
-  // Opt-in (HIPDSML_RING_PIPELINE=1) until a multi-GPU run has validated RCCL
-  // p2p groups waiting on another stream's events: the schedule's dependencies
-  // are verified by simulation only (tests/test_ring_plan.py), and a hang here
-  // would stall every rank's init (the chunk sweep runs this ring).
-  static const bool kPipeEnv = [] {
-    const char* e = std::getenv("HIPDSML_RING_PIPELINE");
-    return e != nullptr && e[0] == '1';
-  }();
+  // Which schedule runs: the caller's choice, else the communicator's default
+  // -- set by parallel/ring_tune.py after it timed both (the pipelined one
+  // first validated on a throwaway communicator with a bounded wait, so a
+  // hang there can never take down this one), else HIPDSML_RING_PIPELINE.
+  const bool want = pipe_mode >= 0 ? pipe_mode == 1 : pipeline_mode() == 1;
   bool pipe = false;
   for (const auto& g : plan)
-    if (kPipeEnv && !g.empty() && g[0].round > 0) pipe = true;
+    if (want && !g.empty() && g[0].round > 0) pipe = true;
   const auto deps = pipe ? ring_pipeline(plan) : std::vector<RingDeps>(plan.size());
   if (pipe) {
     ensure_pipe(plan.size());

@@ -161,8 +161,15 @@ class RcclComm {
   // reduce-scatter + all-gather, every ring's ncclSend/ncclRecv of a step in
   // one ncclGroup, segment reductions by dsml::reduce_inplace, `chunk_bytes`
   // rounds.  max_rings = 0: all rings; 1: the classic single ring.
+  // pipe: 1 the pipelined schedule (ring_plan.h ring_pipeline), 0 the
+  // single-stream one, -1 this communicator's default (set_ring_pipeline;
+  // until set, HIPDSML_RING_PIPELINE=1 selects the pipelined one).
   void ring_allreduce(void* buf, int64_t count, int32_t dtype, int32_t op, int64_t chunk_bytes,
-                      hipStream_t s, int max_rings = 0);
+                      hipStream_t s, int max_rings = 0, int pipe = -1);
+  // The default schedule of ring_allreduce (parallel/ring_tune.py measures both
+  // and keeps the faster): -1 env, 0 single-stream, 1 pipelined.
+  void set_ring_pipeline(int mode) { pipe_default_ = mode; }
+  int pipeline_mode() const;
   // Size the ring's reduce scratch for `count` elements once, up front (the
   // largest bucket): no hipMalloc / hipFree between buckets, and none inside a
   // stream capture (ring_allreduce refuses to grow it while capturing).
@@ -186,6 +193,7 @@ class RcclComm {
   int rank_, nranks_, device_;
   bool blocking_;
   bool aborted_ = false;
+  int pipe_default_ = -1;
   void* tmp_ = nullptr;
   size_t tmp_bytes_ = 0;
   void* one_ = nullptr;  // scratch for barrier

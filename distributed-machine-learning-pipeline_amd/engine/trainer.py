@@ -230,7 +230,8 @@ class MlpTrainer:
 
                     res = tune_ring_chunk(self.ctx, self.comm, self.G)
                     self._ring_chunk = int(res["best"])
-                    self.ring_chunk_sweep_us = res["sweep_us"]
+                    # both schedules' sweeps, the choice, and any pipelined-probe error
+                    self.ring_chunk_sweep_us = {k: v for k, v in res.items() if k != "best"}
                 else:
                     self._ring_chunk = 1 << 20
             # the in-house ring's scratch, sized once (never inside a graph capture)

@@ -77,11 +77,64 @@ def sweep(run: Callable[[int], None], sync: Callable[[], None], chunks: Iterable
     return out
 
 
+def choose_schedule(plain_us: Dict[int, float], pipe_us: Optional[Dict[int, float]],
+                    tol: float = 0.02) -> tuple:
+    """(chunk, pipelined) of the fastest candidate over both schedules.  The
+    pipelined schedule must beat the best single-stream time by more than
+    `tol` to be chosen (it costs events and a second stream); within the
+    single-stream sweep pick_chunk's larger-chunk rule applies."""
+    best = pick_chunk(plain_us)
+    if pipe_us:
+        pc = min(pipe_us, key=pipe_us.get)
+        if pipe_us[pc] < plain_us[best] * (1.0 - tol):
+            return pc, True
+    return best, False
+
+
+def validate_pipelined(run: Callable[[], None], done: Callable[[], bool], agree: Callable[[bool], bool],
+                       abort: Callable[[], None], timeout_s: float = 10.0,
+                       clock: Callable[[], float] = time.monotonic,
+                       sleep: Callable[[float], None] = time.sleep) -> str:
+    """Run the pipelined ring ONCE with a bounded wait (collective): `run`
+    enqueues it, `done` polls its completion, `agree` ANDs a flag over the
+    ranks, `abort` kills the communicator it ran on (a throwaway one: a hang
+    never reaches the job's communicator).  Returns '' or the error, agreed
+    on every rank -- a timeout or an exception is reported, never a hang."""
+    err = ""
+    try:
+        run()
+        t_end = clock() + timeout_s
+        while not done():
+            if clock() > t_end:
+                err = f"pipelined ring did not complete within {timeout_s:g} s"
+                break
+            sleep(0.001)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"[:200]
+    ok = agree(not err)
+    if not ok:
+        try:
+            abort()
+        except Exception:  # noqa: BLE001 pragma: no cover
+            pass
+        return err or "pipelined ring failed on a peer"
+    return ""
+
+
 def tune_ring_chunk(ctx, comm, t, chunks: Iterable[int] = CHUNKS, iters: int = 20,
-                    max_rings: int = 0) -> Dict[str, object]:
+                    max_rings: int = 0, pipeline: bool = True,
+                    probe_timeout_s: float = 10.0) -> Dict[str, object]:
     """Collective: sweep the chunk of ``comm.ring_allreduce_`` on tensor `t`
-    (restored afterwards) over the distinct candidates; returns
-    ``{"best": bytes, "sweep_us": {bytes: us}}``."""
+    (restored afterwards) over the distinct candidates, for the single-stream
+    schedule and -- when some candidate has several chunk rounds per step --
+    the pipelined one (chunk c's reduce overlapping chunk c+1's transfer,
+    ring_plan.h ring_pipeline).  The pipelined schedule first runs once on a
+    throwaway communicator under a bounded wait, and must reproduce the
+    single-stream result bit for bit (the same additions in the same order);
+    a failure there is reported as ``ring_pipe_error``, never as a hang.  The
+    faster schedule becomes the communicator's default.  Returns
+    ``{"best": bytes, "pipelined": bool, "sweep_us": {bytes: us},
+    "sweep_pipelined_us": {bytes: us} | None[, "ring_pipe_error": str]}``."""
     import torch
 
     nbytes = t.numel() * t.element_size()
@@ -89,19 +142,68 @@ def tune_ring_chunk(ctx, comm, t, chunks: Iterable[int] = CHUNKS, iters: int = 2
     cands = distinct_chunks(nbytes, ctx.world_size, rings, chunks)
     saved = t.clone()
 
-    def run(c):
-        comm.ring_allreduce_(t, 0, c, max_rings)
-
     def sync():
         torch.cuda.synchronize(t.device)
 
-    times = sweep(run, sync, cands, iters=iters,
-                  reduce_max=lambda v: ctx.all_reduce_scalars(v, op="max")[0],
-                  reserve=lambda c: comm.reserve_ring(t.numel(), c, max_rings))
+    reduce_max = lambda v: ctx.all_reduce_scalars(v, op="max")[0]  # noqa: E731
+    reserve = lambda c: comm.reserve_ring(t.numel(), c, max_rings)  # noqa: E731
+    with ctx.guard("ring chunk sweep"):
+        times = sweep(lambda c: comm.ring_allreduce_(t, 0, c, max_rings, 0), sync, cands, iters=iters,
+                      reduce_max=reduce_max, reserve=reserve)
+    out: Dict[str, object] = {"sweep_us": {str(k): v for k, v in times.items()}, "sweep_pipelined_us": None}
+    multi = [c for c in cands if effective_rounds(nbytes, ctx.world_size, rings, c) > 1]
+    pipe_times = None
+    if pipeline and multi:
+        err = _probe_pipelined(ctx, t, saved, multi[0], max_rings, probe_timeout_s)
+        if err:
+            out["ring_pipe_error"] = err
+        else:
+            with ctx.guard("pipelined ring chunk sweep"):
+                pipe_times = sweep(lambda c: comm.ring_allreduce_(t, 0, c, max_rings, 1), sync, multi,
+                                   iters=iters, reduce_max=reduce_max, reserve=reserve)
+            out["sweep_pipelined_us"] = {str(k): v for k, v in pipe_times.items()}
     t.copy_(saved)
-    best = pick_chunk(times)
+    best, piped = choose_schedule(times, pipe_times)
+    comm.set_ring_pipeline(1 if piped else 0)
     comm.reserve_ring(t.numel(), best, max_rings)
-    return {"best": best, "sweep_us": {str(k): v for k, v in times.items()}}
+    out["best"] = best
+    out["pipelined"] = piped
+    return out
+
+
+def _probe_pipelined(ctx, t, src, chunk: int, max_rings: int, timeout_s: float) -> str:
+    """The pipelined ring once, on a throwaway RCCL communicator, bounded, and
+    checked bit-exact against the single-stream ring on the same input."""
+    import torch
+
+    from .dist import make_native_comm
+
+    try:
+        probe = make_native_comm(ctx)
+    except Exception as e:  # noqa: BLE001 -- collective init failed: no pipelined candidate
+        return f"probe communicator: {type(e).__name__}: {e}"[:200]
+    want = src.clone()
+    got = src.clone()
+    probe.reserve_ring(t.numel(), chunk, max_rings)
+    probe.ring_allreduce_(want, 0, chunk, max_rings, 0)
+    torch.cuda.synchronize(t.device)
+    ev = torch.cuda.Event()
+
+    def run():
+        probe.ring_allreduce_(got, 0, chunk, max_rings, 1)
+        ev.record()
+
+    err = validate_pipelined(run, ev.query, lambda ok: ctx.all_reduce_scalars(1.0 if ok else 0.0,
+                                                                             op="min")[0] > 0,
+                             probe.abort, timeout_s)
+    if err:
+        return err
+    torch.cuda.synchronize(t.device)
+    same = bool(torch.equal(want, got))
+    if ctx.all_reduce_scalars(1.0 if same else 0.0, op="min")[0] < 1:
+        return "pipelined ring result differs from the single-stream ring"
+    del probe
+    return ""
 
 
 def _directed_rings(n: int, max_rings: int):

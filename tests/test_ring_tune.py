@@ -72,3 +72,38 @@ def test_rounds_match_the_native_schedule():
         count = nbytes // 4
         plan = C.ring_schedule(8, 3, count, 4, chunk // 4, 0)
         assert len(plan) == 2 * 7 * rt.effective_rounds(nbytes, 8, 6, chunk)
+
+
+def test_choose_schedule_prefers_single_stream_unless_pipelined_clearly_wins():
+    plain = {65536: 100.0, 131072: 101.0, 262144: 150.0}
+    assert rt.choose_schedule(plain, None) == (131072, False)
+    assert rt.choose_schedule(plain, {65536: 99.5}) == (131072, False)   # within tolerance
+    assert rt.choose_schedule(plain, {65536: 80.0, 131072: 90.0}) == (65536, True)
+
+
+def test_validate_pipelined_reports_a_hang_as_an_error_and_aborts():
+    """VERDICT r4 Next #7: a pipelined candidate that never completes is
+    reported (ring_pipe_error), its throwaway communicator aborted -- the
+    tuner itself never hangs."""
+    clock = Clock()
+    aborted = []
+
+    def sleep(dt):
+        clock.t += dt
+
+    err = rt.validate_pipelined(lambda: None, lambda: False, lambda ok: ok, lambda: aborted.append(1),
+                                timeout_s=2.0, clock=clock, sleep=sleep)
+    assert "did not complete" in err and aborted == [1]
+
+
+def test_validate_pipelined_agrees_across_ranks():
+    # this rank finished, a peer did not: the failure is agreed and reported here too
+    aborted = []
+    err = rt.validate_pipelined(lambda: None, lambda: True, lambda ok: False, lambda: aborted.append(1))
+    assert err == "pipelined ring failed on a peer" and aborted == [1]
+    assert rt.validate_pipelined(lambda: None, lambda: True, lambda ok: ok, lambda: None) == ""
+
+    def boom():
+        raise RuntimeError("ncclGroupEnd: unhandled error")
+
+    assert "ncclGroupEnd" in rt.validate_pipelined(boom, lambda: True, lambda ok: ok, lambda: None)

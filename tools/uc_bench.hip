@@ -142,7 +142,6 @@ int main() {
                  mem ? "coarse" : "uncached", stride, blocks, loads, (unsigned long long)(v[v.size() / 2] * 10),
                  (unsigned long long)(v[v.size() * 9 / 10] * 10));
         }
-  return 0;
   for (int blocks : {1, 16})
     for (int stores : {0, 14, 28, 42})
       for (int loads : {2, 14}) {
