@@ -91,11 +91,34 @@ constexpr int cmax0(int a, int b) { return a > b ? a : b; }
 // (gn, gk) at blockIdx 8 (8 h + gn) + gk + 1, on its owner's XCD: with 3 the
 // layer-1 roles fill XCDs 1-7, 32 CUs each).
 constexpr int kMaxHelpers = 3;
-template <int NL> constexpr int pk_grid(bool dp, int helpers = 0) {
-  return dp ? kNBlk : 8 * cmax0(kNCH + GTile<NL>::kN, (1 + helpers) * kGN);
+// Data-parallel Gram forms with the tagged one-shot tile sums: kPushers(NL)
+// pusher blocks push the gradient tiles' slots to the peers (pk_pusher).  With
+// 3 helpers the grid has 256 blocks and spare rows on XCD 0: pusher p at
+// blockIdx 8 (4 + kN + p), beside its tiles.  Otherwise the grid keeps its
+// size: pusher p at row (1 + helpers) kGN + p / 7 of XCD p % 7 + 1, in the
+// layer-1 XCDs' spare CUs (the tiles then stage their slots write-through).
+template <int NL> constexpr int kPushers() { return GTile<NL>::kN / 2; }
+__host__ __device__ constexpr bool pk_push_xcd0(int helpers) { return helpers >= 3; }
+template <int NL> constexpr int pk_grid(bool dp, int helpers = 0, bool pushers = false) {
+  return dp ? kNBlk
+            : 8 * cmax0(kNCH + GTile<NL>::kN + (pushers && pk_push_xcd0(helpers) ? kPushers<NL>() : 0),
+                        (1 + helpers) * kGN + (pushers && !pk_push_xcd0(helpers) ? (kPushers<NL>() + 6) / 7 : 0));
+}
+// Pusher index of blockIdx b, or -1.
+template <int NL> __device__ __forceinline__ int pk_pusher_of(int b, int helpers, bool pushers) {
+  if (!pushers) return -1;
+  const int x = b & 7, y = b >> 3;
+  if (pk_push_xcd0(helpers)) {
+    const int y0 = kNCH + GTile<NL>::kN;
+    return x == 0 && y >= y0 && y < y0 + kPushers<NL>() ? y - y0 : -1;
+  }
+  const int y0 = (1 + helpers) * kGN;
+  const int p = (y - y0) * 7 + (x - 1);
+  return x != 0 && y >= y0 && p < kPushers<NL>() ? p : -1;
 }
 // Whether blockIdx b does work in the Gram-form grid (the rest exit).
-template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, int helpers = 0) {
+template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, int helpers = 0, bool pushers = false) {
+  if (pk_pusher_of<NL>(b, helpers, pushers) >= 0) return true;
   return (b & 7) == 0 ? (b >> 3) < kNCH + GTile<NL>::kN : (b >> 3) < (1 + helpers) * kGN;
 }
 // Replicas [pk_hlo(N, H, k), pk_hlo(N, H, k + 1)) of the global-batch dW1 go to
@@ -238,6 +261,15 @@ __device__ __forceinline__ int64_t pk_hx_off(uint64_t s, int h, int lb, int w, i
 __device__ __forceinline__ int64_t pk_hf(uint64_t s, int h, int lb) {
   return kOffHf + ((int64_t)(s & 1) * kMaxHelpers + (h - 1)) * 64 + lb;
 }
+// XS[2][16][3][64 lanes][4 granules]: data-parallel Gram forms (tagged sums),
+// every gradient tile's slot values staged for its pusher block as {value,
+// step tag} granules (no drain, no flag: the pusher polls the data itself).
+constexpr int64_t kOffXs = kTotalG;
+constexpr int64_t kTotalX = kOffXs + 2 * 16 * 3 * 64 * 4;
+__device__ __forceinline__ int64_t pk_xs_g(uint64_t s, int g, int k, int lane) {  // granules
+  return kOffXs + ((((int64_t)(s & 1) * 16 + g) * 3 + k) * 64 + lane) * 4;
+}
+
 static_assert(kCX % 4 == 0 && kWX % 4 == 0 && (kOffCx % 2) == 0 && (kOffWx % 2) == 0,
               "exchange rows travel as 16-B vectors");
 
@@ -273,6 +305,19 @@ __device__ __forceinline__ void st_up4(__amdgpu_buffer_rsrc_t r, int64_t float_o
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4v, v), r, (int)(float_off * 4), 0, 0);
   else
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu4v, v), r, (int)(float_off * 4), 0, kSc1);
+}
+// Stage one slot value as two 16-B granule pairs (plain stores when the
+// consumer shares the XCD: st_up4's rule).
+__device__ __forceinline__ void pk_xs_put(__amdgpu_buffer_rsrc_t rb, int64_t g, float4 v, uint32_t tag, bool local) {
+  const nu4v lo = {__float_as_uint(v.x), tag, __float_as_uint(v.y), tag};
+  const nu4v hi = {__float_as_uint(v.z), tag, __float_as_uint(v.w), tag};
+  if (local) {
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rb, (int)(g * 8), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rb, (int)(g * 8 + 16), 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rb, (int)(g * 8), 0, kSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rb, (int)(g * 8 + 16), 0, kSc1);
+  }
 }
 __device__ __forceinline__ f4v ld_f4(__amdgpu_buffer_rsrc_t r, int64_t float_off) {
   return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(float_off * 4), 0, kSc1));
@@ -444,6 +489,7 @@ struct PersistArgs {
                     // [pk_hlo(nrep, helpers, k), pk_hlo(.., k + 1))
   int32_t mirror;   // testing only (g_pk_probe_mode 2): pushes loop back into this replica's buffer
   int32_t probe;    // testing only (g_pk_probe_mode 1): peers' tagged data taken as arrived
+  int32_t pushers;  // Gram forms, tagged tile sums: the tiles' slots pushed by pusher blocks
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -736,61 +782,64 @@ __device__ __forceinline__ bool px_allreduce_tagged_wave(const PersistArgs& a, u
   return true;
 }
 
-// The same tagged one-shot sum split over two waves (the Gram forms' gradient
+// The same tagged one-shot sum split over waves (the Gram forms' gradient
 // tiles): vmcnt retires loads and stores in issue order, so a wave that polls
 // after pushing waits for every push's write acknowledgement -- a round trip
-// to the peers' (uncached) memory per poll, 6.4 us a step at 8 replicas in the
-// lone-replica probe (profiles/r5_pkx_stamps_base.jsonl).  One wave pushes
-// every slot of its block (px_tagged_push, never drained here); the slots'
-// own waves poll and sum (px_tagged_gather) with no store outstanding.
-__device__ __forceinline__ void px_tagged_push(const PersistArgs& a, uint64_t s, float4 v, int slot) {
-  const int lane = threadIdx.x & 63;
-  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
-  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
-  const uint32_t tag = (uint32_t)(s + 1);
-  const nu4v lo = {__float_as_uint(v.x), tag, __float_as_uint(v.y), tag};
-  const nu4v hi = {__float_as_uint(v.z), tag, __float_as_uint(v.w), tag};
-#pragma unroll
-  for (int d = 0; d < kMaxPeers; ++d) {
-    if (d >= a.nrep || d == a.rep) continue;
-    const __amdgpu_buffer_rsrc_t r =
-        rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot + (int64_t)d * per_src
-                      : a.xt.buf[d] + poff + (int64_t)slot * kPxSlot + (int64_t)a.rep * per_src);
-    __builtin_amdgcn_raw_buffer_store_b128(lo, r, (lane * 16) * 4, 0, kScSys);
-    __builtin_amdgcn_raw_buffer_store_b128(hi, r, (lane * 16 + 4) * 4, 0, kScSys);
-  }
-}
-// v (this replica's value) <- the rank-ordered sum of every replica's `slot`;
+// to the peers' (uncached) memory per poll.  Pusher waves push (px_tagged_push,
+// never drained here), other waves poll and sum (px_tagged_gather) with no
+// store outstanding.  A CU's vector-memory pipe issues a 1 KiB system-scope
+// store only every 30-120 ns (box-dependent), and a gathering wave's loads
+// queue behind the stores of its CU: the pushes run on separate pusher blocks
+// (pk_pusher), two waves per tile, each half the peers (profiles/r5_uc_bench*.jsonl,
+// r5_pkx_stamps_*.jsonl).
+// v[k] (this replica's value of slot slot0 + k, k < NS) <- the rank-ordered
+// sum of every replica's; every source's loads of a round in flight together.
 // false: a source did not arrive in time (error word raised).
-__device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t s, float4& v, int slot) {
+template <int NS>
+__device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t s, float4 (&v)[NS], int slot0,
+                                                 int dbg_row = -1) {
   const int lane = threadIdx.x & 63;
+  // profiling (tools/pk_stamps.py grad_gather): entry / loads issued / data in / exit
+  const bool dbg = dbg_row >= 0 && dbg_row < 6 && threadIdx.x == 0;
+  if (dbg) g_pk_stamps[3][2 + dbg_row][0] = __builtin_amdgcn_s_memrealtime();
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint32_t tag = (uint32_t)(s + 1);
-  const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot;
-  nu4v g[kMaxPeers][2];
+  const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot0 * kPxSlot;
+  nu4v g[kMaxPeers][NS][2];
   uint32_t need = 0;
 #pragma unroll
   for (int src = 0; src < kMaxPeers; ++src)
     if (src < a.nrep && src != a.rep) need |= 1u << src;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t spins = 0;
-  bool ok = true;
+  bool ok = true, first = true;
   while (need != 0u) {
 #pragma unroll
     for (int src = 0; src < kMaxPeers; ++src) {
       if (need & (1u << src)) {
         const __amdgpu_buffer_rsrc_t r = rsrc(mine + src * per_src);
-        g[src][0] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane * 16) * 4, 0, kScSys);
-        g[src][1] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane * 16 + 4) * 4, 0, kScSys);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          g[src][k][0] = __builtin_amdgcn_raw_buffer_load_b128(r, (k * kPxSlot + lane * 16) * 4, 0, kScSys);
+          g[src][k][1] = __builtin_amdgcn_raw_buffer_load_b128(r, (k * kPxSlot + lane * 16 + 4) * 4, 0, kScSys);
+        }
       }
     }
+    if (dbg && first) g_pk_stamps[3][2 + dbg_row][1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int src = 0; src < kMaxPeers; ++src) {
-      if ((need & (1u << src)) &&
-          ((g[src][0].y == tag && g[src][0].w == tag && g[src][1].y == tag && g[src][1].w == tag) || a.probe))
-        need &= ~(1u << src);
+      if (need & (1u << src)) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+          all = all && g[src][k][0].y == tag && g[src][k][0].w == tag && g[src][k][1].y == tag &&
+                g[src][k][1].w == tag;
+        if (all || a.probe) need &= ~(1u << src);
+      }
     }
+    if (dbg && first) g_pk_stamps[3][2 + dbg_row][2] = __builtin_amdgcn_s_memrealtime();
+    first = false;
     if (__builtin_amdgcn_ballot_w64(need != 0u) == 0) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
       __hip_atomic_fetch_or(a.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -806,18 +855,53 @@ __device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t 
   }
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   if (!ok) return false;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int src = 0; src < kMaxPeers; ++src) {
-    if (src < a.nrep) {
-      const float4 y = src == a.rep ? v
-                                    : make_float4(__uint_as_float(g[src][0].x), __uint_as_float(g[src][0].z),
-                                                  __uint_as_float(g[src][1].x), __uint_as_float(g[src][1].z));
-      acc.x += y.x; acc.y += y.y; acc.z += y.z; acc.w += y.w;
+  for (int k = 0; k < NS; ++k) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int src = 0; src < kMaxPeers; ++src) {
+      if (src < a.nrep) {
+        const float4 y = src == a.rep ? v[k]
+                                      : make_float4(__uint_as_float(g[src][k][0].x), __uint_as_float(g[src][k][0].z),
+                                                    __uint_as_float(g[src][k][1].x), __uint_as_float(g[src][k][1].z));
+        acc.x += y.x; acc.y += y.y; acc.z += y.z; acc.w += y.w;
+      }
+    }
+    v[k] = acc;
+  }
+  if (dbg) g_pk_stamps[3][2 + dbg_row][3] = __builtin_amdgcn_s_memrealtime();
+  return true;
+}
+// Pusher wave pw (0 or 1) of a pair: every second peer, all `ns` slots
+// (values in registers, v[k] = slot slot0 + k).
+__device__ __forceinline__ void px_tagged_push_half(const PersistArgs& a, uint64_t s, const float4 (&v)[3], int ns,
+                                                    int slot0, int pw) {
+  const int lane = threadIdx.x & 63;
+  const int64_t poff = (int64_t)(s & 1) * a.xhalf;
+  const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
+  const uint32_t tag = (uint32_t)(s + 1);
+  nu4v lo[3], hi[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = nu4v{__float_as_uint(v[k].x), tag, __float_as_uint(v[k].y), tag};
+    hi[k] = nu4v{__float_as_uint(v[k].z), tag, __float_as_uint(v[k].w), tag};
+  }
+  int j = 0;
+#pragma unroll
+  for (int d = 0; d < kMaxPeers; ++d) {
+    if (d >= a.nrep || d == a.rep) continue;
+    if ((j++ & 1) != pw) continue;
+    const __amdgpu_buffer_rsrc_t r =
+        rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot0 * kPxSlot + (int64_t)d * per_src
+                      : a.xt.buf[d] + poff + (int64_t)slot0 * kPxSlot + (int64_t)a.rep * per_src);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k < ns) {
+        __builtin_amdgcn_raw_buffer_store_b128(lo[k], r, (k * kPxSlot + lane * 16) * 4, 0, kScSys);
+        __builtin_amdgcn_raw_buffer_store_b128(hi[k], r, (k * kPxSlot + lane * 16 + 4) * 4, 0, kScSys);
+      }
     }
   }
-  v = acc;
-  return true;
 }
 
 template <int NV>
@@ -1323,7 +1407,8 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       Dz[m * 17 + 4 * qq + 2] = __uint_as_float(v1.x);
       Dz[m * 17 + 4 * qq + 3] = __uint_as_float(v1.z);
     }
-    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false, a.helpers) && pk_sr_active<NL>(tid, a.helpers) &&
+    if (lb == 0 && it + 1 == a.steps && tid < pk_grid<NL>(false, a.helpers, a.pushers) &&
+        pk_sr_active<NL>(tid, a.helpers, a.pushers) &&
         ok) {
       // hand the step counter on once every block has read it (SF tags)
       const uint32_t t0 = (uint32_t)(s0 + 1);
@@ -2692,6 +2777,10 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
   __syncthreads();
   bool ok = true;
   const bool local = pk_upper_local(a, s0, poll, ok, kNCH + GTile<NL>::kN);
+  // the staged slots stay in the L2 only when the pushers share the upper
+  // group's XCD (3 helpers: pushers on XCD 0), else they are written through
+  const int hl = XM && a.pushers && pk_push_xcd0(a.helpers) ? kPushers<NL>() : 0;
+  const bool xs_local = hl ? pk_upper_local(a, s0, poll, ok, kNCH + GTile<NL>::kN + hl) : false;
   const int stamp_on = g_pk_stamp_on && g == 0;
   const int jit = g_pk_jitter;
   for (int it = 0; it < a.steps && ok; ++it) {
@@ -2788,27 +2877,30 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
       if constexpr (XM) {  // data parallel: this wave's gradients summed over the replicas
         bool xok = true;
         if (a.algo == 0) {
-          // tagged one-shot, pushes on wave 3 (px_tagged_push): the bias
-          // partials ride in the dW3 slot's padding rows o = 12, 13 (q == 3),
-          // so a tile has 2 slots (3 with W3), and wave 3 -- which only
-          // pushes -- never polls behind its own stores
+          // tagged one-shot: the bias partials ride in the dW3 slot's padding
+          // rows o = 12, 13 (q == 3), so a tile has 2 slots (3 with W3).  The
+          // slots are staged for this tile's pusher block (XS + flag, raised by
+          // wave 3, which has no store of its own outstanding), and waves
+          // 0 .. nslot-1 gather with no push on this CU's memory pipe
           if (w == 3 && q == 0) { Bst[i] = sb; Bst[16 + i] = sb3; }
           lds_barrier();
           const int nslot = own3 ? 3 : 2;
           if (w == 2 && own3 && q == 3) { gw[0] = Bst[i]; gw[1] = Bst[16 + i]; }
           if (w < nslot) Stg[w * 64 + lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
           lds_barrier();
+          if (w == 3) {  // stage every slot as tagged granules (no drain: the gathering waves hold no store)
+            for (int k = 0; k < nslot; ++k) pk_xs_put(rb, pk_xs_g(s, g, k, lane), Stg[k * 64 + lane], tag, xs_local);
+          }
           PK_STAMP(2, 5);
-          if (w == 3) {
-            for (int sl = 0; sl < nslot; ++sl) px_tagged_push(a, s, Stg[sl * 64 + lane], kNL1 * 4 + 4 * g + sl);
-          } else if (w < nslot) {
-            float4 v = make_float4(gw[0], gw[1], gw[2], gw[3]);
-            xok = px_tagged_gather(a, s, v, kNL1 * 4 + 4 * g + w);
-            gw = f32x4{v.x, v.y, v.z, v.w};
+          const int dbg = stamp_on && it >= g_pk_stamp_on - 1 ? it - (g_pk_stamp_on - 1) : -1;
+          if (w < nslot) {
+            float4 v[1] = {make_float4(gw[0], gw[1], gw[2], gw[3])};
+            xok = px_tagged_gather<1>(a, s, v, kNL1 * 4 + 4 * g + w, w == 0 ? dbg : -1);
+            gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
             if (w == 2 && q == 3) { sb = gw[0]; sb3 = gw[1]; }
           }
           PK_STAMP(2, 6);
-          // agreed without a vector-memory drain (wave 3's pushes stay in flight)
+          // agreed without a vector-memory drain (wave 3's staging stores stay in flight)
           if (!xok) s_xfail = 1u;
           lds_barrier();
           PK_STAMP(2, 7);
@@ -2833,7 +2925,8 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
       if (w < 2) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) W2[(4 * q + r) * 33 + 16 * w + i] -= a.lr * gw[r];
-      } else if (w == 2 && own3) {
+      }
+      if (w == 2 && own3) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (4 * q + r < kNC) W3[(4 * q + r) * 17 + i] -= a.lr * gw[r];
@@ -2852,19 +2945,18 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
       if constexpr (XM) {
         bool xok = true;
         if (a.algo == 0) {
-          // tagged one-shot, pushes on wave 3: the b2 partial rides in the dW2
-          // slot's padding row o = 12 (q == 3)
+          // tagged one-shot: the b2 partial rides in the dW2 slot's padding
+          // row o = 12 (q == 3); the slot is staged for the pusher block
           if (w == 1 && q == 0) Bst[i] = sb;
           lds_barrier();
           if (w == 0 && q == 3) gw[0] = Bst[i];
           if (w == 0) Stg[lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
           lds_barrier();
-          if (w == 3) {
-            px_tagged_push(a, s, Stg[lane], kNL1 * 4 + 4 * g);
-          } else if (w == 0) {
-            float4 v = make_float4(gw[0], gw[1], gw[2], gw[3]);
-            xok = px_tagged_gather(a, s, v, kNL1 * 4 + 4 * g);
-            gw = f32x4{v.x, v.y, v.z, v.w};
+          if (w == 3) pk_xs_put(rb, pk_xs_g(s, g, 0, lane), Stg[lane], tag, xs_local);
+          if (w == 0) {
+            float4 v[1] = {make_float4(gw[0], gw[1], gw[2], gw[3])};
+            xok = px_tagged_gather<1>(a, s, v, kNL1 * 4 + 4 * g);
+            gw = f32x4{v[0].x, v[0].y, v[0].z, v[0].w};
             if (q == 3) sb = gw[0];
           }
           if (!xok) s_xfail = 1u;
@@ -2947,6 +3039,54 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
   pk_report(a, ok);
 }
 
+// Pusher block p (data-parallel Gram forms, tagged tile sums): pushes the
+// staged slots of gradient tiles p and p + kPushers to every peer -- waves
+// 0, 1 tile p, waves 2, 3 tile p + kPushers, each wave half the peers -- so the
+// tiles' gathers never queue behind their own pushes.  Same XCD as the tiles
+// (blockIdx 8 k): the staged slots stay in that L2.
+template <int NL>
+__device__ __forceinline__ void pk_pusher(const PersistArgs& a, int p, int blk) {
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
+  Poll poll{a.err, a.timeout_ticks, 0, 0};
+  const uint64_t s0 = ld_ctr64(a.ctr + 1);
+  pk_started(a, blk, s0);
+  const int g = p + (w >> 1) * kPushers<NL>();
+  const int nslot = NL == 3 ? ((g & 3) == 0 ? 3 : 2) : 1;
+  bool ok = true;
+  for (int it = 0; it < a.steps && ok; ++it) {
+    const uint64_t s = s0 + (uint64_t)it;
+    const uint32_t tag = (uint32_t)(s + 1);
+    const int par = (int)(s & 1);
+    // the tile's staged slots, polled by their tags (every load of a round in flight)
+    uint4 u[3][2];
+    poll.start();
+    for (;;) {
+      bool all = true;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (k < nslot) {
+          u[k][0] = ld_gran2(rb, pk_xs_g(s, g, k, lane));
+          u[k][1] = ld_gran2(rb, pk_xs_g(s, g, k, lane) + 2);
+          all = all && u[k][0].y == tag && u[k][0].w == tag && u[k][1].y == tag && u[k][1].w == tag;
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
+      if (!poll.again()) { ok = false; break; }
+    }
+    if (!ok) break;
+    (void)par;
+    float4 v[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      v[k] = k < nslot ? make_float4(__uint_as_float(u[k][0].x), __uint_as_float(u[k][0].z),
+                                     __uint_as_float(u[k][1].x), __uint_as_float(u[k][1].z))
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    px_tagged_push_half(a, s, v, nslot, kNL1 * 4 + 4 * g, w & 1);
+  }
+  pk_report(a, ok);
+}
+
 // DP: the data-parallel form (replica exchange compiled in); the single-replica
 // launch runs the exchange-free code.  Placement (speed only, every hand-off is
 // placement-independent): under round-robin dispatch blocks b and b + 8 share
@@ -2975,7 +3115,15 @@ void mlp_persist_k(PersistArgs a) {
     // round-robin dispatch), layer-1 block (gn, gk) at 8 gn + gk + 1; the
     // grid's other blocks exit at once
     constexpr bool XM = MODE >= 2;
-    if (!pk_sr_active<NL>(b, MODE == 3 ? a.helpers : 0)) return;
+    const int hl = MODE == 3 ? a.helpers : 0;
+    if (!pk_sr_active<NL>(b, hl, a.pushers != 0)) return;
+    if constexpr (XM) {
+      const int pu = pk_pusher_of<NL>(b, hl, a.pushers != 0);
+      if (pu >= 0) {
+        pk_pusher<NL>(a, pu, b);
+        return;
+      }
+    }
     if (x == 0) {
       if (y < kNCH) pk_chain<NL, false, XM>(a, lds, y, b);
       else pk_gtile<NL, XM>(a, lds, y - kNCH, b);
@@ -3021,7 +3169,7 @@ bool mlp_persist_supported(const MlpDesc& d) {
   return false;
 }
 
-int64_t mlp_persist_xbuf_granules() { return kTotalG; }
+int64_t mlp_persist_xbuf_granules() { return kTotalX; }
 
 template <int NL, int MODE>
 static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
@@ -3045,7 +3193,7 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     slots = per_cu * cus;
     attr = true;
   }
-  const int grid = pk_grid<NL>(MODE == 1, MODE == 3 ? a.helpers : 0);
+  const int grid = pk_grid<NL>(MODE == 1, MODE == 3 ? a.helpers : 0, a.pushers != 0);
   if (slots < grid) return hipErrorCooperativeLaunchTooLarge;
   hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
@@ -3124,6 +3272,8 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
       else h = 0;
       a.helpers = h;
     }
+    // the tagged one-shot tile sums (pkg, pkx) push from pusher blocks
+    a.pushers = (algo == 2 || algo == 4) ? 1 : 0;
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)
     if (algo < 2) a.carry = 0;

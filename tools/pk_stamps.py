@@ -67,6 +67,15 @@ def decode(v, spec) -> dict:
             "gathered_to_all_waves_us": med([(st[2][s][7] - st[2][s][6]) / 100.0 for s in range(8)]),
             "update_us": med([(st[2][s][3] - st[2][s][7]) / 100.0 for s in range(8)]),
         }
+    gd = [[v[(3 * 8 + 2 + r) * 8 + p] for p in range(4)] for r in range(6)]
+    if all(all(x) for x in gd):
+        # tile 0 wave 0's px_tagged_gather, steps 8..13: entry -> loads issued ->
+        # first round's data in -> sum done
+        out["grad_gather"] = {
+            "issue_us": med([(x[1] - x[0]) / 100.0 for x in gd]),
+            "data_us": med([(x[2] - x[1]) / 100.0 for x in gd]),
+            "rest_us": med([(x[3] - x[2]) / 100.0 for x in gd]),
+        }
     out["upper_group_xcd_local"] = bool(v[(3 * 8 + 1) * 8 + 0])
     return out
 
