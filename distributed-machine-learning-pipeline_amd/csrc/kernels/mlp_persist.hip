@@ -872,10 +872,10 @@ __device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t 
   if (dbg) g_pk_stamps[3][2 + dbg_row][3] = __builtin_amdgcn_s_memrealtime();
   return true;
 }
-// Pusher wave pw (0 or 1) of a pair: every second peer, all `ns` slots
-// (values in registers, v[k] = slot slot0 + k).
-__device__ __forceinline__ void px_tagged_push_half(const PersistArgs& a, uint64_t s, const float4 (&v)[3], int ns,
-                                                    int slot0, int pw) {
+// Pusher wave pw of npw: every npw-th peer, all `ns` slots (values in
+// registers, v[k] = slot slot0 + k).
+__device__ __forceinline__ void px_tagged_push_part(const PersistArgs& a, uint64_t s, const float4 (&v)[3], int ns,
+                                                    int slot0, int pw, int npw) {
   const int lane = threadIdx.x & 63;
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
@@ -890,7 +890,7 @@ __device__ __forceinline__ void px_tagged_push_half(const PersistArgs& a, uint64
 #pragma unroll
   for (int d = 0; d < kMaxPeers; ++d) {
     if (d >= a.nrep || d == a.rep) continue;
-    if ((j++ & 1) != pw) continue;
+    if ((j++ % npw) != pw) continue;
     const __amdgpu_buffer_rsrc_t r =
         rsrc(a.mirror ? a.xt.buf[a.rep] + poff + (int64_t)slot0 * kPxSlot + (int64_t)d * per_src
                       : a.xt.buf[d] + poff + (int64_t)slot0 * kPxSlot + (int64_t)a.rep * per_src);
@@ -2888,8 +2888,15 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
           if (w == 2 && own3 && q == 3) { gw[0] = Bst[i]; gw[1] = Bst[16 + i]; }
           if (w < nslot) Stg[w * 64 + lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
           lds_barrier();
-          if (w == 3) {  // stage every slot as tagged granules (no drain: the gathering waves hold no store)
-            for (int k = 0; k < nslot; ++k) pk_xs_put(rb, pk_xs_g(s, g, k, lane), Stg[k * 64 + lane], tag, xs_local);
+          if (w == 3) {
+            if (a.pushers) {  // stage every slot as tagged granules for the pusher block (no drain)
+              for (int k = 0; k < nslot; ++k) pk_xs_put(rb, pk_xs_g(s, g, k, lane), Stg[k * 64 + lane], tag, xs_local);
+            } else {  // few peers: wave 3 pushes every slot itself
+              float4 v3[3];
+#pragma unroll
+              for (int k = 0; k < 3; ++k) v3[k] = k < nslot ? Stg[k * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+              px_tagged_push_part(a, s, v3, nslot, kNL1 * 4 + 4 * g, 0, 1);
+            }
           }
           PK_STAMP(2, 5);
           const int dbg = stamp_on && it >= g_pk_stamp_on - 1 ? it - (g_pk_stamp_on - 1) : -1;
@@ -2952,7 +2959,14 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
           if (w == 0 && q == 3) gw[0] = Bst[i];
           if (w == 0) Stg[lane] = make_float4(gw[0], gw[1], gw[2], gw[3]);
           lds_barrier();
-          if (w == 3) pk_xs_put(rb, pk_xs_g(s, g, 0, lane), Stg[lane], tag, xs_local);
+          if (w == 3) {
+            if (a.pushers) {
+              pk_xs_put(rb, pk_xs_g(s, g, 0, lane), Stg[lane], tag, xs_local);
+            } else {
+              const float4 v3[3] = {Stg[lane], make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+              px_tagged_push_part(a, s, v3, 1, kNL1 * 4 + 4 * g, 0, 1);
+            }
+          }
           if (w == 0) {
             float4 v[1] = {make_float4(gw[0], gw[1], gw[2], gw[3])};
             xok = px_tagged_gather<1>(a, s, v, kNL1 * 4 + 4 * g);
@@ -3082,7 +3096,7 @@ __device__ __forceinline__ void pk_pusher(const PersistArgs& a, int p, int blk) 
       v[k] = k < nslot ? make_float4(__uint_as_float(u[k][0].x), __uint_as_float(u[k][0].z),
                                      __uint_as_float(u[k][1].x), __uint_as_float(u[k][1].z))
                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    px_tagged_push_half(a, s, v, nslot, kNL1 * 4 + 4 * g, w & 1);
+    px_tagged_push_part(a, s, v, nslot, kNL1 * 4 + 4 * g, w & 1, 2);
   }
   pk_report(a, ok);
 }
@@ -3272,8 +3286,11 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
       else h = 0;
       a.helpers = h;
     }
-    // the tagged one-shot tile sums (pkg, pkx) push from pusher blocks
-    a.pushers = (algo == 2 || algo == 4) ? 1 : 0;
+    // the tagged one-shot tile sums (pkg, pkx): from 4 replicas on the slots
+    // (2-3 per tile x N-1 peers) go out through pusher blocks, so a tile's
+    // gather never queues behind its own pushes; with fewer peers the tile's
+    // spare wave pushes them itself (a staging hop would cost more)
+    a.pushers = ((algo == 2 || algo == 4) && a.nrep >= 4) ? 1 : 0;
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)
     if (algo < 2) a.carry = 0;
