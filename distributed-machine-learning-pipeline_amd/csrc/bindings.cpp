@@ -494,6 +494,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
      py::arg("sgdW") = py::none(), py::arg("lr") = 0.0, py::arg("splits") = 1,
      py::arg("ws") = py::none(), py::arg("ctr") = py::none(), py::arg("bgrad") = py::none(),
      py::arg("bsgd") = py::none());
+  m.def("gemm_skinny_ws", [](int64_t M, int64_t N, int64_t K, int64_t splits) {
+    int64_t wsw = 0, ctw = 0;
+    gemm_skinny_ws((int)M, (int)N, (int)K, (int)splits, &wsw, &ctw);
+    return py::make_tuple(wsw, ctw);
+  }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0,
+     "split-K workspace of a skinny GEMM: (fp32 words of ws, int32 words of ctr), both zeroed once");
   m.def("gemm_skinny", [bf16p](torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, int64_t K, bool nn,
                               double alpha, c10::optional<torch::Tensor> bias, bool relu,
                               c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
@@ -521,10 +527,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (S > 1) {
       TORCH_CHECK(ws && ctr, "split-K skinny GEMM needs ws (slabs) and ctr (tile counters)");
       check_f32(*ws, "ws");
-      const int64_t tiles = ((N + 63) / 64) * ((M + 63) / 64);
-      TORCH_CHECK(ws->numel() >= (int64_t)S * tiles * 4096, "ws too small: need ", (int64_t)S * tiles * 4096);
+      int64_t wsw = 0, ctw = 0;
+      gemm_skinny_ws((int)M, (int)N, (int)K, (int)splits, &wsw, &ctw);
+      TORCH_CHECK(ws->numel() >= wsw, "ws too small: need ", wsw);
       check_cuda(*ctr, "ctr");
-      TORCH_CHECK(ctr->scalar_type() == torch::kInt32 && ctr->numel() >= tiles, "ctr: int32, one per 64x64 tile");
+      TORCH_CHECK(ctr->scalar_type() == torch::kInt32 && ctr->numel() >= ctw,
+                  "ctr: int32, one per 64x64 tile: need ", ctw);
       cp = ws->data_ptr<float>();
       tc = ctr->data_ptr<int32_t>();
     }

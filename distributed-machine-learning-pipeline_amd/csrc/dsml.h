@@ -283,6 +283,9 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
 // and applying `epi` (no sgdW / bgrad / bsgd).  slabs: S * tiles * 4096 fp32,
 // tile_ctr: one zeroed int per 64 x 64 tile (left zero).  K, N multiples of 8.
 int gemm_skinny_splits(int M, int N, int K, int splits);
+// split-K workspace of one launch: fp32 words of `slabs`, int32 words of `tile_ctr`
+// (zeroed once; every launch leaves its tickets at 0)
+void gemm_skinny_ws(int M, int N, int K, int splits, int64_t* ws_words, int64_t* ctr_words);
 hipError_t gemm_skinny_read_stamps(uint64_t* host_out);  // [1024][5], profiling only
 void gemm_skinny_set_stamping(bool on);
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N,

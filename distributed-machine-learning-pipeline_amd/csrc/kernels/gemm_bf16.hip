@@ -781,17 +781,29 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 // Fused classifier head: logits[m][c] = H[m] . W[c] + b[c] for C <= 16
 // classes, then softmax-CE as softmax_xent_k — one 256-thread block per row.
 // Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
+// Both products run on packed-bf16 dot instructions (v_dot2c_f32_bf16: two
+// bf16 MACs per lane per issue, straight from the loaded bf16 pairs, no
+// unpacking): the logits pair k-neighbours, the activation gradient pairs
+// class neighbours (one v_perm per output pair).  The per-class block sum is a
+// DPP row sum per class + 16 row partials through LDS (no bank conflicts: the
+// r4 LDS transpose read 16 consecutive floats per lane, 71% conflicted).
 __device__ uint64_t g_head_stamps[64][6];
-__device__ int g_head_stamp_on;
-__device__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bit 1 the dzp phase
+__constant__ int g_head_stamp_on;  // __constant__: scalar loads, no vector wait ahead of the batch
+__constant__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bit 1 the dzp phase
 #define HEAD_STAMP(k)                                                               \
   do {                                                                              \
     if (g_head_stamp_on && t == 0 && m < 64) g_head_stamps[m][(k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 constexpr int kHeadMaxC = 16;  // classes the head supports (instantiated for <= 10 and <= 16)
 constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
-// MAXC: the class count rounded up to an instantiated size -- register arrays
-// sized for 16 classes spilled into AGPRs at the BASELINE's 10
+typedef __bf16 hbf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float hdot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(hbf2, a), __builtin_bit_cast(hbf2, b), c, false);
+}
+__device__ __forceinline__ float hdot8(const uint4& a, const uint4& b, float c) {
+  return hdot2(a.w, b.w, hdot2(a.z, b.z, hdot2(a.y, b.y, hdot2(a.x, b.x, c))));
+}
+// MAXC: the class count rounded up to an instantiated size (even: class pairs)
 template <int MAXC>
 __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
@@ -800,62 +812,53 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats,
     uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt,
     int row_stats) {
-  __shared__ float part[MAXC][257];  // per-thread partial dot products, per class
-  __shared__ float zsum[MAXC];
-  __shared__ float gz[MAXC];         // bf16-rounded dLogits of this row
+  static_assert(MAXC % 2 == 0 && MAXC <= 16, "class pairs, one 16-lane row");
+  __shared__ float part[MAXC][17];     // [class][wave * 4 + 16-lane row] partial sums (+1: pad)
+  __shared__ uint32_t gz2[MAXC / 2];   // bf16-rounded dLogits of this row, class pairs
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* hr = H + (int64_t)m * ldh;
   // the softmax's own operands go out with the first loads (not after the reduction)
   HEAD_STAMP(0);
   const int y = labels[m];
-  const float bc = (bias && lane < C) ? bias[lane] : 0.f;
+  const float bc = bias ? bias[min(lane, C - 1)] : 0.f;  // lanes >= C: unused
   // this row's own loss / correct / count accumulators (row_stats: only this
   // workgroup touches them): read now, under the operand loads, and written
   // back with one plain store after the softmax -- a read-modify-write with
   // no round trip of its own (device atomics there kept the kernel's tail
   // waiting 1.8 us for their completion: head_bench dbg1)
-  const bool rst = row_stats && stats && w == 0 && !(g_head_dbg & 1);
+  const bool rst = row_stats && stats && w == 0;
   float4 racc = rst ? *reinterpret_cast<const float4*>(stats + 4 * (int64_t)m) : make_float4(0.f, 0.f, 0.f, 0.f);
-  // every load of the thread in one batch: its H chunks and the same chunks of all C rows of W
+  // every load of the thread in one batch, unpredicated (clamped addresses,
+  // out-of-range chunks zeroed after): its H chunks and the same chunks of all
+  // C rows of W.  A predicated load is a branch around it, and the compiler
+  // waited for each branch's load before the next (three serialised L2 round
+  // trips in the r4 head's ISA).  Rows past C load row C - 1: their logits are
+  // never read and their dLogits are 0.
   uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][MAXC];
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
-    const int k = (t + 256 * j) * 8;
-    const bool kv = k < K;
-    hv[j] = kv ? *reinterpret_cast<const uint4*>(hr + k) : make_uint4(0u, 0u, 0u, 0u);
+    const int k = min((t + 256 * j) * 8, K - 8);
+    hv[j] = *reinterpret_cast<const uint4*>(hr + k);
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      wv[j][c] = (kv && c < C) ? *reinterpret_cast<const uint4*>(W + (int64_t)c * ldw + k)
-                               : make_uint4(0u, 0u, 0u, 0u);
+      wv[j][c] = *reinterpret_cast<const uint4*>(W + (int64_t)min(c, C - 1) * ldw + k);
   }
+#pragma unroll
+  for (int j = 0; j < kHeadMaxK8; ++j)
+    if ((t + 256 * j) * 8 >= K) hv[j] = make_uint4(0u, 0u, 0u, 0u);  // zero H: zero products
   float acc[MAXC];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
+  for (int c = 0; c < MAXC; ++c) {
+    acc[c] = 0.f;
 #pragma unroll
-  for (int j = 0; j < kHeadMaxK8; ++j) {
-    const float h[8] = {bf16lo(hv[j].x), bf16hi(hv[j].x), bf16lo(hv[j].y), bf16hi(hv[j].y),
-                        bf16lo(hv[j].z), bf16hi(hv[j].z), bf16lo(hv[j].w), bf16hi(hv[j].w)};
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      const uint4 x = wv[j][c];
-      acc[c] += h[0] * bf16lo(x.x) + h[1] * bf16hi(x.x) + h[2] * bf16lo(x.y) + h[3] * bf16hi(x.y) +
-                h[4] * bf16lo(x.z) + h[5] * bf16hi(x.z) + h[6] * bf16lo(x.w) + h[7] * bf16hi(x.w);
-    }
+    for (int j = 0; j < kHeadMaxK8; ++j) acc[c] = hdot8(hv[j], wv[j][c], acc[c]);
   }
   HEAD_STAMP(1);
-  // block reduction per class: LDS transpose, then one 16-lane DPP row per class
+  // block reduction per class: DPP sum over each 16-lane row, 16 row partials via LDS
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) part[c][t] = acc[c];
-  lds_barrier();  // LDS only: no wait for this block's global stores
-  {
-    const int c = t >> 4, sg = t & 15;  // class c = row of 16 lanes; 16 partials per lane
-    if (c < MAXC) {  // whole 16-lane rows: the DPP row sum stays within active lanes
-      float v = 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v += part[c][16 * sg + u];
-      v = row16_sum(v);
-      if (sg == 0) zsum[c] = v;
-    }
+  for (int c = 0; c < MAXC; ++c) {
+    const float v = row16_sum(acc[c]);
+    if ((lane & 15) == 0) part[c][4 * w + (lane >> 4)] = v;
   }
   lds_barrier();  // LDS only: no wait for this block's global stores
   HEAD_STAMP(2);
@@ -863,7 +866,12 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
     const int c = lane;
     const bool cv = c < C;
     float z = -3.402823466e38f;
-    if (cv) z = zsum[c] + bc;
+    if (cv) {
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += part[c][r];
+      z = v + bc;
+    }
     if (cv && logits) logits[(int64_t)m * ldl + c] = z;
     // every class sits in lanes 0-15 (C <= 16): 16-lane DPP reductions
     // instead of 64-lane shuffles (each an LDS-path ds_bpermute round trip)
@@ -879,7 +887,9 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
       dz[(int64_t)m * ldz + c] = hq;
       if (dzT) dzT[(int64_t)c * ldt + m] = hq;
     }
-    if (c < MAXC) gz[c] = bf16_to_f32(hq);
+    // class pairs for the packed dZ pass: lane 2i packs (its, lane 2i+1's)
+    const uint32_t hi = (uint32_t)__shfl_xor((int)hq, 1);
+    if (c < MAXC && !(c & 1)) gz2[c >> 1] = (uint32_t)hq | (hi << 16);
     if (c == y && stats && !(g_head_dbg & 1)) {
       if (row_stats) {
         racc.x += -logf(p + 1e-10f);
@@ -899,27 +909,34 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(
   // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
   // chunks this thread already holds; bf16 row store + transposed copy.
   lds_barrier();  // LDS only: no wait for this block's global stores
-  float g[MAXC];
+  uint32_t g2[MAXC / 2];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) g[c] = c < C ? gz[c] : 0.f;
+  for (int i = 0; i < MAXC / 2; ++i) g2[i] = gz2[i];
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
     const int k = (t + 256 * j) * 8;
     if (k >= K) continue;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      const uint4 x = wv[j][c];
-      a[0] += g[c] * bf16lo(x.x); a[1] += g[c] * bf16hi(x.x);
-      a[2] += g[c] * bf16lo(x.y); a[3] += g[c] * bf16hi(x.y);
-      a[4] += g[c] * bf16lo(x.z); a[5] += g[c] * bf16hi(x.z);
-      a[6] += g[c] * bf16lo(x.w); a[7] += g[c] * bf16hi(x.w);
+    for (int i = 0; i < MAXC / 2; ++i) {
+      if (2 * i >= C) break;  // zero pairs past the classes (W rows not loaded)
+      const uint32_t x0[4] = {wv[j][2 * i].x, wv[j][2 * i].y, wv[j][2 * i].z, wv[j][2 * i].w};
+      const uint32_t x1[4] = {wv[j][2 * i + 1].x, wv[j][2 * i + 1].y, wv[j][2 * i + 1].z,
+                              wv[j][2 * i + 1].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        // (W[2i][k'], W[2i+1][k']) for the even and the odd k' of this dword
+        a[2 * d] = hdot2(__builtin_amdgcn_perm(x1[d], x0[d], 0x05040100u), g2[i], a[2 * d]);
+        a[2 * d + 1] = hdot2(__builtin_amdgcn_perm(x1[d], x0[d], 0x07060302u), g2[i], a[2 * d + 1]);
+      }
     }
-    const float h[8] = {bf16lo(hv[j].x), bf16hi(hv[j].x), bf16lo(hv[j].y), bf16hi(hv[j].y),
-                        bf16lo(hv[j].z), bf16hi(hv[j].z), bf16lo(hv[j].w), bf16hi(hv[j].w)};
+    const uint32_t hw[4] = {hv[j].x, hv[j].y, hv[j].z, hv[j].w};
     uint16_t q[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = f32_to_bf16(h[e] > 0.f ? a[e] : 0.f);
+    for (int e = 0; e < 8; ++e) {
+      const int16_t hb = (int16_t)(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xffffu);
+      q[e] = hb > 0 ? f32_to_bf16(a[e]) : (uint16_t)0;  // bf16 bits > 0 <=> value > 0
+    }
     *reinterpret_cast<uint4*>(dzp + (int64_t)m * ldzp + k) =
         make_uint4(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16),
                    q[4] | ((uint32_t)q[5] << 16), q[6] | ((uint32_t)q[7] << 16));

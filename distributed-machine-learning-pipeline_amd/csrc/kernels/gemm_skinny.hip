@@ -205,16 +205,19 @@ __global__ __launch_bounds__(kSkThreads, 1) void gemm_skinny_k(SkArgs a) {
   const int rl = tid >> 4, cl = 4 * (tid & 15);  // epilogue map: rows rl + 16j, columns cl..cl+3
   const int n = n0 + cl;
   const bool nv = n < a.N;  // N % 8 == 0: a 4-column group is whole or absent
-  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e.bias && nv) bias = *reinterpret_cast<const float4*>(e.bias + n);
-  uint2 mk[4] = {make_uint2(~0u, ~0u), make_uint2(~0u, ~0u), make_uint2(~0u, ~0u), make_uint2(~0u, ~0u)};
-  if (e.mask && nv) {
+  // Unpredicated: absent operands read A's first bytes instead and are dropped
+  // at their use, columns past N read column 0 and are never stored.  A load
+  // under a condition (even a uniform one) compiled to a branch whose copy out
+  // waited vmcnt(0): one memory round trip before the first DMA (rounds 2-4,
+  // ~0.5 us a launch).
+  const int nc = nv ? n : 0;
+  const float* bp = e.bias ? e.bias + nc : reinterpret_cast<const float*>(a.A);
+  float4 bias = *reinterpret_cast<const float4*>(bp);
+  const uint16_t* mp = e.mask ? e.mask + nc : a.A;
+  const int64_t ldm = e.mask ? e.ldm : 0;
+  uint2 mk[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = min(m0 + rl + 16 * j, a.M - 1);
-      mk[j] = *reinterpret_cast<const uint2*>(e.mask + (int64_t)m * e.ldm + n);
-    }
-  }
+  for (int j = 0; j < 4; ++j) mk[j] = *reinterpret_cast<const uint2*>(mp + (int64_t)min(m0 + rl + 16 * j, a.M - 1) * ldm);
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -302,6 +305,7 @@ __global__ __launch_bounds__(kSkThreads, 1) void gemm_skinny_k(SkArgs a) {
   }
 
   SK_STAMP(3);
+  if (!e.bias) bias = make_float4(0.f, 0.f, 0.f, 0.f);
   // ---- epilogue ----
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -367,6 +371,13 @@ void gemm_skinny_set_stamping(bool on) {
   const int v = on ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
+}
+
+void gemm_skinny_ws(int M, int N, int K, int splits, int64_t* ws_words, int64_t* ctr_words) {
+  const int S = gemm_skinny_splits(M, N, K, splits);
+  const int64_t tiles = ((N + 63) / 64) * ((M + 63) / 64);
+  *ws_words = S > 1 ? (int64_t)S * tiles * 4096 : 0;  // every slice's fp32 partial tile
+  *ctr_words = S > 1 ? tiles : 0;                     // an arrival ticket per tile
 }
 
 int gemm_skinny_splits(int M, int N, int K, int splits) {

@@ -54,10 +54,6 @@ def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
-def _tiles(M: int, N: int) -> int:
-    return math.ceil(M / 64) * math.ceil(N / 64)
-
-
 class WideMlpTrainer:
     def __init__(self, spec: MlpSpec, data: Dataset, batch: int = 64, lr: float = 0.01, *,
                  ctx: Optional[DistContext] = None, seed: int = 0, init: str = "kaiming",
@@ -127,11 +123,11 @@ class WideMlpTrainer:
                 self._plan(f"f{l}", batch, d[l + 1], d[l], False)
             if l > 0 and not (self.fused_head and l == L - 1):
                 self._plan(f"b{l}", batch, d[l], self.pd[l + 1], True)
-        ws = max([S * _tiles(M, N) * 4096 for (M, N, _, _, S) in self.plans.values()] + [16])
-        self.Cp = torch.zeros(ws, dtype=torch.float32, device=dev)
-        # split-K arrival tickets (one per 64x64 tile; every GEMM leaves them 0)
-        self.tctr = torch.zeros(max([_tiles(M, N) for (M, N, _, _, _) in self.plans.values()] + [1]),
-                                dtype=torch.int32, device=dev)
+        # split-K workspace shared by every skinny GEMM of the step: the slices'
+        # partial tiles and an arrival ticket per tile (kernels/gemm_skinny.hip)
+        sizes = [self.C.gemm_skinny_ws(M, N, K, 0) for (M, N, K, _, _) in self.plans.values()]
+        self.Cp = torch.zeros(max([w for w, _ in sizes] + [16]), dtype=torch.float32, device=dev)
+        self.tctr = torch.zeros(max([c for _, c in sizes] + [1]), dtype=torch.int32, device=dev)
         self.steps_done = 0
         # One hipGraph per epoch (every batch offset baked in): replaying it
         # removes the host launches per step.  With several replicas the

@@ -1,7 +1,8 @@
 """Skinny bf16 GEMMs (kernels/gemm_skinny.hip) against the fp32 torch product of
 the same bf16 operands: NT (forward, B = W [N x K]) and NN (dgrad, B = W
 [K x N] read through transposing LDS reads), split-K with the last-arriver
-reduction, every fused epilogue output, K / N / M tails."""
+reduction, every fused epilogue output, K / N / M tails, one workspace
+shared by launches of different shapes."""
 import pytest
 import torch
 
@@ -15,10 +16,10 @@ def _ref(A, B, nn):
     return A.float() @ (B.float() if nn else B.float().t())
 
 
-def _ws(M, N, S):
-    tiles = ((N + 63) // 64) * ((M + 63) // 64)
-    return (torch.zeros(max(S, 1) * tiles * 4096, device=DEV),
-            torch.zeros(tiles, dtype=torch.int32, device=DEV))
+def _ws(M, N, K, splits=0):
+    C = require_native()
+    wsw, ctw = C.gemm_skinny_ws(M, N, K, splits)
+    return (torch.zeros(max(wsw, 1), device=DEV), torch.zeros(max(ctw, 1), dtype=torch.int32, device=DEV))
 
 
 @pytest.mark.parametrize("nn", [False, True])
@@ -31,15 +32,16 @@ def test_skinny_matches_fp32(nn, M, N, K, splits):
     A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
     B = (torch.randn(K, N, generator=g) if nn else torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
     S = C.gemm_skinny_splits(M, N, K, splits)
-    ws, ctr = _ws(M, N, S)
-    out = torch.full((M, N), float("nan"), device=DEV)
-    got = C.gemm_skinny(A, B, M, N, K, nn=nn, of32=out, splits=splits, ws=ws, ctr=ctr)
-    assert got == S
-    torch.cuda.synchronize()
+    ws, ctr = _ws(M, N, K, splits)
     want = _ref(A, B, nn)
-    err = (out - want).abs().max().item()
-    assert err <= 2e-5 * K ** 0.5 * want.abs().max().item() + 1e-4, err
-    assert int(ctr.abs().sum().item()) == 0  # counters re-armed
+    for _ in range(3):  # back-to-back launches on one workspace
+        out = torch.full((M, N), float("nan"), device=DEV)
+        got = C.gemm_skinny(A, B, M, N, K, nn=nn, of32=out, splits=splits, ws=ws, ctr=ctr)
+        assert got == S
+        torch.cuda.synchronize()
+        err = (out - want).abs().max().item()
+        assert err <= 2e-5 * K ** 0.5 * want.abs().max().item() + 1e-4, err
+    assert int(ctr.abs().sum().item()) == 0  # tickets re-armed
 
 
 @pytest.mark.parametrize("nn", [False, True])
@@ -51,8 +53,7 @@ def test_skinny_epilogue_bias_relu_mask_and_copies(nn):
     B = (torch.randn(K, N, generator=g) if nn else torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
     bias = torch.randn(N, generator=g).to(DEV)
     mask = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
-    S = C.gemm_skinny_splits(M, N, K, 0)
-    ws, ctr = _ws(M, N, S)
+    ws, ctr = _ws(M, N, K)
     o32 = torch.empty(M, N, device=DEV)
     obf = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     obfT = torch.empty(N, M, dtype=torch.bfloat16, device=DEV)
@@ -72,7 +73,7 @@ def test_skinny_repeated_calls_are_bit_identical():
     M, N, K = 64, 4096, 4096
     A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
-    ws, ctr = _ws(M, N, C.gemm_skinny_splits(M, N, K, 0))
+    ws, ctr = _ws(M, N, K)
     outs = []
     for _ in range(5):
         o = torch.empty(M, N, device=DEV)
@@ -80,6 +81,32 @@ def test_skinny_repeated_calls_are_bit_identical():
         outs.append(o)
     torch.cuda.synchronize()
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+def test_skinny_shared_workspace_across_shapes():
+    """One ws / ctr pair serving launches of different tile counts and split
+    counts, interleaved (as the wide engine shares them)."""
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    shapes = [(64, 4096, 4096, 0, False), (64, 512, 4096, 3, True), (64, 1024, 2048, 0, False),
+              (64, 4096, 784, 0, True), (64, 512, 4096, 7, False)]
+    wsw = max(C.gemm_skinny_ws(M, N, K, sp)[0] for (M, N, K, sp, _) in shapes)
+    ctw = max(C.gemm_skinny_ws(M, N, K, sp)[1] for (M, N, K, sp, _) in shapes)
+    ws = torch.zeros(wsw, device=DEV)
+    ctr = torch.zeros(ctw, dtype=torch.int32, device=DEV)
+    ops = []
+    for (M, N, K, sp, nn) in shapes:
+        A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        B = (torch.randn(K, N, generator=g) if nn else torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
+        ops.append((A, B, M, N, K, sp, nn, _ref(A, B, nn)))
+    for rep in range(3):
+        for (A, B, M, N, K, sp, nn, want) in ops[rep % 2:] + ops[:rep % 2]:
+            out = torch.full((M, N), float("nan"), device=DEV)
+            C.gemm_skinny(A, B, M, N, K, nn=nn, of32=out, splits=sp, ws=ws, ctr=ctr)
+            torch.cuda.synchronize()
+            err = (out - want).abs().max().item()
+            assert err <= 2e-5 * K ** 0.5 * want.abs().max().item() + 1e-4, (M, N, K, sp, err)
+    assert int(ctr.abs().sum().item()) == 0
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 4096, 4096), (64, 4096, 784), (64, 10, 4096), (48, 200, 136),

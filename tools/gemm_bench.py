@@ -69,10 +69,9 @@ def main() -> int:
         bias = torch.randn(N, device=dev)
         H = torch.empty(B, N, **bf)
         HT = torch.empty(N, B, **bf)
-        S = C.gemm_skinny_splits(B, N, K, 0)
-        tiles = (N + 63) // 64
-        ws = torch.zeros(S * tiles * 4096, device=dev)
-        ctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
+        wsw, ctw = C.gemm_skinny_ws(B, N, K, 8)
+        ws = torch.zeros(wsw, device=dev)
+        ctr = torch.zeros(ctw, dtype=torch.int32, device=dev)
         timeit(f"skinny_nt_{N}x{K}", lambda: C.gemm_skinny(A, W, B, N, K, bias=bias, relu=True, obf=H, obfT=HT,
                                                              ws=ws, ctr=ctr), nbytes=N * K * 2, flops=2 * B * N * K)
     for (N, K) in [(4096, 4096)]:
@@ -81,14 +80,13 @@ def main() -> int:
         mask = torch.randn(B, N, device=dev).to(torch.bfloat16)
         H = torch.empty(B, N, **bf)
         HT = torch.empty(N, B, **bf)
-        S = C.gemm_skinny_splits(B, N, K, 0)
-        tiles = (N + 63) // 64
-        ws = torch.zeros(S * tiles * 4096, device=dev)
-        ctr = torch.zeros(tiles, dtype=torch.int32, device=dev)
+        wsw, ctw = C.gemm_skinny_ws(B, N, K, 8)
+        ws = torch.zeros(wsw, device=dev)
+        ctr = torch.zeros(ctw, dtype=torch.int32, device=dev)
         timeit(f"skinny_nn_{N}x{K}", lambda: C.gemm_skinny(A, W, B, N, K, nn=True, mask=mask, obf=H, obfT=HT,
                                                              ws=ws, ctr=ctr), nbytes=N * K * 2, flops=2 * B * N * K)
         for sp in (2, 4, 8):
-            ws8 = torch.zeros(sp * tiles * 4096, device=dev)
+            ws8 = ws
             timeit(f"skinny_nn_{N}x{K}_s{sp}", lambda sp=sp, ws8=ws8: C.gemm_skinny(
                 A, W, B, N, K, nn=True, mask=mask, obf=H, obfT=HT, splits=sp, ws=ws8, ctr=ctr),
                 nbytes=N * K * 2, flops=2 * B * N * K)
