@@ -305,7 +305,9 @@ def run(a) -> int:
                 # (the Gram forms assume the reference's fixed batch order,
                 # client.go:596: no shuffle), with their build times
                 "precompute": ({"gram_table": "gram_table" in tr.precompute_ms or
-                                "gram_table_dp" in tr.precompute_ms, "ms": dict(tr.precompute_ms)}
+                                "gram_table_dp" in tr.precompute_ms, "ms": dict(tr.precompute_ms),
+                                # hand-off buffer placements tried (us/step), fastest kept
+                                "persist_place_us": getattr(tr, "persist_place_us", None)}
                                if getattr(tr, "precompute_ms", None) else None),
             },
             "world_size": n,
