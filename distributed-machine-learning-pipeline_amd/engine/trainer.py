@@ -164,11 +164,13 @@ class MlpTrainer:
         self._want_persist = bool(persist)
         # hand-off buffers tried for the single-replica persistent step (the
         # fastest kept, see _place_persist_buffer); HIPDSML_PK_PLACE overrides
-        if persist_place_trials is None:
-            import os
+        import os
 
+        if persist_place_trials is None:
             persist_place_trials = int(os.environ.get("HIPDSML_PK_PLACE", "12"))
         self._place_trials = int(persist_place_trials)
+        # data parallel: candidates per rank in the collective search
+        self._place_trials_dp = int(os.environ.get("HIPDSML_PK_PLACE_DP", "4"))
         self.persist_place_us: Optional[list] = None
         self.pk_buf: Optional[torch.Tensor] = None
         self.pk_err: Optional[torch.Tensor] = None
@@ -397,6 +399,10 @@ class MlpTrainer:
             log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
             self.sync_times = times
         self._set_mode(choice or self.sync_active)
+        if self.sync_active in PERSIST_MODES and self._place_trials_dp > 1:
+            t0 = time.perf_counter()
+            self._place_persist_buffer_dp(self._place_trials_dp)  # collective
+            self.precompute_ms["persist_place_dp"] = round(1e3 * (time.perf_counter() - t0), 2)
         self._plain = None  # the all-gathered fp32 shards: only the tables' builds read them
         if self.sync_active not in XALL_MODES and self.Xall is not None:
             # the replicated inputs (N x the shard) are only read by xact / pkx:
@@ -485,6 +491,41 @@ class MlpTrainer:
         torch.cuda.synchronize(self.device)
         self.persist_place_us = [round(1e6 * t, 3) for t in times]
         del cands  # the other candidates go back to the allocator
+
+    def _place_persist_buffer_dp(self, trials: int, steps: int = 300) -> None:
+        """Collective: the data-parallel persistent step's hand-off buffer
+        placement (see _place_persist_buffer: the lone-replica pkx step at
+        N = 4 runs 9.5-10.7 us/step over 8 allocations of that buffer,
+        profiles/r5_pk_placement.json).  The step is as slow as its slowest
+        replica, so the search is coordinate descent over the ranks: in rank
+        r's turn, r alone tries `trials` - 1 fresh buffers (the others keep
+        theirs) and keeps one only if the max-over-ranks step time improves.
+        Every rank sees the same timings (_time_steps reduces them), so every
+        decision agrees."""
+        algo = PERSIST_MODES[self.sync_active]
+        timeout = max(2000.0, self.xchg_timeout_ms)
+        best = self._time_steps(steps)
+        times = [best]
+        cands = [self.pk_buf]
+        for r in range(self.ctx.world_size):
+            for _ in range(trials - 1):
+                prev = self.pk_buf
+                if self.ctx.rank == r:
+                    cands.append(torch.zeros_like(prev))
+                    self.pk_buf = cands[-1]
+                    self.runner.set_persist(self.pk_buf, self.pk_err, timeout, self.xchg, algo)
+                t = self._time_steps(steps)
+                times.append(t)
+                if t < best:
+                    best = t
+                elif self.ctx.rank == r:
+                    self.pk_buf = prev
+                    self.runner.set_persist(prev, self.pk_err, timeout, self.xchg, algo)
+        self._rewound()
+        torch.cuda.synchronize(self.device)
+        self.ctx.barrier()
+        self.persist_place_us = [round(1e6 * t, 3) for t in times]
+        del cands
 
     def _hip_step_torch_sync(self, n: int) -> None:
         import torch.distributed as dist
