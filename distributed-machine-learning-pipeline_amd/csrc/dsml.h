@@ -334,6 +334,9 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // 128 x 128 tiles for every layer with N, K >= 128, 64 x 64 for the rest; 64:
 // 64 x 64 everywhere; 0 (auto): 128 for fp32-master layers at M >= 512 rows,
 // else 64.
+// tile: 0 auto, 64 / 128 square tiles, kWgRowBlkTile the row-block form (split
+// master, one M of 64 / 128 / 256 / 512 for every layer; auto picks it from M >= 256)
+constexpr int kWgRowBlkTile = 256;
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);

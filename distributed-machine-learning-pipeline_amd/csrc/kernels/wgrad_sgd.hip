@@ -15,6 +15,8 @@
 // every workgroup issues its W-tile loads FIRST, so that HBM round trip
 // overlaps the operand staging and the MFMAs instead of following them.
 // Reference hot loop replaced: the per-sample weight update of client.go:112-202.
+#include <type_traits>
+
 #include "common.h"
 #include "../dsml.h"
 
@@ -638,6 +640,321 @@ __global__ __launch_bounds__(256) void wgrad_multi_big_k(WgMultiBig mb) {
   else wgrad_tile(a, kt, nt, lds);
 }
 
+// ---------------------------------------------------------------------------
+// Row-block form for a long batch: the global-batch update of sync=xact (M =
+// 64 N rows, up to 512).  At M = 512 the 64 x 64 tiles above re-read the
+// activation blocks 64 x 64 KiB per tile -- 537 MB of L2 traffic for the
+// 4096 x 4096 layer -- in M / 64 dependent rounds, and the 128 x 128 tiles run
+// two workgroups a CU: both 74 us (profiles/r4_wide_xact_cost.json).
+//
+// Here a workgroup owns a run of UNITS (a unit = 128 W rows x 64 k columns;
+// units in (layer, n block, k tile) order, G = #CU contiguous runs, one
+// workgroup a CU).  For each n block of its run it loads the Z^T operand of
+// those 128 rows ONCE into registers (MFMA A fragments for every 32-row batch
+// step: wave w keeps rows 32 w .. +31, M / 32 x 2 fragments), then streams the
+// X column blocks of its k tiles through an LDS ring that holds one k tile
+// (M / 32 blocks of 32 rows x 64 columns, 4 KiB each, one LDS-DMA per wave per
+// block).  Block b's slot is refilled with the NEXT tile's block b as soon as
+// every wave has read it, so a whole k tile of X stays in flight behind the
+// MFMAs; the W words of a tile (split master: hi + lo, 16 B each) are loaded
+// at the tile's start and the update is stored at its end.  Every wait is an
+// exact vmcnt (the issue order per wave is fixed: the ring's DMA, the W loads,
+// the stores -- all unpredicated buffer ops, out-of-range words dropped by
+// the descriptor), every LDS access of the loop is inline asm (the compiler's
+// own waits before an LDS access would be vmcnt(0) and drain the ring).
+// Activation traffic for the 4096 x 4096 layer at M = 512: X 128 MB + Z 32 MB
+// (vs 537 MB), and no dependent rounds.
+// ---------------------------------------------------------------------------
+constexpr int kRbN = 128;                      // W rows of an n block
+constexpr int kRbRing = 16 * 4096;             // one k tile of X: <= 16 blocks of 32 rows, 4 KiB each
+constexpr int kRbPitch = 68;                   // floats per row of the fp32 epilogue tile [128][68]
+constexpr int kRbLds = kRbRing + kRbN * kRbPitch * 4;
+constexpr int kRbMaxM = 512;
+constexpr bool kRbAuto = false;                // auto dispatch (tile 0) picks it at M >= 256
+constexpr int kRbOob = 0x7ffffff0;             // offset of a dropped word: past every bound (host check)
+
+struct WgRowBlk {
+  WgArgs l[kWgMaxLayers];
+  int ustart[kWgMaxLayers + 1];  // first unit of each layer (prefix sums); ustart[n] = all units
+  int ktiles[kWgMaxLayers];
+  int n;
+  int groups;  // workgroups: g owns units [g U / G, (g + 1) U / G)
+};
+
+// s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] << 14).  N is a
+// compile-time constant: a runtime count became a 48-way branch tree, ~50
+// scalar branches per block of the ring (round 5, first cut: 83.8 us at M = 512).
+template <int N>
+__device__ __forceinline__ void rb_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// f(integral_constant<int, B>) for B = B0 .. N - 1 (compile-time block indices)
+template <int B0, int N, class F>
+__device__ __forceinline__ void rb_for(F& f) {
+  if constexpr (B0 < N) {
+    f(std::integral_constant<int, B0>{});
+    rb_for<B0 + 1, N>(f);
+  }
+}
+// the wait for block B of a k tile: this tile's later blocks, the last tile's
+// 8 stores (tile > 0), this tile's 8 W loads, the refills made in this loop
+template <int NBLK, int B, bool LATER, bool MORE>
+__device__ __forceinline__ void rb_vm_block() {
+  rb_vm<(NBLK - 1 - B) + (LATER ? 8 : 0) + 8 + ((MORE && B > 0) ? B - 1 : 0)>();
+}
+__device__ __forceinline__ void rb_dsw32(uint32_t addr, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ wg_u4 rb_dsr128(uint32_t addr) {
+  wg_u4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void rb_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// A or B fragment (16 x 16 x 32 bf16) from a row-major image: lane (i, g) gets
+// image column c0 + i at rows 8 g .. +7 of the 32-row block (two transposing
+// 8-B reads).  pitch: 128 (X blocks, wg_swz) or 256 (Z chunks, bg_swz).
+template <int PITCH>
+__device__ __forceinline__ void rb_frag_issue(uint32_t img, int c0, int lane, wg_u2& lo, wg_u2& hi) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  const int s0 = PITCH == 128 ? wg_swz(r0) : bg_swz(r0), s1 = PITCH == 128 ? wg_swz(r1) : bg_swz(r1);
+  lo = bg_dstr(img + r0 * PITCH + 16 * (ch ^ s0) + 8 * (p & 1));
+  hi = bg_dstr(img + r1 * PITCH + 16 * (ch ^ s1) + 8 * (p & 1));
+}
+
+template <int NBLK>
+__global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
+  extern __shared__ __attribute__((aligned(16))) char rb_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const uint32_t ring = (uint32_t)(uintptr_t)(wg_lptr)rb_lds;
+  const uint32_t tileb = ring + kRbRing;
+  const int U = rb.ustart[rb.n];
+  const int u0 = (int)((int64_t)blockIdx.x * U / rb.groups);
+  const int u1 = (int)((int64_t)(blockIdx.x + 1) * U / rb.groups);
+  for (int u = u0; u < u1;) {
+    // ---- segment: units u .. of one n block of one layer ----
+    int j = 0;
+#pragma unroll
+    for (int q = 1; q < kWgMaxLayers; ++q)
+      if (q < rb.n && u >= rb.ustart[q]) j = q;
+    WgArgs a = rb.l[0];
+    int kts = rb.ktiles[0];
+#pragma unroll
+    for (int q = 1; q < kWgMaxLayers; ++q)
+      if (j == q) { a = rb.l[q]; kts = rb.ktiles[q]; }
+    const int lu = u - rb.ustart[j];
+    const int nb = lu / kts, kt0 = lu - nb * kts;
+    const int ntl = min(u1, rb.ustart[j] + (nb + 1) * kts) - u;  // k tiles of this segment
+    u += ntl;
+    const int n0 = nb * kRbN;
+    constexpr int nblk = NBLK;  // M = 32 NBLK (the host picks the instance)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous segment's stores
+    rb_barrier();                                      // and every wave out of the LDS
+
+    // Buffer-addressed LDS-DMA (32-bit per-lane offsets; 64-bit global_load_lds
+    // addresses had the compiler hoist an address pair per unrolled block and
+    // spill them).  Every offset is clamped inside its tensor (columns past N /
+    // K re-read the row's last 8 words, as the 64 x 64 form does: they only feed
+    // outputs that are never stored), so no access relies on the bounds check.
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.Z), (short)0, (int)(a.M * a.ldz * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.X), (short)0, (int)(a.M * a.ldx * 2), 0x00020000);
+    const int nmax = (int)((a.N + 7) & ~7) - 8, kmax = (int)((a.K + 7) & ~7) - 8;
+    int zv[2];  // this lane's Z chunk offset (row r of the chunk, clamped column), bytes
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int r = 8 * w + 4 * jj + (lane >> 4), pc = lane & 15;
+      zv[jj] = (int)((r * a.ldz + min(n0 + 8 * (pc ^ bg_swz(r)), nmax)) * 2);
+    }
+    const int xr = 8 * w + (lane >> 3), xc = 8 * ((lane & 7) ^ wg_swz(xr));
+
+    // ---- Z^T fragments into registers: 32-row chunks [32][128] (256-B rows), 8 per phase ----
+    wg_u4 zf[16][2];
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      if (8 * ph < nblk) {
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          const int c = 8 * ph + cc;
+          if (c < nblk) {
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (wg_lptr)(rb_lds + cc * 8192 + (8 * w + 4 * jj) * 256), 16,
+                                                      zv[jj] + (int)(32 * c * a.ldz * 2), 0, 0, 0);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rb_barrier();
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          const int c = 8 * ph + cc;
+          if (c < nblk) {
+            wg_u2 lo0, hi0, lo1, hi1;
+            rb_frag_issue<256>(ring + cc * 8192, 32 * w, lane, lo0, hi0);
+            rb_frag_issue<256>(ring + cc * 8192, 32 * w + 16, lane, lo1, hi1);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo0), "+v"(hi0), "+v"(lo1), "+v"(hi1)::"memory");
+            zf[c][0] = wg_u4{lo0.x, lo0.y, hi0.x, hi0.y};
+            zf[c][1] = wg_u4{lo1.x, lo1.y, hi1.x, hi1.y};
+          }
+        }
+        rb_barrier();  // the chunks' slots are free again
+      }
+    }
+
+    // ---- bias gradient (the segment holding k tile 0): column sums of Z, from the fragments ----
+    if (kt0 == 0 && (a.bias || a.bgrad)) {
+      float sm[2] = {0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c < nblk) {
+#pragma unroll
+          for (int xm = 0; xm < 2; ++xm) {
+            const wg_u4 v = zf[c][xm];
+            sm[xm] += ((bf16_to_f32(v.x & 0xffffu) + bf16_to_f32(v.x >> 16)) +
+                       (bf16_to_f32(v.y & 0xffffu) + bf16_to_f32(v.y >> 16))) +
+                      ((bf16_to_f32(v.z & 0xffffu) + bf16_to_f32(v.z >> 16)) +
+                       (bf16_to_f32(v.w & 0xffffu) + bf16_to_f32(v.w >> 16)));
+          }
+        }
+      }
+#pragma unroll
+      for (int xm = 0; xm < 2; ++xm) {
+        sm[xm] += __shfl_xor(sm[xm], 16, 64);
+        sm[xm] += __shfl_xor(sm[xm], 32, 64);
+        const int n = n0 + 32 * w + 16 * xm + i;
+        if (lane < 16 && n < a.N) {
+          const float db = a.alpha * sm[xm];
+          if (a.bias) a.bias[n] -= a.lr * db;
+          if (a.bgrad) a.bgrad[n] = db;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's count starts from zero
+    }
+
+    // ---- X ring: block b of local k tile lt -> slot b (wave w: rows 8 w .. +7) ----
+    auto xdma = [&](int lt, int b) __attribute__((always_inline)) {
+      const int off = (int)(((32 * b + xr) * a.ldx + min((kt0 + lt) * 64 + xc, kmax)) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (wg_lptr)(rb_lds + b * 4096 + w * 1024), 16, off, 0, 0, 0);
+    };
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+      if (b < nblk) xdma(0, b);
+
+    // bounds = the matrices' exact byte sizes: the out-of-range words' offset
+    // kRbOob lies past every one of them, so those loads return 0 and those
+    // stores are dropped (a bound of 0x7fffffff would have let them through)
+    const int bh = (int)(a.N * a.ldwh * 2), bl = (int)(a.N * a.ldwl * 2), bw = (int)(a.N * a.ldwb * 2);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.Wh), (short)0, bh, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(a.Wl, (short)0, bl, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.Wb, (short)0, bw, 0x00020000);
+    const int er = tid >> 3, ec = 8 * (tid & 7);  // epilogue: rows er + 32 jj, columns ec .. +7
+    for (int lt = 0; lt < ntl; ++lt) {
+      const int k0 = (kt0 + lt) * 64;
+      const bool more = lt + 1 < ntl;
+      // W words of this tile: 4 hi + 4 lo loads, always issued (out of range -> 0)
+      wg_u4 whv[4], wlv[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int nr = n0 + er + 32 * jj, kc = k0 + ec;
+        const bool ok = nr < a.N && kc < a.K;
+        whv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? (int)((nr * a.ldwh + kc) * 2) : kRbOob, 0, 0);
+        wlv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rl, ok ? (int)((nr * a.ldwl + kc) * 2) : kRbOob, 0, 0);
+      }
+      f32x4 acc[2][4];
+#pragma unroll
+      for (int xm = 0; xm < 2; ++xm)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[xm][y] = {0.f, 0.f, 0.f, 0.f};
+      // one 32-row block of the ring (b: a compile-time index -- the waits' counts
+      // and the Z^T fragment registers are static)
+      auto block = [&](auto bc) __attribute__((always_inline)) {
+        constexpr int b = decltype(bc)::value;
+        if (lt > 0) {
+          if (more) rb_vm_block<NBLK, b, true, true>();
+          else rb_vm_block<NBLK, b, true, false>();
+        } else {
+          if (more) rb_vm_block<NBLK, b, false, true>();
+          else rb_vm_block<NBLK, b, false, false>();
+        }
+        rb_barrier();  // every wave's part of block b landed; block b - 1 read by all
+        if (more && b > 0) xdma(lt + 1, b - 1);
+        wg_u2 lo[4], hi[4];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) rb_frag_issue<128>(ring + b * 4096, 16 * y, lane, lo[y], hi[y]);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]),
+                       "+v"(hi[2]), "+v"(hi[3])::"memory");
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const wg_u4 fx = {lo[y].x, lo[y].y, hi[y].x, hi[y].y};
+#pragma unroll
+          for (int xm = 0; xm < 2; ++xm)
+            acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][xm]),
+                                                                __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
+                                                                0, 0, 0);
+        }
+      };
+      rb_for<0, NBLK>(block);
+      // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
+      if (more) rb_vm<NBLK - 1>();  // this tile's W words (only the refills are younger)
+      else rb_vm<0>();
+#pragma unroll
+      for (int xm = 0; xm < 2; ++xm)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rb_dsw32(tileb + ((32 * w + 16 * xm + 4 * g + r) * kRbPitch + 16 * y + i) * 4, acc[xm][y][r] * a.alpha);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      rb_barrier();  // the tile is whole; every wave has read the last block
+      if (more) xdma(lt + 1, nblk - 1);
+      wg_u4 gv[4][2];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        gv[jj][0] = rb_dsr128(tileb + ((er + 32 * jj) * kRbPitch + ec) * 4);
+        gv[jj][1] = rb_dsr128(tileb + ((er + 32 * jj) * kRbPitch + ec + 4) * 4);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(gv[0][0]), "+v"(gv[0][1]), "+v"(gv[1][0]), "+v"(gv[1][1]), "+v"(gv[2][0]),
+                     "+v"(gv[2][1]), "+v"(gv[3][0]), "+v"(gv[3][1])::"memory");
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int nr = n0 + er + 32 * jj, kc = k0 + ec;
+        const bool ok = nr < a.N && kc < a.K;
+        float wv[8];
+        hl_join8(make_uint4(whv[jj].x, whv[jj].y, whv[jj].z, whv[jj].w),
+                 make_uint4(wlv[jj].x, wlv[jj].y, wlv[jj].z, wlv[jj].w), wv);
+        const float gg[8] = {__uint_as_float(gv[jj][0].x), __uint_as_float(gv[jj][0].y),
+                             __uint_as_float(gv[jj][0].z), __uint_as_float(gv[jj][0].w),
+                             __uint_as_float(gv[jj][1].x), __uint_as_float(gv[jj][1].y),
+                             __uint_as_float(gv[jj][1].z), __uint_as_float(gv[jj][1].w)};
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v0 = wv[2 * e] - a.lr * gg[2 * e], v1 = wv[2 * e + 1] - a.lr * gg[2 * e + 1];
+          const uint32_t h0 = hl_hi(v0), h1 = hl_hi(v1);
+          hw[e] = h0 | (h1 << 16);
+          lw[e] = hl_lo(v0, h0) | (hl_lo(v1, h1) << 16);
+        }
+        // always issued (the ring's counts assume 8 stores a tile): out of range -> dropped
+        __builtin_amdgcn_raw_buffer_store_b128(wg_u4{hw[0], hw[1], hw[2], hw[3]}, rw,
+                                               ok ? (int)((nr * a.ldwb + kc) * 2) : kRbOob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(wg_u4{lw[0], lw[1], lw[2], lw[3]}, rl,
+                                               ok ? (int)((nr * a.ldwl + kc) * 2) : kRbOob, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 bool wg_valid(const WgArgs& a) {
   if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
       a.ldz < ((a.N + 7) & ~7) || a.ldx < ((a.K + 7) & ~7) || (((uintptr_t)a.Z | (uintptr_t)a.X) & 15))
@@ -666,8 +983,59 @@ hipError_t wgrad_sgd(const uint16_t* Z, int64_t ldz, const uint16_t* X, int64_t 
   return hipGetLastError();
 }
 
+// The row-block form's launch (see wgrad_rowblk_k); false: a layer does not fit it.
+static bool rowblk_fits(const WgLayer& L) {
+  return L.Wl != nullptr && L.W == nullptr && L.G == nullptr &&
+         (L.M == 64 || L.M == 128 || L.M == 256 || L.M == kRbMaxM) &&
+         (int64_t)L.M * L.ldz * 2 < 0x7fffffff && (int64_t)L.M * L.ldx * 2 < 0x7fffffff &&
+         (int64_t)L.N * L.ldwb * 2 + 16 <= kRbOob && (int64_t)L.N * L.ldwl * 2 + 16 <= kRbOob &&
+         (int64_t)L.N * L.ldwh * 2 + 16 <= kRbOob;
+}
+static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t s) {
+  WgRowBlk rb{};
+  rb.n = n;
+  int u = 0;
+  for (int j = 0; j < n; ++j) {
+    rb.l[j] = layers[j];
+    rb.ustart[j] = u;
+    rb.ktiles[j] = (layers[j].K + 63) / 64;
+    u += rb.ktiles[j] * ((layers[j].N + kRbN - 1) / kRbN);
+  }
+  for (int j = n; j <= kWgMaxLayers; ++j) rb.ustart[j] = u;
+  for (int j = n; j < kWgMaxLayers; ++j) { rb.l[j] = layers[0]; rb.ktiles[j] = rb.ktiles[0]; }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const void* fs[4] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
+                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>)};
+    for (const void* f : fs) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRbLds);
+      if (e != hipSuccess) { cus = 0; return e; }
+    }
+  }
+  rb.groups = std::min(cus, u);
+  switch (layers[0].M) {
+    case 64: hipLaunchKernelGGL(wgrad_rowblk_k<2>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    case 128: hipLaunchKernelGGL(wgrad_rowblk_k<4>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    case 256: hipLaunchKernelGGL(wgrad_rowblk_k<8>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    default: hipLaunchKernelGGL(wgrad_rowblk_k<16>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile) {
-  if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT)) return hipErrorInvalidValue;
+  if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT && tile != kWgRowBlkTile))
+    return hipErrorInvalidValue;
+  // the row-block form when asked for (tile kWgRowBlkTile); auto keeps the
+  // square tiles until the row-block form measures faster (kRbAuto)
+  bool rows = tile == kWgRowBlkTile || (tile == 0 && kRbAuto);
+  for (int j = 0; j < n && rows; ++j)
+    rows = wg_valid(layers[j]) && rowblk_fits(layers[j]) && layers[j].M == layers[0].M &&
+           (tile == kWgRowBlkTile || layers[j].M >= 256);
+  if (tile == kWgRowBlkTile && !rows) return hipErrorInvalidValue;
+  if (rows) return wgrad_rowblk_launch(layers, n, s);
   WgMultiBig mb{};
   WgMulti& m = mb.m;
   m.n = n;

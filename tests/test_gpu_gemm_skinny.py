@@ -190,3 +190,52 @@ def test_wgrad_sgd_multi_big_tiles_gradient_form(M):
     Gref = 0.5 * Z.float().t() @ X.float()
     assert (G - Gref).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
     assert (db - 0.5 * Z.float().sum(0)).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
+
+
+@pytest.mark.parametrize("M", [64, 256, 512])
+def test_wgrad_rowblk_matches_square_tiles(M):
+    """The row-block form of the split-master update (tile=256: Z^T resident in
+    registers, X streamed through a one-tile LDS ring; what sync=xact runs from
+    M = 256 on) against the 64 x 64 tiles: the same 32-row MFMA sequence per
+    element, so the updated hi / lo words are bit-identical; the bias sums run
+    in another order (tolerance).  Shapes with an n tail (200 rows: a partial
+    128-row block), a k tail (784 = 12 x 64 + 16) and the 10-row classifier;
+    more units than workgroups, so runs cross n blocks and layers."""
+    C = require_native()
+    g = torch.Generator(device="cpu").manual_seed(123 + M)
+    shapes = [(10, 1024), (200, 784), (1024, 1024)]
+    runs = {}
+    for tile in (64, 256):
+        args = []
+        for N, K in shapes:
+            pn, pk = (N + 15) // 16 * 16, (K + 15) // 16 * 16
+            g.manual_seed(7 * N + K + M)
+            Z = torch.zeros(M, pn, dtype=torch.bfloat16)
+            X = torch.zeros(M, pk, dtype=torch.bfloat16)
+            Z[:, :N] = torch.randn(M, N, generator=g).to(torch.bfloat16)
+            X[:, :K] = torch.randn(M, K, generator=g).to(torch.bfloat16)
+            W = torch.randn(N, pk, generator=g)
+            W[:, K:] = 0
+            Wh = torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV)
+            Wl = torch.zeros(N, pk, dtype=torch.int16, device=DEV)
+            C.hilo_split(W.to(DEV), Wh, Wl)
+            b = torch.randn(N, generator=g).to(DEV)
+            args.append((Z.to(DEV), X.to(DEV), M, N, K, 0.5, 0.01, None,
+                         torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV), None, b, None, Wh, Wl))
+        C.wgrad_sgd_multi(args, tile=tile)
+        torch.cuda.synchronize()
+        runs[tile] = args
+    for a64, a256 in zip(runs[64], runs[256]):
+        assert torch.equal(a64[8], a256[8]), "updated hi words differ"
+        assert torch.equal(a64[13], a256[13]), "updated lo words differ"
+        assert (a64[10] - a256[10]).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
+    # and against fp32: W - lr * alpha * Z^T X
+    for (Z, X, M_, N, K, al, lr, _, Wb, _, b, _, Wh, Wl) in runs[256]:
+        Wn = torch.zeros(N, Wb.shape[1], device=DEV)
+        C.hilo_join(Wb, Wl, Wn)
+        g.manual_seed(7 * N + K + M)
+        Zr = torch.randn(M, N, generator=g).to(torch.bfloat16).float()
+        Xr = torch.randn(M, K, generator=g).to(torch.bfloat16).float()
+        W0 = torch.randn(N, (K + 15) // 16 * 16, generator=g)[:, :K]
+        want = W0 - lr * al * (Zr.t() @ Xr)
+        assert (Wn[:, :K].cpu() - want).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
