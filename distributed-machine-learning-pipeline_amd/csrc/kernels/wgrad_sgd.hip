@@ -670,7 +670,7 @@ constexpr int kRbRing = 16 * 4096;             // one k tile of X: <= 16 blocks 
 constexpr int kRbPitch = 68;                   // floats per row of the fp32 epilogue tile [128][68]
 constexpr int kRbLds = kRbRing + kRbN * kRbPitch * 4;
 constexpr int kRbMaxM = 512;
-constexpr bool kRbAuto = false;                // auto dispatch (tile 0) picks it at M >= 256
+constexpr bool kRbAuto = true;                 // auto dispatch (tile 0) picks it at M >= 256
 constexpr int kRbOob = 0x7ffffff0;             // offset of a dropped word: past every bound (host check)
 
 struct WgRowBlk {
@@ -698,11 +698,13 @@ __device__ __forceinline__ void rb_for(F& f) {
     rb_for<B0 + 1, N>(f);
   }
 }
-// the wait for block B of a k tile: this tile's later blocks, the last tile's
-// 8 stores (tile > 0), this tile's 8 W loads, the refills made in this loop
+// the wait in iteration B for block B + 1 of a k tile (B = -1: block 0, before
+// the loop): ops issued after it are this tile's later blocks, the last tile's
+// 8 stores (tile > 0), this tile's 8 W loads and the refills of iterations
+// 0 .. B - 1 (slot b takes the next tile's block b in iteration b)
 template <int NBLK, int B, bool LATER, bool MORE>
 __device__ __forceinline__ void rb_vm_block() {
-  rb_vm<(NBLK - 1 - B) + (LATER ? 8 : 0) + 8 + ((MORE && B > 0) ? B - 1 : 0)>();
+  rb_vm<(NBLK - 2 - B) + (LATER ? 8 : 0) + 8 + ((MORE && B > 0) ? B : 0)>();
 }
 __device__ __forceinline__ void rb_dsw32(uint32_t addr, float v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
@@ -873,34 +875,51 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
       for (int xm = 0; xm < 2; ++xm)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[xm][y] = {0.f, 0.f, 0.f, 0.f};
-      // one 32-row block of the ring (b: a compile-time index -- the waits' counts
-      // and the Z^T fragment registers are static)
+      // The ring, software-pipelined: block b + 1's X fragments are read while
+      // block b's MFMAs run (b: a compile-time index -- the waits' counts and the
+      // Z^T fragment registers are static).  Block b was read (and its reads
+      // retired) one iteration earlier, so after iteration b's barrier its slot
+      // takes the next tile's block b.
+      wg_u2 lo[2][4], hi[2][4];
+      auto reads = [&](int b, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) rb_frag_issue<128>(ring + b * 4096, 16 * y, lane, lo[buf][y], hi[buf][y]);
+      };
+      auto lgkm = [&](int buf) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(lo[buf][0]), "+v"(lo[buf][1]), "+v"(lo[buf][2]), "+v"(lo[buf][3]), "+v"(hi[buf][0]),
+                       "+v"(hi[buf][1]), "+v"(hi[buf][2]), "+v"(hi[buf][3])::"memory");
+      };
+      if (lt > 0) rb_vm_block<NBLK, -1, true, false>();  // block 0 (nothing of this loop issued yet)
+      else rb_vm_block<NBLK, -1, false, false>();
+      rb_barrier();
+      reads(0, 0);
+      lgkm(0);
       auto block = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
-        if (lt > 0) {
-          if (more) rb_vm_block<NBLK, b, true, true>();
-          else rb_vm_block<NBLK, b, true, false>();
-        } else {
-          if (more) rb_vm_block<NBLK, b, false, true>();
-          else rb_vm_block<NBLK, b, false, false>();
+        constexpr int cur = b & 1, nxt = cur ^ 1;
+        if constexpr (b + 1 < NBLK) {
+          if (lt > 0) {
+            if (more) rb_vm_block<NBLK, b, true, true>();
+            else rb_vm_block<NBLK, b, true, false>();
+          } else {
+            if (more) rb_vm_block<NBLK, b, false, true>();
+            else rb_vm_block<NBLK, b, false, false>();
+          }
+          rb_barrier();  // block b + 1 landed everywhere; block b read by all
+          if (more) xdma(lt + 1, b);
+          reads(b + 1, nxt);
         }
-        rb_barrier();  // every wave's part of block b landed; block b - 1 read by all
-        if (more && b > 0) xdma(lt + 1, b - 1);
-        wg_u2 lo[4], hi[4];
-#pragma unroll
-        for (int y = 0; y < 4; ++y) rb_frag_issue<128>(ring + b * 4096, 16 * y, lane, lo[y], hi[y]);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]),
-                       "+v"(hi[2]), "+v"(hi[3])::"memory");
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          const wg_u4 fx = {lo[y].x, lo[y].y, hi[y].x, hi[y].y};
+          const wg_u4 fx = {lo[cur][y].x, lo[cur][y].y, hi[cur][y].x, hi[cur][y].y};
 #pragma unroll
           for (int xm = 0; xm < 2; ++xm)
             acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][xm]),
                                                                 __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
                                                                 0, 0, 0);
         }
+        if constexpr (b + 1 < NBLK) lgkm(nxt);
       };
       rb_for<0, NBLK>(block);
       // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
@@ -1028,8 +1047,9 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile) {
   if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT && tile != kWgRowBlkTile))
     return hipErrorInvalidValue;
-  // the row-block form when asked for (tile kWgRowBlkTile); auto keeps the
-  // square tiles until the row-block form measures faster (kRbAuto)
+  // the row-block form when asked for (tile kWgRowBlkTile) or, auto, at M >= 256
+  // (M = 256 / 512: 47.3 / 64.7 us against 48.0 / 73.5 for the 64 x 64 tiles,
+  // profiles/r5_wide_xact_cost.json; below 256 the square tiles are faster)
   bool rows = tile == kWgRowBlkTile || (tile == 0 && kRbAuto);
   for (int j = 0; j < n && rows; ++j)
     rows = wg_valid(layers[j]) && rowblk_fits(layers[j]) && layers[j].M == layers[0].M &&
