@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "head_row.h"
 #include "../dsml.h"
 
 namespace dsml {
@@ -778,174 +779,19 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
   return hipGetLastError();
 }
 
-// Fused classifier head: logits[m][c] = H[m] . W[c] + b[c] for C <= 16
-// classes, then softmax-CE as softmax_xent_k — one 256-thread block per row.
-// Replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
-// Both products run on packed-bf16 dot instructions (v_dot2c_f32_bf16: two
-// bf16 MACs per lane per issue, straight from the loaded bf16 pairs, no
-// unpacking): the logits pair k-neighbours, the activation gradient pairs
-// class neighbours (one v_perm per output pair).  The per-class block sum is a
-// DPP row sum per class + 16 row partials through LDS (no bank conflicts: the
-// r4 LDS transpose read 16 consecutive floats per lane, 71% conflicted).
+// Fused classifier head (kernels/head_row.h): one 256-thread block per row;
+// replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
 __device__ uint64_t g_head_stamps[64][6];
 __constant__ int g_head_stamp_on;  // __constant__: scalar loads, no vector wait ahead of the batch
 __constant__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bit 1 the dzp phase
-#define HEAD_STAMP(k)                                                               \
-  do {                                                                              \
-    if (g_head_stamp_on && t == 0 && m < 64) g_head_stamps[m][(k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-constexpr int kHeadMaxC = 16;  // classes the head supports (instantiated for <= 10 and <= 16)
-constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
-typedef __bf16 hbf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float hdot2(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(hbf2, a), __builtin_bit_cast(hbf2, b), c, false);
-}
-__device__ __forceinline__ float hdot8(const uint4& a, const uint4& b, float c) {
-  return hdot2(a.w, b.w, hdot2(a.z, b.z, hdot2(a.y, b.y, hdot2(a.x, b.x, c))));
-}
 // MAXC: the class count rounded up to an instantiated size (even: class pairs)
 template <int MAXC>
-__global__ __launch_bounds__(256) void head_softmax_xent_k(
-    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw,
-    const float* __restrict__ bias, int K, int C, const int32_t* __restrict__ labels,
-    float inv_batch, float* __restrict__ logits, int64_t ldl, uint16_t* __restrict__ dz,
-    int64_t ldz, uint16_t* __restrict__ dzT, int64_t ldt, int Cp, float* __restrict__ stats,
-    uint16_t* __restrict__ dzp, int64_t ldzp, uint16_t* __restrict__ dzpT, int64_t ldpt,
-    int row_stats) {
-  static_assert(MAXC % 2 == 0 && MAXC <= 16, "class pairs, one 16-lane row");
+__global__ __launch_bounds__(256) void head_softmax_xent_k(HeadRow h) {
   __shared__ float part[MAXC][17];     // [class][wave * 4 + 16-lane row] partial sums (+1: pad)
   __shared__ uint32_t gz2[MAXC / 2];   // bf16-rounded dLogits of this row, class pairs
-  const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint16_t* hr = H + (int64_t)m * ldh;
-  // the softmax's own operands go out with the first loads (not after the reduction)
-  HEAD_STAMP(0);
-  const int y = labels[m];
-  const float bc = bias ? bias[min(lane, C - 1)] : 0.f;  // lanes >= C: unused
-  // this row's own loss / correct / count accumulators (row_stats: only this
-  // workgroup touches them): read now, under the operand loads, and written
-  // back with one plain store after the softmax -- a read-modify-write with
-  // no round trip of its own (device atomics there kept the kernel's tail
-  // waiting 1.8 us for their completion: head_bench dbg1)
-  const bool rst = row_stats && stats && w == 0;
-  float4 racc = rst ? *reinterpret_cast<const float4*>(stats + 4 * (int64_t)m) : make_float4(0.f, 0.f, 0.f, 0.f);
-  // every load of the thread in one batch, unpredicated (clamped addresses,
-  // out-of-range chunks zeroed after): its H chunks and the same chunks of all
-  // C rows of W.  A predicated load is a branch around it, and the compiler
-  // waited for each branch's load before the next (three serialised L2 round
-  // trips in the r4 head's ISA).  Rows past C load row C - 1: their logits are
-  // never read and their dLogits are 0.
-  uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][MAXC];
-#pragma unroll
-  for (int j = 0; j < kHeadMaxK8; ++j) {
-    const int k = min((t + 256 * j) * 8, K - 8);
-    hv[j] = *reinterpret_cast<const uint4*>(hr + k);
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      wv[j][c] = *reinterpret_cast<const uint4*>(W + (int64_t)min(c, C - 1) * ldw + k);
-  }
-#pragma unroll
-  for (int j = 0; j < kHeadMaxK8; ++j)
-    if ((t + 256 * j) * 8 >= K) hv[j] = make_uint4(0u, 0u, 0u, 0u);  // zero H: zero products
-  float acc[MAXC];
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    acc[c] = 0.f;
-#pragma unroll
-    for (int j = 0; j < kHeadMaxK8; ++j) acc[c] = hdot8(hv[j], wv[j][c], acc[c]);
-  }
-  HEAD_STAMP(1);
-  // block reduction per class: DPP sum over each 16-lane row, 16 row partials via LDS
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const float v = row16_sum(acc[c]);
-    if ((lane & 15) == 0) part[c][4 * w + (lane >> 4)] = v;
-  }
-  lds_barrier();  // LDS only: no wait for this block's global stores
-  HEAD_STAMP(2);
-  if (w == 0) {
-    const int c = lane;
-    const bool cv = c < C;
-    float z = -3.402823466e38f;
-    if (cv) {
-      float v = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v += part[c][r];
-      z = v + bc;
-    }
-    if (cv && logits) logits[(int64_t)m * ldl + c] = z;
-    // every class sits in lanes 0-15 (C <= 16): 16-lane DPP reductions
-    // instead of 64-lane shuffles (each an LDS-path ds_bpermute round trip)
-    float mx = z;
-    int am = cv ? c : 0x7fffffff;
-    row16_argmax(mx, am);
-    const float e = cv ? expf(z - mx) : 0.f;
-    const float se = row16_sum(e);
-    const float p = e / se;
-    const float gr = cv ? (p - (c == y ? 1.f : 0.f)) * inv_batch : 0.f;
-    const uint16_t hq = f32_to_bf16(gr);
-    if (c < Cp) {
-      dz[(int64_t)m * ldz + c] = hq;
-      if (dzT) dzT[(int64_t)c * ldt + m] = hq;
-    }
-    // class pairs for the packed dZ pass: lane 2i packs (its, lane 2i+1's)
-    const uint32_t hi = (uint32_t)__shfl_xor((int)hq, 1);
-    if (c < MAXC && !(c & 1)) gz2[c >> 1] = (uint32_t)hq | (hi << 16);
-    if (c == y && stats && !(g_head_dbg & 1)) {
-      if (row_stats) {
-        racc.x += -logf(p + 1e-10f);
-        racc.y += am == y ? 1.f : 0.f;
-        racc.z += 1.f;
-        *reinterpret_cast<float4*>(stats + 4 * (int64_t)m) = racc;
-      } else {
-        atomicAdd(stats + 0, -logf(p + 1e-10f));
-        atomicAdd(stats + 1, am == y ? 1.f : 0.f);
-        atomicAdd(stats + 2, 1.f);
-      }
-    }
-  }
-  HEAD_STAMP(3);
-  if (dzp == nullptr || (g_head_dbg & 2)) return;
-  // ---- fused activation gradient of the layer below (the NEXT backward GEMM):
-  // dZ_prev[m][k] = (sum_c dZ[m][c] W[c][k]) * (H[m][k] > 0), from the W and H
-  // chunks this thread already holds; bf16 row store + transposed copy.
-  lds_barrier();  // LDS only: no wait for this block's global stores
-  uint32_t g2[MAXC / 2];
-#pragma unroll
-  for (int i = 0; i < MAXC / 2; ++i) g2[i] = gz2[i];
-#pragma unroll
-  for (int j = 0; j < kHeadMaxK8; ++j) {
-    const int k = (t + 256 * j) * 8;
-    if (k >= K) continue;
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < MAXC / 2; ++i) {
-      if (2 * i >= C) break;  // zero pairs past the classes (W rows not loaded)
-      const uint32_t x0[4] = {wv[j][2 * i].x, wv[j][2 * i].y, wv[j][2 * i].z, wv[j][2 * i].w};
-      const uint32_t x1[4] = {wv[j][2 * i + 1].x, wv[j][2 * i + 1].y, wv[j][2 * i + 1].z,
-                              wv[j][2 * i + 1].w};
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        // (W[2i][k'], W[2i+1][k']) for the even and the odd k' of this dword
-        a[2 * d] = hdot2(__builtin_amdgcn_perm(x1[d], x0[d], 0x05040100u), g2[i], a[2 * d]);
-        a[2 * d + 1] = hdot2(__builtin_amdgcn_perm(x1[d], x0[d], 0x07060302u), g2[i], a[2 * d + 1]);
-      }
-    }
-    const uint32_t hw[4] = {hv[j].x, hv[j].y, hv[j].z, hv[j].w};
-    uint16_t q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int16_t hb = (int16_t)(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xffffu);
-      q[e] = hb > 0 ? f32_to_bf16(a[e]) : (uint16_t)0;  // bf16 bits > 0 <=> value > 0
-    }
-    *reinterpret_cast<uint4*>(dzp + (int64_t)m * ldzp + k) =
-        make_uint4(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16),
-                   q[4] | ((uint32_t)q[5] << 16), q[6] | ((uint32_t)q[7] << 16));
-    if (dzpT) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dzpT[(int64_t)(k + e) * ldpt + m] = q[e];
-    }
-  }
-  HEAD_STAMP(4);
+  const int m = blockIdx.x;
+  h.dbg = g_head_dbg;
+  head_row<MAXC>(h, m, part, gz2, (g_head_stamp_on && m < 64) ? g_head_stamps[m] : nullptr);
 }
 
 hipError_t head_read_stamps(uint64_t* host_out) {
@@ -975,14 +821,12 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
       (ldw & 7) ||
       (((uintptr_t)H | (uintptr_t)W) & 15))
     return hipErrorInvalidValue;
+  HeadRow h{H, ldh, W, ldw, bias, K, C, Cp, labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, stats,
+            dzp, ldzp, dzpT, ldpt, row_stats, 0};
   if (C <= 10)
-    hipLaunchKernelGGL(head_softmax_xent_k<10>, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K, C,
-                       labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
-                       ldpt, row_stats);
+    hipLaunchKernelGGL(head_softmax_xent_k<10>, dim3(B), dim3(256), 0, s, h);
   else
-    hipLaunchKernelGGL(head_softmax_xent_k<kHeadMaxC>, dim3(B), dim3(256), 0, s, H, ldh, W, ldw, bias, K,
-                       C, labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, Cp, stats, dzp, ldzp, dzpT,
-                       ldpt, row_stats);
+    hipLaunchKernelGGL(head_softmax_xent_k<kHeadMaxC>, dim3(B), dim3(256), 0, s, h);
   return hipGetLastError();
 }
 
