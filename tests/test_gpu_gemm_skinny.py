@@ -203,7 +203,8 @@ def test_wgrad_rowblk_matches_square_tiles(M):
     more units than workgroups, so runs cross n blocks and layers."""
     C = require_native()
     g = torch.Generator(device="cpu").manual_seed(123 + M)
-    shapes = [(10, 1024), (200, 784), (1024, 1024)]
+    # (4096, 512): 32 n blocks of 128 rows x 8 k tiles -- the XCD-split walk on 256 CUs
+    shapes = [(10, 1024), (200, 784), (1024, 1024), (4096, 512)]
     runs = {}
     for tile in (64, 256):
         args = []
