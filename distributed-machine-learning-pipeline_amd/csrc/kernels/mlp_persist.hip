@@ -1402,7 +1402,11 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     pk_jit(jit, blk, s, 2);
 
     // ---- wait for dZ1[:, n0 .. n0+15] of step s (4 chain blocks) ----
-    {
+    // (data parallel, gatherers and pkx owners: polled together with the
+    // peers' rows below -- one round of loads instead of the local rows'
+    // round trip and then the peers')
+    const bool dz_merged = XM && (XL || gat);
+    if (!dz_merged) {
       const int m = tid >> 2, qq = tid & 3;
       const int64_t g = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
       uint4 v0, v1;
@@ -1439,13 +1443,16 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     // ---- every other replica's dZ1[:, tile] (pushed by its chains), in rank
     // order: for the correction (gatherers) and, in pkx, every block's dW1 ----
     float* DzX = Gl;
-    if (XM && (XL || gat)) {
-      // every peer's granules loaded together (one round of loads in flight,
-      // not one poll per peer in turn); peers not yet complete are re-read
+    if (dz_merged) {
+      // every replica's granules loaded together (one round of loads in
+      // flight, not one poll per replica in turn), this replica's own rows
+      // (its local DZ1 region, never a probe preset) among them; replicas not
+      // yet complete are re-read
       const int m = tid >> 2, qq = tid & 3;
       const int off = (m * kD1 + n0 + 4 * qq) * 8;
+      const int64_t gl = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
       const float* rbase = a.xt.buf[a.rep];
-      uint32_t need = 0;  // peers whose rows this thread still waits for
+      uint32_t need = 1u << a.rep;  // replicas whose rows this thread still waits for
       // gatherers: every replica (the correction); other pkx owners: only the
       // replicas of their own dW1 part (the helpers read theirs) -- the exchange
       // memory is uncached, and every redundant poll is HBM traffic
@@ -1460,16 +1467,21 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
           if (need & (1u << r2)) {
-            const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
-            v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
-            v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
+            if (r2 == a.rep) {
+              v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(gl * 8), 0, kSc1);
+              v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)((gl + 2) * 8), 0, kSc1);
+            } else {
+              const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
+              v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
+              v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
+            }
           }
         }
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
-          if ((need & (1u << r2)) &&
-              (probe || (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
-            float* d = DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
+          if ((need & (1u << r2)) && ((probe && r2 != a.rep) ||
+                                      (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
+            float* d = r2 == a.rep ? Dz + m * 17 + 4 * qq : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
             d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
             d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
             need &= ~(1u << r2);
