@@ -12,6 +12,8 @@
 // lane, 71 % conflicted).  Every load of a thread goes out in one unpredicated
 // batch (a predicated load compiled to a branch whose copy-out waited vmcnt(0):
 // three serialised L2 round trips in the r4 ISA).
+// Reference: the client's softmax and loss gradient (DSML/client/client.go:76-90
+// softmax, :143-165 backwardPass: loss and dLogits), one batch row per workgroup here.
 #pragma once
 #include "common.h"
 
