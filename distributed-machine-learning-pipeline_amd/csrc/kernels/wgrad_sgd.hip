@@ -672,6 +672,10 @@ constexpr int kRbPitch = 68;                   // floats per row of the fp32 epi
 constexpr int kRbLds = kRbRing + kRbN * kRbPitch * 4;
 constexpr int kRbMaxM = 512;
 constexpr bool kRbAuto = true;                 // auto dispatch (tile 0) picks it at M >= 256
+#ifndef HIPDSML_RB_PAIR
+#define HIPDSML_RB_PAIR 1
+#endif
+constexpr bool kRbPair = HIPDSML_RB_PAIR != 0;  // two ring blocks per wait / barrier (NBLK >= 4)
 constexpr int kRbOob = 0x7ffffff0;             // offset of a dropped word: past every bound (host check)
 
 struct WgRowBlk {
@@ -883,6 +887,74 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
       // Z^T fragment registers are static).  Block b was read (and its reads
       // retired) one iteration earlier, so after iteration b's barrier its slot
       // takes the next tile's block b.
+      if constexpr (kRbPair && NBLK >= 4) {
+        // Two blocks per wait and barrier: blocks 2j + 2 and 2j + 3 are read
+        // while blocks 2j and 2j + 1 run their MFMAs -- half the waits,
+        // barriers and wait-select branches of the one-block form (the launch
+        // is issue-bound: 52 of 64 us at M = 512 with every byte dropped).
+        // Refills stay one DMA op a block, in block order, so the counts keep
+        // the one-block form's rule: waiting for block k of this tile, the ops
+        // issued after it are blocks k + 1 .. NBLK - 1, the last tile's 8
+        // stores, this tile's 8 W loads and this tile's refills so far.
+        wg_u2 lo[2][2][4], hi[2][2][4];
+        auto reads2 = [&](int b0, int buf) __attribute__((always_inline)) {
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+              rb_frag_issue<128>(ring + (b0 + sb) * 4096, 16 * y, lane, lo[buf][sb][y], hi[buf][sb][y]);
+        };
+        auto lgkm2 = [&](int buf) __attribute__((always_inline)) {
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(lo[buf][0][0]), "+v"(lo[buf][0][1]), "+v"(lo[buf][0][2]), "+v"(lo[buf][0][3]),
+                         "+v"(hi[buf][0][0]), "+v"(hi[buf][0][1]), "+v"(hi[buf][0][2]), "+v"(hi[buf][0][3]),
+                         "+v"(lo[buf][1][0]), "+v"(lo[buf][1][1]), "+v"(lo[buf][1][2]), "+v"(lo[buf][1][3]),
+                         "+v"(hi[buf][1][0]), "+v"(hi[buf][1][1]), "+v"(hi[buf][1][2]), "+v"(hi[buf][1][3])::"memory");
+        };
+        // blocks 0 and 1 (nothing of this loop issued yet)
+        if (lt > 0) rb_vm<(NBLK - 2) + 8 + 8>();
+        else rb_vm<(NBLK - 2) + 8>();
+        rb_barrier();
+        reads2(0, 0);
+        lgkm2(0);
+        auto pair = [&](auto jc) __attribute__((always_inline)) {
+          constexpr int j = decltype(jc)::value;
+          constexpr int cur = j & 1, nxt = cur ^ 1;
+          if constexpr (2 * j + 3 < NBLK) {
+            // block 2j + 3 landed: refills so far 2j (this tile's slots 0 .. 2j - 1)
+            constexpr int later = NBLK - 1 - (2 * j + 3);
+            if (lt > 0) {
+              if (more) rb_vm<later + 8 + 8 + 2 * j>();
+              else rb_vm<later + 8 + 8>();
+            } else {
+              if (more) rb_vm<later + 8 + 2 * j>();
+              else rb_vm<later + 8>();
+            }
+            rb_barrier();  // blocks 2j + 2, 2j + 3 landed everywhere; 2j, 2j + 1 read by all
+            if (more) {
+              xdma(lt + 1, 2 * j);
+              xdma(lt + 1, 2 * j + 1);
+            }
+            reads2(2 * j + 2, nxt);
+          }
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+              const wg_u4 fx = {lo[cur][sb][y].x, lo[cur][sb][y].y, hi[cur][sb][y].x, hi[cur][sb][y].y};
+#pragma unroll
+              for (int xm = 0; xm < 2; ++xm)
+                acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(wg_bf16x8, zf[2 * j + sb][xm]), __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
+                    0, 0, 0);
+            }
+          if constexpr (2 * j + 3 < NBLK) lgkm2(nxt);
+        };
+        rb_for<0, NBLK / 2>(pair);
+        // this tile's W words: only the refills of slots 0 .. NBLK - 3 are younger
+        if (more) rb_vm<NBLK - 2>();
+        else rb_vm<0>();
+      } else {
       wg_u2 lo[2][4], hi[2][4];
       auto reads = [&](int b, int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -925,9 +997,10 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         if constexpr (b + 1 < NBLK) lgkm(nxt);
       };
       rb_for<0, NBLK>(block);
-      // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
       if (more) rb_vm<NBLK - 1>();  // this tile's W words (only the refills are younger)
       else rb_vm<0>();
+      }
+      // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
 #pragma unroll
       for (int xm = 0; xm < 2; ++xm)
 #pragma unroll
@@ -936,8 +1009,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           for (int r = 0; r < 4; ++r)
             rb_dsw32(tileb + ((32 * w + 16 * xm + 4 * g + r) * kRbPitch + 16 * y + i) * 4, acc[xm][y][r] * a.alpha);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      rb_barrier();  // the tile is whole; every wave has read the last block
-      if (more) xdma(lt + 1, nblk - 1);
+      rb_barrier();  // the tile is whole; every wave has read the last block(s)
+      if (more) {
+        if constexpr (kRbPair && NBLK >= 4) xdma(lt + 1, nblk - 2);
+        xdma(lt + 1, nblk - 1);
+      }
       wg_u4 gv[4][2];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
