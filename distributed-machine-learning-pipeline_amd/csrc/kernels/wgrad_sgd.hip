@@ -62,18 +62,25 @@ __device__ __forceinline__ void hl_join8(uint4 h, uint4 l, float (&w)[8]) {
     w[2 * i + 1] = hl_join(hw[i] >> 16, lw[i] >> 16);
   }
 }
-__device__ __forceinline__ void hl_store8(const WgArgs& a, int nr, int kc, const float (&w)[8]) {
-  uint32_t hw[4], lw[4];
+__device__ __forceinline__ void hl_pack8(const float (&w)[8], uint32_t (&hw)[4], uint32_t (&lw)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint32_t h0 = hl_hi(w[2 * i]), h1 = hl_hi(w[2 * i + 1]);
     hw[i] = h0 | (h1 << 16);
     lw[i] = hl_lo(w[2 * i], h0) | (hl_lo(w[2 * i + 1], h1) << 16);
   }
+}
+__device__ __forceinline__ void hl_put8(const WgArgs& a, int nr, int kc, const uint32_t (&hw)[4],
+                                        const uint32_t (&lw)[4]) {
   __builtin_nontemporal_store(wg_u4{hw[0], hw[1], hw[2], hw[3]},
                               reinterpret_cast<wg_u4*>(a.Wb + (int64_t)nr * a.ldwb + kc));
   __builtin_nontemporal_store(wg_u4{lw[0], lw[1], lw[2], lw[3]},
                               reinterpret_cast<wg_u4*>(a.Wl + (int64_t)nr * a.ldwl + kc));
+}
+__device__ __forceinline__ void hl_store8(const WgArgs& a, int nr, int kc, const float (&w)[8]) {
+  uint32_t hw[4], lw[4];
+  hl_pack8(w, hw, lw);
+  hl_put8(a, nr, kc, hw, lw);
 }
 
 // Several layers' weight gradients in ONE launch (flattened tile grid): the
@@ -101,6 +108,7 @@ __device__ __forceinline__ uint4 wg_frag(const char* img, int m0, int c0, int la
   return make_uint4(l2.x, l2.y, h2.x, h2.y);
 }
 
+constexpr int kWgOob = 0x7ffffff0;  // byte offset of a dropped store: past every bound (host check)
 constexpr int kWgLds = 64 * kWgPitch * 4;  // two operand images (16 KiB), later the fp32 tile (17 KiB)
 static_assert(kWgLds >= 2 * kWgImg, "LDS carve");
 // + the bias gradient's 4 row-group partials per column ([4][64] floats)
@@ -258,17 +266,34 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
   if (a.Wl) {  // split master: 8 consecutive weights per 16-B word
     const int kc8 = k0 + 8 * (tid & 7);
     if (kc8 < a.K) {
+      // both row halves packed first, the four stores issued together at the
+      // end: a store between them made the compiler wait vmcnt(0) (its data
+      // registers reused by the second half) -- a store round trip per tile
+      uint32_t hw[2][4], lw[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int rr = (tid >> 3) + 32 * j, nr = n0 + rr;
-        if (nr >= a.N) continue;
+        const int rr = (tid >> 3) + 32 * j;
         const float4 g0 = *reinterpret_cast<const float4*>(tile + rr * kWgPitch + 8 * (tid & 7));
         const float4 g1 = *reinterpret_cast<const float4*>(tile + rr * kWgPitch + 8 * (tid & 7) + 4);
         float w[8];
         hl_join8(wr[2 * j], wr[2 * j + 1], w);
         w[0] -= a.lr * g0.x; w[1] -= a.lr * g0.y; w[2] -= a.lr * g0.z; w[3] -= a.lr * g0.w;
         w[4] -= a.lr * g1.x; w[5] -= a.lr * g1.y; w[6] -= a.lr * g1.z; w[7] -= a.lr * g1.w;
-        hl_store8(a, nr, kc8, w);
+        hl_pack8(w, hw[j], lw[j]);
+      }
+      // unpredicated buffer stores (rows past N: an offset past the bound,
+      // dropped) -- a predicated store let the compiler sink the second
+      // half's arithmetic behind the first store again
+      const __amdgpu_buffer_rsrc_t rwb = __builtin_amdgcn_make_buffer_rsrc(a.Wb, (short)0, (int)(a.N * a.ldwb * 2), 0x00020000);
+      const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc(a.Wl, (short)0, (int)(a.N * a.ldwl * 2), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int nr = n0 + (tid >> 3) + 32 * j;
+        const bool ok = nr < a.N;
+        __builtin_amdgcn_raw_buffer_store_b128(wg_u4{hw[j][0], hw[j][1], hw[j][2], hw[j][3]}, rwb,
+                                               ok ? (int)((nr * a.ldwb + kc8) * 2) : kWgOob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(wg_u4{lw[j][0], lw[j][1], lw[j][2], lw[j][3]}, rwl,
+                                               ok ? (int)((nr * a.ldwl + kc8) * 2) : kWgOob, 0, 0);
       }
     }
   }
@@ -1062,8 +1087,8 @@ bool wg_valid(const WgArgs& a) {
   // split master: the current hi words in, the next step's hi copy and lo (in place) out
   if (a.Wl && (a.W || a.Wh == nullptr || a.Wb == nullptr || (a.K & 7) ||
                (((uintptr_t)a.Wh | (uintptr_t)a.Wl | (uintptr_t)a.Wb) & 15) || (a.ldwh & 7) || (a.ldwl & 7) ||
-               (a.ldwb & 7)))
-    return false;
+               (a.ldwb & 7) || (int64_t)a.N * a.ldwb * 2 + 16 > kWgOob || (int64_t)a.N * a.ldwl * 2 + 16 > kWgOob))
+    return false;  // (the tile epilogue's buffer stores: dropped rows sit past both bounds)
   if ((a.W && (((uintptr_t)a.W & 15) || (a.ldw & 3))) || (a.Wb && (((uintptr_t)a.Wb & 7) || (a.ldwb & 3))) ||
       (a.G && (((uintptr_t)a.G & 15) || (a.ldg & 3))))
     return false;
