@@ -250,6 +250,11 @@ struct PyComm {
   }
 };
 
+RcclComm* live(PyComm& s) {
+  if (!s.c) throw std::runtime_error("RcclComm used after destroy()");
+  return s.c.get();
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -991,53 +996,57 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<PyComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int, bool>(), py::arg("uid"), py::arg("rank"),
            py::arg("nranks"), py::arg("device"), py::arg("blocking") = true)
-      .def_property_readonly("rank", [](PyComm& s) { return s.c->rank(); })
-      .def_property_readonly("nranks", [](PyComm& s) { return s.c->nranks(); })
+      .def_property_readonly("rank", [](PyComm& s) { return live(s)->rank(); })
+      .def_property_readonly("nranks", [](PyComm& s) { return live(s)->nranks(); })
       .def("allreduce_", [](PyComm& s, torch::Tensor t, int op) {
         check_cuda(t, "t");
-        s.c->allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, cur_stream());
+        live(s)->allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, cur_stream());
       }, py::arg("t"), py::arg("op") = 0)
       .def("ring_allreduce_", [](PyComm& s, torch::Tensor t, int op, int64_t chunk_bytes,
                                  int max_rings, int pipe) {
         check_cuda(t, "t");
         TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "tensor must be 16 B aligned");
-        s.c->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream(),
+        live(s)->ring_allreduce(t.data_ptr(), t.numel(), dtype_of(t), op, chunk_bytes, cur_stream(),
                             max_rings, pipe);
       }, py::arg("t"), py::arg("op") = 0, py::arg("chunk_bytes") = 1 << 20,
          py::arg("max_rings") = 0, py::arg("pipe") = -1,
          "pipe: 1 pipelined schedule, 0 single-stream, -1 the communicator's default")
-      .def("set_ring_pipeline", [](PyComm& s, int mode) { s.c->set_ring_pipeline(mode); }, py::arg("mode"))
-      .def_property_readonly("ring_pipeline", [](PyComm& s) { return s.c->pipeline_mode(); })
+      .def("set_ring_pipeline", [](PyComm& s, int mode) { live(s)->set_ring_pipeline(mode); }, py::arg("mode"))
+      .def_property_readonly("ring_pipeline", [](PyComm& s) { return live(s)->pipeline_mode(); })
       .def("reserve_ring", [](PyComm& s, int64_t count, int64_t chunk_bytes, int max_rings) {
-        s.c->reserve_ring(count, kF32, chunk_bytes, max_rings);
+        live(s)->reserve_ring(count, kF32, chunk_bytes, max_rings);
       }, py::arg("count"), py::arg("chunk_bytes") = 1 << 20, py::arg("max_rings") = 0,
          "size the fp32 ring all-reduce scratch for `count` elements up front")
       .def("broadcast_", [](PyComm& s, torch::Tensor t, int root) {
         check_cuda(t, "t");
-        s.c->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());
+        live(s)->broadcast(t.data_ptr(), t.numel(), dtype_of(t), root, cur_stream());
       })
       .def("allgather_", [](PyComm& s, torch::Tensor t) {
         check_cuda(t, "t");
-        TORCH_CHECK(t.is_contiguous() && t.numel() % s.c->nranks() == 0,
+        TORCH_CHECK(t.is_contiguous() && t.numel() % live(s)->nranks() == 0,
                     "allgather_: contiguous, nranks equal parts");
-        s.c->allgather(t.data_ptr(), t.numel() / s.c->nranks(), dtype_of(t), cur_stream());
+        live(s)->allgather(t.data_ptr(), t.numel() / live(s)->nranks(), dtype_of(t), cur_stream());
       }, py::arg("t"), "in-place all-gather: rank r contributes part r of t")
       .def("send", [](PyComm& s, torch::Tensor t, int peer) {
         check_cuda(t, "t");
-        s.c->send(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
+        live(s)->send(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
       })
       .def("recv_", [](PyComm& s, torch::Tensor t, int peer) {
         check_cuda(t, "t");
-        s.c->recv(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
+        live(s)->recv(t.data_ptr(), t.numel(), dtype_of(t), peer, cur_stream());
       })
       .def("barrier", [](PyComm& s) {
         hipStream_t st = cur_stream();
         py::gil_scoped_release nogil;
-        s.c->barrier(st);
+        live(s)->barrier(st);
       })
-      .def("abort", [](PyComm& s) { s.c->abort(); })
-      .def("async_error", [](PyComm& s) { return s.c->async_error(); })
-      .def_property_readonly("aborted", [](PyComm& s) { return s.c->aborted(); });
+      .def("abort", [](PyComm& s) { if (s.c) s.c->abort(); })
+      .def("destroy", [](PyComm& s) {
+        py::gil_scoped_release nogil;  // ncclCommDestroy (or the aborted comm's buffers) freed now
+        s.c.reset();
+      }, "free the communicator now (a destroyed comm raises on any further use)")
+      .def("async_error", [](PyComm& s) { return s.c ? s.c->async_error() : std::string("aborted"); })
+      .def_property_readonly("aborted", [](PyComm& s) { return !s.c || s.c->aborted(); });
 
   // ---- device runtime (arena / copy engine / stream table) ------------------
   py::class_<DeviceArena>(m, "DeviceArena")

@@ -99,6 +99,17 @@ class DistContext:
         self.all_reduce_(t, op)
         return [float(v) for v in t.tolist()]
 
+    def host_agree(self, key: str, ok: bool) -> bool:
+        """Collective AND of `ok` over the ranks through the TCP store only: no
+        device tensor, no stream, no synchronize -- so it cannot queue behind
+        a hung kernel on this rank's GPU (the agreement after a bounded wait
+        must not block on the very work it bounded)."""
+        if not self.is_distributed:
+            return bool(ok)
+        self._agree_calls = getattr(self, "_agree_calls", 0) + 1
+        vals = self.all_gather_bytes(f"hipdsml/agree/{key}/{self._agree_calls}", b"1" if ok else b"0")
+        return all(v == b"1" for v in vals)
+
     def barrier(self) -> None:
         if self.is_distributed:
             with self.guard("barrier"):
@@ -165,14 +176,16 @@ def rccl_blocking_default() -> bool:
     return os.environ.get("HIPDSML_RCCL_NONBLOCKING", "0") != "1"
 
 
-def make_native_comm(ctx: DistContext, blocking: Optional[bool] = None):
+def make_native_comm(ctx: DistContext, blocking: Optional[bool] = None, watch: bool = True):
     """Bootstrap a native RCCL communicator over the process group's store.
 
     Blocking by default (:func:`rccl_blocking_default`).  Either way the
     context's watchdog polls the communicator's async error and, on a fault or a
     stalled guarded section, aborts it from its own thread (``ncclCommAbort`` is
     legal on a blocking communicator while another thread waits in RCCL), so a
-    dead peer ends the job instead of hanging it (parallel/watchdog.py)."""
+    dead peer ends the job instead of hanging it (parallel/watchdog.py).
+    ``watch=False`` leaves it unregistered (a throwaway probe communicator the
+    caller aborts and destroys itself)."""
     if blocking is None:
         blocking = rccl_blocking_default()
     from ..ops.native import require_native
@@ -185,6 +198,6 @@ def make_native_comm(ctx: DistContext, blocking: Optional[bool] = None):
     uid = ctx.share_bytes(key, uid)
     with ctx.guard("ncclCommInitRank"):
         comm = C.RcclComm(uid, ctx.rank, ctx.world_size, ctx.device.index, blocking)
-    if ctx.watchdog is not None:
+    if watch and ctx.watchdog is not None:
         ctx.watchdog.watch_comm(comm)
     return comm

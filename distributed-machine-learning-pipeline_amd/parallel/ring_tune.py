@@ -99,7 +99,12 @@ def validate_pipelined(run: Callable[[], None], done: Callable[[], bool], agree:
     enqueues it, `done` polls its completion, `agree` ANDs a flag over the
     ranks, `abort` kills the communicator it ran on (a throwaway one: a hang
     never reaches the job's communicator).  Returns '' or the error, agreed
-    on every rank -- a timeout or an exception is reported, never a hang."""
+    on every rank -- a timeout or an exception is reported, never a hang.
+
+    A rank that timed out aborts its probe BEFORE it takes part in the
+    agreement, and `agree` must be host-only (parallel/dist.py host_agree):
+    an agreement that needed this rank's GPU would queue behind the hung
+    ring and never return."""
     err = ""
     try:
         run()
@@ -111,18 +116,38 @@ def validate_pipelined(run: Callable[[], None], done: Callable[[], bool], agree:
             sleep(0.001)
     except Exception as e:  # noqa: BLE001
         err = f"{type(e).__name__}: {e}"[:200]
+    aborted = False
+    if err:
+        aborted = True
+        _quiet(abort)
     ok = agree(not err)
     if not ok:
-        try:
-            abort()
-        except Exception:  # noqa: BLE001 pragma: no cover
-            pass
+        if not aborted:
+            _quiet(abort)  # a peer failed: its half of the ring never completes
         return err or "pipelined ring failed on a peer"
     return ""
 
 
+def _quiet(fn: Callable[[], None]) -> None:
+    try:
+        fn()
+    except Exception:  # noqa: BLE001 pragma: no cover
+        pass
+
+
+def pipeline_default() -> bool:
+    """Whether the tuner times the pipelined ring schedule at all: off unless
+    HIPDSML_RING_PIPELINE=1, until a multi-GPU run has recorded a pipelined
+    sweep (``sweep_pipelined_us``) -- one-GPU boxes cannot run RCCL at
+    nranks > 1, so the schedule is validated only by the FIFO simulation in
+    tests/test_ring_plan.py so far."""
+    import os
+
+    return os.environ.get("HIPDSML_RING_PIPELINE", "0") == "1"
+
+
 def tune_ring_chunk(ctx, comm, t, chunks: Iterable[int] = CHUNKS, iters: int = 20,
-                    max_rings: int = 0, pipeline: bool = True,
+                    max_rings: int = 0, pipeline: Optional[bool] = None,
                     probe_timeout_s: float = 10.0) -> Dict[str, object]:
     """Collective: sweep the chunk of ``comm.ring_allreduce_`` on tensor `t`
     (restored afterwards) over the distinct candidates, for the single-stream
@@ -137,6 +162,8 @@ def tune_ring_chunk(ctx, comm, t, chunks: Iterable[int] = CHUNKS, iters: int = 2
     "sweep_pipelined_us": {bytes: us} | None[, "ring_pipe_error": str]}``."""
     import torch
 
+    if pipeline is None:
+        pipeline = pipeline_default()
     nbytes = t.numel() * t.element_size()
     rings = len(_directed_rings(ctx.world_size, max_rings))
     cands = distinct_chunks(nbytes, ctx.world_size, rings, chunks)
@@ -172,38 +199,52 @@ def tune_ring_chunk(ctx, comm, t, chunks: Iterable[int] = CHUNKS, iters: int = 2
 
 
 def _probe_pipelined(ctx, t, src, chunk: int, max_rings: int, timeout_s: float) -> str:
-    """The pipelined ring once, on a throwaway RCCL communicator, bounded, and
-    checked bit-exact against the single-stream ring on the same input."""
+    """The pipelined ring once, on a throwaway RCCL communicator and its own
+    stream, bounded, and checked bit-exact against the single-stream ring on
+    the same input.  The probe is never registered with the watchdog and is
+    destroyed on every path (it used to stay alive, polled, next to
+    the job's communicator); every agreement goes through the TCP store, so a
+    hung probe cannot block it."""
     import torch
 
     from .dist import make_native_comm
 
     try:
-        probe = make_native_comm(ctx)
+        probe = make_native_comm(ctx, watch=False)
     except Exception as e:  # noqa: BLE001 -- collective init failed: no pipelined candidate
         return f"probe communicator: {type(e).__name__}: {e}"[:200]
+    side = torch.cuda.Stream(device=t.device)
+    side.wait_stream(torch.cuda.current_stream(t.device))
     want = src.clone()
     got = src.clone()
-    probe.reserve_ring(t.numel(), chunk, max_rings)
-    probe.ring_allreduce_(want, 0, chunk, max_rings, 0)
-    torch.cuda.synchronize(t.device)
     ev = torch.cuda.Event()
+    agree = lambda ok: ctx.host_agree("ring_pipe_probe", ok)  # noqa: E731
+    try:
+        with torch.cuda.stream(side):
+            probe.reserve_ring(t.numel(), chunk, max_rings)
+            probe.ring_allreduce_(want, 0, chunk, max_rings, 0)
+            ev.record()
+        poll = ev.query
+        # the single-stream reference ring, bounded the same way
+        err = validate_pipelined(lambda: None, poll, agree, probe.abort, timeout_s)
+        if err:
+            return "single-stream probe: " + err
 
-    def run():
-        probe.ring_allreduce_(got, 0, chunk, max_rings, 1)
-        ev.record()
+        def run():
+            with torch.cuda.stream(side):
+                probe.ring_allreduce_(got, 0, chunk, max_rings, 1)
+                ev.record()
 
-    err = validate_pipelined(run, ev.query, lambda ok: ctx.all_reduce_scalars(1.0 if ok else 0.0,
-                                                                             op="min")[0] > 0,
-                             probe.abort, timeout_s)
-    if err:
-        return err
-    torch.cuda.synchronize(t.device)
-    same = bool(torch.equal(want, got))
-    if ctx.all_reduce_scalars(1.0 if same else 0.0, op="min")[0] < 1:
-        return "pipelined ring result differs from the single-stream ring"
-    del probe
-    return ""
+        err = validate_pipelined(run, poll, agree, probe.abort, timeout_s)
+        if err:
+            return err
+        side.synchronize()  # both rings completed on every rank
+        if not agree(bool(torch.equal(want, got))):
+            return "pipelined ring result differs from the single-stream ring"
+        return ""
+    finally:
+        _quiet(probe.destroy)
+        del probe
 
 
 def _directed_rings(n: int, max_rings: int):

@@ -74,6 +74,11 @@ class Watchdog:
         with self._lock:
             self._comms.append(comm)
 
+    def unwatch_comm(self, comm) -> None:
+        """Stop polling / aborting `comm` (before it is destroyed)."""
+        with self._lock:
+            self._comms = [c for c in self._comms if c is not comm]
+
     def on_fault(self, fn: Callable[[], None]) -> None:
         """Extra abort action (e.g. a process-group abort)."""
         with self._lock:

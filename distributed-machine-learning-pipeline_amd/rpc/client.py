@@ -46,6 +46,22 @@ def _align(x: int, a: int = 256) -> int:
     return (x + a - 1) // a * a
 
 
+def auto_backend(mds, addrs) -> str:
+    """CommInit backend for `train_device_mode`: GPU device servers on ONE
+    node (by the hostnames they report, not by the form of their addresses: a
+    same-node server reached by LAN IP is still node-local) join a process
+    group on the coordinator's store ("pg": the xGMI exchange candidates need
+    it); servers spread over nodes take the RCCL bootstrap, whose id travels
+    over gRPC ("rccl"); host (CPU) servers use the gRPC ring ("rpc").  Servers
+    too old to report a host fall back to the address test."""
+    if len(mds) < 2 or {m.backend for m in mds} != {"hip"}:
+        return "rpc"
+    hosts = [m.host for m in mds]
+    if all(hosts):
+        return "pg" if len(set(hosts)) == 1 else "rccl"
+    return "pg" if all(is_loopback(a) for a in addrs) else "rccl"
+
+
 class TrainingClient:
     def __init__(self, coordinator: str, devices: List[str], dims=(784, 128, 64, 10), batch: int = 64,
                  lr: float = 0.01, seed: int = 0, timeout: float = 600.0, out=print):
@@ -90,12 +106,9 @@ class TrainingClient:
         # host (CPU) device servers: the device-driven gRPC ring (DeviceAllReduce's
         # transfers), or a gloo group with backend="pg"
         if backend == "auto":
-            backends = {s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata.backend
-                        for s in self.devs}
-            # the process group meets on a store the coordinator hosts; devices on
-            # other hosts take the RCCL bootstrap, whose id travels over gRPC
-            remote = not all(is_loopback(a) for a in self.dev_addrs)
-            backend = ("rccl" if remote else "pg") if n > 1 and backends == {"hip"} else "rpc"
+            mds = [s.GetDeviceMetadata(pb.GetDeviceMetadataRequest(), timeout=self.timeout).metadata
+                   for s in self.devs]
+            backend = auto_backend(mds, self.dev_addrs)
         self.comm_init(backend)
 
         def cfg(i, s):

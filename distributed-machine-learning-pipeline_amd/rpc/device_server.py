@@ -9,6 +9,7 @@ communicator and run collectives / whole training steps on the GPU.
 """
 from __future__ import annotations
 
+import socket as _socket
 import json
 import logging
 import threading
@@ -119,7 +120,8 @@ class GPUDeviceServicer:
         md = pb.DeviceMetadata(deviceId=pb.DeviceId(value=self.dev.device_id),
                                minMemAddr=pb.MemAddr(value=self.dev.min_addr),
                                maxMemAddr=pb.MemAddr(value=self.dev.max_addr),
-                               name=self.name, backend=self.dev.backend)
+                               name=self.name, backend=self.dev.backend,
+                               host=_socket.gethostname())
         return pb.GetDeviceMetadataResponse(metadata=md)
 
     def BeginSend(self, request, context):

@@ -58,7 +58,8 @@ MESSAGES: M = {
     "DeviceMetadata": [("deviceId", 1, ".DeviceId"), ("minMemAddr", 2, ".MemAddr"),
                        ("maxMemAddr", 3, ".MemAddr"),
                        # extension
-                       ("name", 4, "string"), ("backend", 5, "string")],
+                       ("name", 4, "string"), ("backend", 5, "string"),
+                       ("host", 6, "string")],  # the server's hostname (node identity)
     # -- device ------------------------------------------------------------
     "GetDeviceMetadataRequest": [],
     "GetDeviceMetadataResponse": [("metadata", 1, ".DeviceMetadata")],

@@ -90,3 +90,21 @@ def test_device_mode_host_data_parallel_matches_reference():
     assert (got[0] - P).abs().max().item() < 1e-5
     assert res["steps_per_epoch"] == spe
     assert lines[1].startswith("Epoch 1 complete") and lines[-1].startswith("Final Test Accuracy:")
+
+
+def test_auto_backend_decides_by_host_identity():
+    """same-node GPU servers reached by LAN IP keep the 'pg' group
+    (and the xGMI candidates); servers on different hosts take 'rccl'."""
+    from hipdsml.rpc.client import auto_backend
+    from hipdsml.rpc.proto import pb
+
+    def md(host, backend="hip"):
+        return pb.DeviceMetadata(backend=backend, host=host)
+
+    lan = ["10.0.0.5:5003", "10.0.0.5:5004"]
+    assert auto_backend([md("nodeA"), md("nodeA")], lan) == "pg"
+    assert auto_backend([md("nodeA"), md("nodeB")], ["127.0.0.1:1", "127.0.0.1:2"]) == "rccl"
+    assert auto_backend([md(""), md("")], lan) == "rccl"            # no host reported: address test
+    assert auto_backend([md(""), md("")], ["127.0.0.1:1", "localhost:2"]) == "pg"
+    assert auto_backend([md("a", "host"), md("a", "host")], lan) == "rpc"
+    assert auto_backend([md("a")], lan) == "rpc"

@@ -107,3 +107,77 @@ def test_validate_pipelined_agrees_across_ranks():
         raise RuntimeError("ncclGroupEnd: unhandled error")
 
     assert "ncclGroupEnd" in rt.validate_pipelined(boom, lambda: True, lambda ok: ok, lambda: None)
+
+
+def test_validate_pipelined_aborts_before_agreeing_on_a_local_timeout():
+    """a rank whose probe timed out must abort it BEFORE
+    the agreement -- an agreement that needed the GPU would queue behind the
+    hung ring.  The order of the two calls is the contract."""
+    clock = Clock()
+    order = []
+
+    def sleep(dt):
+        clock.t += dt
+
+    def agree(ok):
+        order.append(("agree", ok))
+        return ok
+
+    err = rt.validate_pipelined(lambda: None, lambda: False, agree, lambda: order.append(("abort",)),
+                                timeout_s=1.0, clock=clock, sleep=sleep)
+    assert "did not complete" in err
+    assert order == [("abort",), ("agree", False)]
+
+
+def test_pipelined_schedule_is_opt_in(monkeypatch):
+    monkeypatch.delenv("HIPDSML_RING_PIPELINE", raising=False)
+    assert rt.pipeline_default() is False
+    monkeypatch.setenv("HIPDSML_RING_PIPELINE", "1")
+    assert rt.pipeline_default() is True
+
+
+def test_watchdog_unwatch_comm():
+    from hipdsml.parallel.watchdog import Watchdog
+
+    class C:
+        aborted = 0
+
+        def async_error(self):
+            return ""
+
+        def abort(self):
+            self.aborted += 1
+
+    wd = Watchdog(timeout=60, interval=0.01, exit_on_stuck=False)
+    a, b = C(), C()
+    wd.watch_comm(a)
+    wd.watch_comm(b)
+    wd.unwatch_comm(b)
+    wd.declare("test fault")
+    wd.stop()
+    assert a.aborted == 1 and b.aborted == 0
+
+
+def _agree_worker(rank, world, port, votes, outdir):
+    import os
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from hipdsml.parallel.dist import DistContext
+
+    ctx = DistContext.from_env(device="cpu", watchdog_s=0)
+    res = [ctx.host_agree("t", v[rank]) for v in votes]
+    with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
+        f.write(",".join("1" if r else "0" for r in res))
+    ctx.destroy()
+
+
+def test_host_agree_is_a_store_only_and(tmp_path):
+    """The probe's agreement runs on the TCP store (no device tensor): an AND
+    over ranks, repeated calls independent."""
+    from spawn_util import spawn_group
+
+    votes = [(True, True, True), (True, False, True), (False, False, False), (True, True, True)]
+    spawn_group(_agree_worker, 3, lambda port: (3, port, votes, str(tmp_path)))
+    got = [(tmp_path / f"r{r}.txt").read_text() for r in range(3)]
+    assert got == ["1,0,0,1"] * 3
