@@ -6,7 +6,15 @@ linked with the PyTorch binding TU into ``<package>/_C.so``, which travels to
 the GPU box with the repository snapshot.  Objects are rebuilt when their
 source or any header under ``csrc/`` is newer.
 
-Usage:  python -m hipdsml._build [--force] [-j N]
+Usage:  python -m hipdsml._build [--force] [-j N] [--measure]
+
+``--measure`` makes a measurement build (-DHIPDSML_MEASURE, objects under
+``build/obj_measure``): the profiling knobs of csrc/kernels/common.h
+``DSML_MEASURE_KNOB`` (traffic-dropping, grid-growing) become live and
+``_C.measure_build`` is True.  Tools that need them build it, measure, and
+run the default build again; every default build relinks the production
+module (the flavor of the last link is recorded next to the objects), and the
+GPU tests refuse to run on a measurement build.
 """
 from __future__ import annotations
 
@@ -63,14 +71,20 @@ def _compile(src: Path, obj: Path, flags: list[str]) -> tuple[Path, str]:
     return obj, p.stderr
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
+          measure: bool = False) -> Path:
     kernels, runtime, binding = _sources()
-    OBJ.mkdir(parents=True, exist_ok=True)
+    obj_dir = OBJ.parent / "obj_measure" if measure else OBJ
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    flavor = "measure" if measure else "production"
+    stamp = OBJ.parent / "linked_flavor"
+    relink = not stamp.exists() or stamp.read_text().strip() != flavor
     inc, lib, abi = _torch_paths()
+    extra = ["-DHIPDSML_MEASURE"] if measure else []
     base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(CSRC),
-            "-Wno-unused-result", "-Wno-pass-failed"]
+            "-Wno-unused-result", "-Wno-pass-failed"] + extra
     host_only = ["-O3", "-std=c++17", "-fPIC", "-I", str(CSRC), "-D__HIP_PLATFORM_AMD__=1",
-                 "-Wno-unused-result"]
+                 "-Wno-unused-result"] + extra
     torch_flags = host_only + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
                                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                                "-I", sysconfig.get_paths()["include"]]
@@ -80,14 +94,14 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     jobs_todo = []
     objs = []
     for src in kernels:
-        obj = OBJ / (src.stem + ".hip.o")
+        obj = obj_dir / (src.stem + ".hip.o")
         objs.append(obj)
         jobs_todo.append((src, obj, base))
     for src in runtime:
-        obj = OBJ / (src.stem + ".cpp.o")
+        obj = obj_dir / (src.stem + ".cpp.o")
         objs.append(obj)
         jobs_todo.append((src, obj, base))
-    obj_b = OBJ / "bindings.o"
+    obj_b = obj_dir / "bindings.o"
     objs.append(obj_b)
     jobs_todo.append((binding, obj_b, torch_flags))
 
@@ -102,7 +116,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
                     if err.strip():
                         print(err, file=sys.stderr)
     newest = max(o.stat().st_mtime for o in objs)
-    if force or stale or not OUT.exists() or OUT.stat().st_mtime < newest:
+    if force or stale or relink or not OUT.exists() or OUT.stat().st_mtime < newest:
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(OUT)]
         link += [str(o) for o in objs]
         for p in lib:
@@ -112,6 +126,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         p = subprocess.run(link, capture_output=True, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(link)}\n{p.stdout}\n{p.stderr}")
+        stamp.write_text(flavor)
     return OUT
 
 
@@ -119,8 +134,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--measure", action="store_true",
+                    help="measurement build (-DHIPDSML_MEASURE): profiling knobs live; tools only")
     a = ap.parse_args()
-    out = build(force=a.force, jobs=a.j, verbose=True)
+    out = build(force=a.force, jobs=a.j, verbose=True, measure=a.measure)
     print(out)
 
 

@@ -607,7 +607,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return v;
   });
   m.def("head_set_stamping", &head_set_stamping);
+#ifdef HIPDSML_MEASURE
   m.def("head_set_debug", &head_set_debug);
+#endif
+#ifdef HIPDSML_MEASURE
+  m.attr("measure_build") = true;
+#else
+  m.attr("measure_build") = false;
+#endif
   // one layer of the fused weight-gradient launches:
   // (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl]); tensors may be None
   auto wg_layer = [bf16p](py::handle it) -> WgLayer {

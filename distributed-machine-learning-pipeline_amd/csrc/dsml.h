@@ -340,7 +340,9 @@ constexpr int kWgRowBlkTile = 256;
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
+#ifdef HIPDSML_MEASURE
 void head_set_debug(int v);
+#endif
 hipError_t rowsum_bf16(const uint16_t* X, int64_t ld, int N, int cols, float* out, float* bias,
                        float lr, hipStream_t s);
 hipError_t sgd_cast(float* W, const float* G, int N, int K, float lr, uint16_t* Wb, int64_t ldw,

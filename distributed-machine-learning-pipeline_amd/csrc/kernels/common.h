@@ -9,6 +9,17 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+// Measurement-only knobs (drop a phase's memory traffic, grow a grid, ...) exist
+// only in a measurement build (`python -m hipdsml._build --measure` adds
+// -DHIPDSML_MEASURE; tools/ profiles them).  A production build -- every build
+// _build.py and __graft_entry__ make by default -- folds them to constant 0,
+// so no environment variable can change what a training kernel computes.
+#ifdef HIPDSML_MEASURE
+#define DSML_MEASURE_KNOB(x) (x)
+#else
+#define DSML_MEASURE_KNOB(x) 0
+#endif
+
 namespace dsml {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -783,14 +783,20 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 // replaces a K-long, N = C GEMM (one tile: no parallelism) + the softmax launch.
 __device__ uint64_t g_head_stamps[64][6];
 __constant__ int g_head_stamp_on;  // __constant__: scalar loads, no vector wait ahead of the batch
-__constant__ int g_head_dbg;  // profiling only: bit 0 skips the stats atomics, bit 1 the dzp phase
+#ifdef HIPDSML_MEASURE
+__constant__ int g_head_dbg;  // measurement builds: bit 0 skips the stats atomics, bit 1 the dzp phase
+#endif
 // MAXC: the class count rounded up to an instantiated size (even: class pairs)
 template <int MAXC>
 __global__ __launch_bounds__(256) void head_softmax_xent_k(HeadRow h) {
   __shared__ float part[MAXC][17];     // [class][wave * 4 + 16-lane row] partial sums (+1: pad)
   __shared__ uint32_t gz2[MAXC / 2];   // bf16-rounded dLogits of this row, class pairs
   const int m = blockIdx.x;
+#ifdef HIPDSML_MEASURE
   h.dbg = g_head_dbg;
+#else
+  h.dbg = 0;
+#endif
   head_row<MAXC>(h, m, part, gz2, (g_head_stamp_on && m < 64) ? g_head_stamps[m] : nullptr);
 }
 
@@ -798,10 +804,12 @@ hipError_t head_read_stamps(uint64_t* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_head_stamps), sizeof(uint64_t) * 64 * 6, 0,
                              hipMemcpyDeviceToHost);
 }
+#ifdef HIPDSML_MEASURE
 void head_set_debug(int v) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dbg), &v, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
+#endif
 void head_set_stamping(bool on) {
   const int v = on ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);

@@ -40,7 +40,7 @@ struct HeadRow {
   uint16_t* dzpT;  // nullable
   int64_t ldpt;
   int row_stats;
-  int dbg;  // profiling only: bit 0 skips the stats, bit 1 the dzp phase
+  int dbg;  // measurement builds only: bit 0 skips the stats, bit 1 the dzp phase
 };
 constexpr int kHeadMaxC = 16;  // classes the head supports (instantiated for <= 10 and <= 16)
 constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
@@ -68,7 +68,7 @@ __device__ __forceinline__ void head_row(const HeadRow& h, int m, float (*part)[
   const int64_t ldh = h.ldh, ldw = h.ldw, ldl = h.ldl, ldz = h.ldz, ldt = h.ldt, ldzp = h.ldzp, ldpt = h.ldpt;
   const uint16_t* W = h.W;
   const float* bias = h.bias;
-  const int K = h.K, C = h.C, Cp = h.Cp, row_stats = h.row_stats, dbg = h.dbg;
+  const int K = h.K, C = h.C, Cp = h.Cp, row_stats = h.row_stats, dbg = DSML_MEASURE_KNOB(h.dbg);
   const int32_t* labels = h.labels;
   const float inv_batch = h.inv_batch;
   float* logits = h.logits;

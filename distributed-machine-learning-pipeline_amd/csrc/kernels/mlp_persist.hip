@@ -3234,13 +3234,17 @@ static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {
     slots = per_cu * cus;
     attr = true;
   }
-  // HIPDSML_PK_GRID_EXTRA (measurement only): that many more idle workgroups
-  // (rounded to whole rows of 8, so the XCD map holds) -- prices the idle blocks
-  // the round-robin XCD placement forces on the single-replica grid
+  // HIPDSML_PK_GRID_EXTRA (measurement builds only): that many more idle
+  // workgroups (rounded to whole rows of 8, so the XCD map holds) -- prices the
+  // idle blocks the round-robin XCD placement forces on the single-replica grid
+#ifdef HIPDSML_MEASURE
   static const int extra = [] {
     const char* e = std::getenv("HIPDSML_PK_GRID_EXTRA");
     return e ? std::max(0, std::atoi(e)) / 8 * 8 : 0;
   }();
+#else
+  constexpr int extra = 0;
+#endif
   const int grid = pk_grid<NL>(MODE == 1, MODE == 3 ? a.helpers : 0, a.pushers != 0) + (MODE == 0 ? extra : 0);
   if (slots < grid) return hipErrorCooperativeLaunchTooLarge;
   hipLaunchKernelGGL((mlp_persist_k<NL, MODE>), dim3(grid), dim3(kThreads), lds, s, a);

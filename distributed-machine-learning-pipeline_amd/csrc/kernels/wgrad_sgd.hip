@@ -697,10 +697,12 @@ constexpr int kRbPitch = 68;                   // floats per row of the fp32 epi
 constexpr int kRbLds = kRbRing + kRbN * kRbPitch * 4;
 constexpr int kRbMaxM = 512;
 constexpr bool kRbAuto = true;                 // auto dispatch (tile 0) picks it at M >= 256
-#ifndef HIPDSML_RB_PAIR
-#define HIPDSML_RB_PAIR 1
+#if defined(HIPDSML_MEASURE) && defined(HIPDSML_RB_PAIR)
+constexpr bool kRbPair = HIPDSML_RB_PAIR != 0;  // measurement builds: the single-block A/B
+#else
+constexpr bool kRbPair = true;
 #endif
-constexpr bool kRbPair = HIPDSML_RB_PAIR != 0;  // two ring blocks per wait / barrier (NBLK >= 4)
+  // two ring blocks per wait / barrier (NBLK >= 4)
 constexpr int kRbOob = 0x7ffffff0;             // offset of a dropped word: past every bound (host check)
 
 struct WgRowBlk {
@@ -709,7 +711,7 @@ struct WgRowBlk {
   int ktiles[kWgMaxLayers];
   int n;
   int groups;  // workgroups: g owns units [g U / G, (g + 1) U / G)
-  int dbg;     // profiling only (HIPDSML_RB_DBG): bit 0/1/2 drop the W / Z / X traffic (same instructions)
+  int dbg;     // measurement builds only (HIPDSML_RB_DBG): bit 0/1/2 drop the W / Z / X traffic
 };
 
 // s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding:
@@ -820,7 +822,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)
               __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (wg_lptr)(rb_lds + cc * 8192 + (8 * w + 4 * jj) * 256), 16,
-                                                      (rb.dbg & 2) ? kRbOob : zv[jj] + (int)(32 * c * a.ldz * 2), 0, 0, 0);
+                                                      (DSML_MEASURE_KNOB(rb.dbg) & 2) ? kRbOob : zv[jj] + (int)(32 * c * a.ldz * 2), 0, 0, 0);
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -875,7 +877,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
     auto xdma = [&](int lt, int b) __attribute__((always_inline)) {
       const int off = (int)(((32 * b + xr) * a.ldx + min((kt0 + lt) * 64 + xc, kmax)) * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (wg_lptr)(rb_lds + b * 4096 + w * 1024), 16,
-                                               (rb.dbg & 4) ? kRbOob : off, 0, 0, 0);
+                                               (DSML_MEASURE_KNOB(rb.dbg) & 4) ? kRbOob : off, 0, 0, 0);
     };
 #pragma unroll
     for (int b = 0; b < 16; ++b)
@@ -898,7 +900,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int nr = n0 + er + 32 * jj, kc = k0 + ec;
-        const bool ok = nr < a.N && kc < a.K && !(rb.dbg & 1);
+        const bool ok = nr < a.N && kc < a.K && !(DSML_MEASURE_KNOB(rb.dbg) & 1);
         whv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? (int)((nr * a.ldwh + kc) * 2) : kRbOob, 0, 0);
         wlv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rl, ok ? (int)((nr * a.ldwl + kc) * 2) : kRbOob, 0, 0);
       }
@@ -1051,7 +1053,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int nr = n0 + er + 32 * jj, kc = k0 + ec;
-        const bool ok = nr < a.N && kc < a.K && !(rb.dbg & 1);
+        const bool ok = nr < a.N && kc < a.K && !(DSML_MEASURE_KNOB(rb.dbg) & 1);
         float wv[8];
         hl_join8(make_uint4(whv[jj].x, whv[jj].y, whv[jj].z, whv[jj].w),
                  make_uint4(wlv[jj].x, wlv[jj].y, wlv[jj].z, wlv[jj].w), wv);
@@ -1139,8 +1141,12 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
     }
   }
   rb.groups = std::min(cus, u);
+#ifdef HIPDSML_MEASURE
   static const int rb_dbg = getenv("HIPDSML_RB_DBG") ? atoi(getenv("HIPDSML_RB_DBG")) : 0;
   rb.dbg = rb_dbg;
+#else
+  rb.dbg = 0;
+#endif
   switch (layers[0].M) {
     case 64: hipLaunchKernelGGL(wgrad_rowblk_k<2>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
     case 128: hipLaunchKernelGGL(wgrad_rowblk_k<4>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;

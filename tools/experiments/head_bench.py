@@ -8,6 +8,7 @@ sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(_
 from hipdsml.ops.native import require_native  # noqa: E402
 
 C = require_native()
+assert C.measure_build, "head_set_debug needs the measurement build: python -m hipdsml._build --measure"
 dev = torch.device("cuda", 0)
 B, K, Cn = 64, 4096, 10
 H = torch.randn(B, K, device=dev).to(torch.bfloat16)

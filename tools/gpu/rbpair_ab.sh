@@ -1,6 +1,8 @@
 # Row-block update with two ring blocks per wait / barrier: the row-block and
 # DP tests on the new tree, then the global-batch update cost of the staged
 # old (one block) / new (pairs) builds, alternating, with and without traffic.
+# The no-traffic rows need measurement builds of both trees (HIPDSML_RB_DBG is
+# compiled out of production builds): python -m hipdsml._build --measure.
 set -e
 T=${1:-rp}
 R=$GRAFT_REPO_ROOT
