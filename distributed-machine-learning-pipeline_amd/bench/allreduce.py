@@ -85,8 +85,12 @@ def bench_rpc(a) -> None:
             coord.Memcpy(pb.MemcpyRequest(hostToDevice=pb.MemcpyHostToDeviceRequest(
                 hostSrcData=rng.standard_normal(size // 4).astype(np.float32).tobytes(),
                 dstDeviceId=d.deviceId, dstMemAddr=pb.MemAddr(value=0x1000))))
-        res = {}
+        res, ran = {}, {}
+        # "" = no algo flag: the coordinator's own choice (coordinator.choose_algo:
+        # xgmi for fp32 sums on GPU devices of one node, the tuned RCCL ring on
+        # distinct GPUs, else the stream ring) -- the algorithm that ran is recorded
         runs = [("ring_as_published", size // 4, DT_UINT8, ""), ("ring_full_fp32", size, DT_FLOAT32, ""),
+                ("stream_ring_fp32", size, DT_FLOAT32, "stream-ring"),
                 ("ring_per_segment_rpc_fp32", size, DT_FLOAT32, "device-ring")]
         if pg:
             runs.append(("xgmi_fp32", size, DT_FLOAT32, "xgmi"))
@@ -94,16 +98,19 @@ def bench_rpc(a) -> None:
             ts = []
             for k in range(a.reps + 1):
                 t0 = time.perf_counter()
-                coord.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=count, dtype=dt, algo=algo))
+                rr = coord.AllReduceRing(pb.AllReduceRingRequest(commId=cid, count=count, dtype=dt, algo=algo))
                 if k:  # the first call opens the streams / exchange buffers
                     ts.append((time.perf_counter() - t0) * 1e3)
             res[label] = ts
+            ran[label] = {"algo": rr.algo, "chunk_bytes": rr.chunkBytes}
         out = {"bench": "allreduce_rpc", "n_devices": a.n, "backend": backend,
                "processes": "in-process" if a.inproc else "one per server",
                "data_bytes": size, "latency_ms_injected": a.latency_ms,
                "naive_ms_median": round(statistics.median(naive), 3),
                "ring_as_published_ms_median": round(statistics.median(res["ring_as_published"]), 3),
                "ring_full_fp32_ms_median": round(statistics.median(res["ring_full_fp32"]), 3),
+               "stream_ring_fp32_ms_median": round(statistics.median(res["stream_ring_fp32"]), 3),
+               "algo_ran": ran,
                "ring_per_segment_rpc_fp32_ms_median": round(statistics.median(res["ring_per_segment_rpc_fp32"]), 3),
                "xgmi_fp32_ms_median": (round(statistics.median(res["xgmi_fp32"]), 3) if "xgmi_fp32" in res
                                        else None),

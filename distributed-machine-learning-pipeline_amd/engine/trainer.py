@@ -23,6 +23,7 @@ import torch
 from ..data.mnist import Dataset
 from ..models.mlp import MlpLayout, MlpSpec, forward_ref, grads_ref, init_params
 from ..parallel.dist import DistContext, make_native_comm
+from ..utils.initbudget import InitPhases
 
 log = logging.getLogger("hipdsml.trainer")
 
@@ -93,10 +94,14 @@ class MlpTrainer:
                  xact_waves: int = 0, auto_fallback: str = "rccl",
                  stream: Optional["torch.cuda.Stream"] = None, persist: Optional[bool] = None,
                  grad_allreduce=None, node_local: Optional[bool] = None,
-                 persist_place_trials: Optional[int] = None):
+                 persist_place_trials: Optional[int] = None,
+                 init_phases: Optional[InitPhases] = None):
         if sync not in SYNC_MODES:
             raise ValueError(f"sync must be one of {SYNC_MODES}")
         self.ctx = ctx or DistContext()
+        # init wall-clock phases + the total budget of the optional ones
+        # (utils/initbudget.py); bench.py passes its own to cover the whole job
+        self.init_phases = init_phases if init_phases is not None else InitPhases(self.ctx)
         self.spec = spec
         self.device = self.ctx.device
         self.batch = int(batch)
@@ -109,11 +114,16 @@ class MlpTrainer:
             raise ValueError(f"dataset has {len(data)} rows < batch {self.batch}")
         if data.X.shape[1] != spec.dims[0]:
             raise ValueError(f"data dim {data.X.shape[1]} != model input {spec.dims[0]}")
-        self.X = _pad_cols(data.X.to(self.device, torch.float32))
-        self.y = data.y.to(self.device, torch.int32).contiguous()
+        ph = self.init_phases
+        with ph.phase("upload"):
+            self.X = _pad_cols(data.X.to(self.device, torch.float32))
+            self.y = data.y.to(self.device, torch.int32).contiguous()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
         self.nbatches = len(data) // self.batch
         self.layout = MlpLayout(spec, self.batch, self.nbatches)
-        P = params if params is not None else init_params(self.layout, seed, init)
+        with ph.phase("param_init"):
+            P = params if params is not None else init_params(self.layout, seed, init)
         if P.numel() != self.layout.nparams:
             raise ValueError("params do not match the layout")
         self.P = P.to(self.device, torch.float32).contiguous().clone()
@@ -176,7 +186,8 @@ class MlpTrainer:
         self.pk_err: Optional[torch.Tensor] = None
         if self.device.type == "cuda":
             self.backend = "hip"
-            self._init_hip(ring_chunk_bytes)
+            with ph.phase("native_init"):
+                self._init_hip(ring_chunk_bytes)
         else:
             self.backend = "torch"
 
@@ -213,15 +224,17 @@ class MlpTrainer:
                 self.pk_buf = torch.zeros(C.mlp_persist_xbuf_granules(), dtype=torch.int64, device=d)
                 self.pk_err = torch.zeros(1, dtype=torch.int32, device=d)
                 t0 = time.perf_counter()
-                self.pk_gram = self._gram_table()
-                torch.cuda.synchronize(d)
+                with self.init_phases.phase("gram_table"):
+                    self.pk_gram = self._gram_table()
+                    torch.cuda.synchronize(d)
                 self.precompute_ms["gram_table"] = round(1e3 * (time.perf_counter() - t0), 2)
                 self.runner.set_persist_gram(self.pk_gram)
                 self.runner.set_persist(self.pk_buf, self.pk_err, 2000.0)
                 self.sync_active = "none"
                 if self.device.type == "cuda" and self._place_trials > 1:
                     t0 = time.perf_counter()
-                    self._place_persist_buffer(self._place_trials)
+                    with self.init_phases.phase("persist_place"):
+                        self._place_persist_buffer(self._place_trials)
                     self.precompute_ms["persist_place"] = round(1e3 * (time.perf_counter() - t0), 2)
             return
         if self.sync == "torch":
@@ -235,15 +248,19 @@ class MlpTrainer:
         if torch_fallback:
             self.sync_active = "torch"
         elif self.sync not in EXCHANGE_MODES:  # strict exchange modes: no RCCL fallback
+            ph = self.init_phases
             if self.comm is None:
-                self.comm = make_native_comm(self.ctx)
+                with ph.phase("rccl_comm_init"):
+                    self.comm = make_native_comm(self.ctx)
             if self._ring_chunk <= 0:
-                if self.sync in ("auto", "ring") and self.ctx.backend != "none":
+                if (self.sync in ("auto", "ring") and self.ctx.backend != "none"
+                        and ph.allow("ring_tune")):
                     # measured, not guessed: every distinct chunk timed on the
                     # gradient itself, max over ranks (parallel/ring_tune.py)
                     from ..parallel.ring_tune import tune_ring_chunk
 
-                    res = tune_ring_chunk(self.ctx, self.comm, self.G)
+                    with ph.phase("ring_tune"):
+                        res = tune_ring_chunk(self.ctx, self.comm, self.G)
                     self._ring_chunk = int(res["best"])
                     # both schedules' sweeps, the choice, and any pipelined-probe error
                     self.ring_chunk_sweep_us = {k: v for k, v in res.items() if k != "best"}
@@ -254,7 +271,8 @@ class MlpTrainer:
             self.runner.set_comm(self.comm, 1 if self.sync == "ring" else 0, self._ring_chunk)
             self.sync_active = "ring" if self.sync == "ring" else "rccl"
         if self.exchange_candidates():
-            self._init_exchanges()
+            with self.init_phases.phase("exchanges"):
+                self._init_exchanges()
 
     def exchange_candidates(self) -> list:
         """The fused xGMI exchange forms _init_exchanges self-tests, in
@@ -380,9 +398,26 @@ class MlpTrainer:
         self.pk_gram_dp = None
         strict = self.sync in EXCHANGE_MODES
         modes = self.exchange_candidates()
+        ph = self.init_phases
         ok = []
+        try:
+            self._init_exchange_modes(modes, strict, ok, ph)
+        finally:
+            # the all-gathered fp32 shards: only the tables' builds read them
+            # (released on the failure path too)
+            self._plain = None
+        if self.sync_active not in XALL_MODES and self.Xall is not None:
+            # the replicated inputs (N x the shard) are only read by xact / pkx:
+            # free them, the runner's references included
+            self.Xall = None
+            self.runner.release_xall()
+
+    def _init_exchange_modes(self, modes, strict: bool, ok: list, ph: InitPhases) -> None:
         for m in modes:
-            err = self._setup_exchange(m)
+            if ok and not strict and not ph.allow(f"selftest_{m}"):
+                continue  # init budget spent: the candidates that passed are enough
+            with ph.phase(f"selftest_{m}"):
+                err = self._setup_exchange(m)
             if err:
                 if strict:
                     raise RuntimeError(f"{m} exchange unavailable: {err}")
@@ -390,25 +425,23 @@ class MlpTrainer:
             else:
                 ok.append(m)
         choice = ok[0] if ok else None
-        if self.sync == "auto" and ok:
+        if self.sync == "auto" and ok and ph.allow("sync_timing"):
             # every candidate timed the way train_steps runs it (graph replay,
             # RCCL collectives captured too); ties go to the earlier candidate
+            # (over budget: the first candidate that passed, in preference order)
             fallback = ["rccl", "ring"] if self.comm is not None else [self.sync_active]
-            times = self.time_sync_modes(ok + fallback)
+            with ph.phase("sync_timing"):
+                times = self.time_sync_modes(ok + fallback)
             choice = min(times, key=times.get)
             log.info("sync auto: %s", ", ".join(f"{k} {v:.1f} us/step" for k, v in times.items()))
             self.sync_times = times
         self._set_mode(choice or self.sync_active)
-        if self.sync_active in PERSIST_MODES and self._place_trials_dp > 1:
+        if (self.sync_active in PERSIST_MODES and self._place_trials_dp > 1
+                and ph.allow("persist_place_dp")):
             t0 = time.perf_counter()
-            self._place_persist_buffer_dp(self._place_trials_dp)  # collective
+            with ph.phase("persist_place_dp"):
+                self._place_persist_buffer_dp(self._place_trials_dp)  # collective
             self.precompute_ms["persist_place_dp"] = round(1e3 * (time.perf_counter() - t0), 2)
-        self._plain = None  # the all-gathered fp32 shards: only the tables' builds read them
-        if self.sync_active not in XALL_MODES and self.Xall is not None:
-            # the replicated inputs (N x the shard) are only read by xact / pkx:
-            # free them, the runner's references included
-            self.Xall = None
-            self.runner.release_xall()
 
     @staticmethod
     def runner_module():

@@ -43,6 +43,7 @@ class GPUDeviceServicer:
         self._ring_in: Dict[int, dict] = {}
         self._ring_cv = threading.Condition()
         self._xgmi_ar: Dict[int, object] = {}   # commId -> XgmiAllReduce (pg comms on GPUs)
+        self._ring_chunks: Dict[int, Dict[int, int]] = {}  # commId -> size class -> tuned chunk
         self._aborted_comms: set = set()        # Abort is sticky for its communicator
         self._peer_stubs: Dict[str, GPUDeviceStub] = {}
         self._lock = threading.Lock()
@@ -254,6 +255,8 @@ class GPUDeviceServicer:
             backend = "rccl"
         if request.storeAddress:
             backend = self._join_process_group(cid, request, context)
+            if self.dev.backend == "hip" and self.pg_node_local:
+                backend += "+xgmi"  # GPU peers on one node: the xGMI peer all-reduce applies
         self.comm_meta[cid] = meta
         return pb.CommSetupResponse(success=True, backend=backend)
 
@@ -585,7 +588,7 @@ class GPUDeviceServicer:
             except RuntimeError as e:
                 context.abort(grpc.StatusCode.INTERNAL, f"xGMI all-reduce failed: {e}")
             self.counters["allreduces"] += max(1, request.repeat)
-            return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
+            return pb.DeviceAllReduceResponse(success=True, elapsedUs=us, algo="xgmi")
         comm = self.comms.get(request.commId)
         if comm is None and request.commId in self.comm_meta:
             es = DT_SIZE.get(request.dtype, 0)
@@ -607,8 +610,9 @@ class GPUDeviceServicer:
             except Exception as e:
                 context.abort(grpc.StatusCode.INTERNAL, f"device ring failed: {e}")
             self.counters["allreduces"] += max(1, request.repeat)
-            return pb.DeviceAllReduceResponse(success=True,
-                                              elapsedUs=(time.perf_counter() - t0) * 1e6)
+            return pb.DeviceAllReduceResponse(success=True, elapsedUs=(time.perf_counter() - t0) * 1e6,
+                                              algo=request.algo if request.algo == "stream-ring" else "rpc-ring",
+                                              chunkBytes=request.chunkBytes)
         if comm is None:
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"no communicator {request.commId} on this device")
         if comm.aborted:
@@ -622,7 +626,15 @@ class GPUDeviceServicer:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         algo = request.algo or "ring"
         reps = max(1, request.repeat)
-        chunk = request.chunkBytes or (1 << 20)
+        chunk = int(request.chunkBytes)
+        if algo != "rccl" and chunk <= 0:
+            # the in-house ring's chunk (and schedule), measured once per comm
+            # and size class on this very buffer (parallel/ring_tune.py), not
+            # a fixed 1 MiB: collective, every device gets the same call
+            try:
+                chunk = self._tuned_chunk(request.commId, comm, t)
+            except Exception as e:  # noqa: BLE001
+                context.abort(grpc.StatusCode.INTERNAL, f"ring chunk tuning failed: {e}")
         torch.cuda.synchronize(self.dev.gpu)
         t0 = time.perf_counter()
         try:
@@ -642,7 +654,32 @@ class GPUDeviceServicer:
             context.abort(grpc.StatusCode.INTERNAL, f"RCCL error: {err}")
         us = (time.perf_counter() - t0) * 1e6 / reps
         self.counters["allreduces"] += reps
-        return pb.DeviceAllReduceResponse(success=True, elapsedUs=us)
+        return pb.DeviceAllReduceResponse(success=True, elapsedUs=us, algo=algo,
+                                          chunkBytes=0 if algo == "rccl" else chunk)
+
+    def _tuned_chunk(self, cid: int, comm, t) -> int:
+        """Chunk of the in-house ring for `t`'s size class (the power of two
+        at or above its byte size) on comm `cid`: tuned on the first call of
+        that class with ring_tune.tune_ring_chunk (max over ranks, the
+        pipelined schedule only where HIPDSML_RING_PIPELINE=1 opts in) and
+        cached for the comm's life.  A 1-element class keeps RCCL's scratch
+        sane: nothing below 4 KiB is tuned."""
+        from ..parallel.dist import DistContext
+        from ..parallel.ring_tune import tune_ring_chunk
+
+        nbytes = t.numel() * t.element_size()
+        cls = max(4096, 1 << max(0, (nbytes - 1).bit_length()))
+        cache = self._ring_chunks.setdefault(cid, {})
+        if cls not in cache:
+            meta = self.comm_meta[cid]
+            ctx = DistContext(rank=meta["rank"], world_size=meta["nranks"], device=self._torch_device(),
+                              backend="gloo")
+            with torch.cuda.device(self.dev.gpu):
+                res = tune_ring_chunk(ctx, comm, t.view(-1), iters=10)  # restores t
+            cache[cls] = int(res["best"])
+            log.info("%s: comm %d ring chunk for <= %d B: %d B (%s)", self.name, cid, cls, cache[cls],
+                     res.get("sweep_us"))
+        return cache[cls]
 
     def Abort(self, request, context):
         # unblock any device-driven ring step waiting on a peer that died, and

@@ -104,7 +104,8 @@ MESSAGES: M = {
                              ("memAddrs", 4, "", "map:uint32:.MemAddr"),
                              ("dtype", 5, ".DataType"), ("algo", 6, "string"),
                              ("chunkBytes", 7, "uint64")],
-    "AllReduceRingResponse": [("success", 1, "bool"), ("elapsedUs", 2, "double")],
+    "AllReduceRingResponse": [("success", 1, "bool"), ("elapsedUs", 2, "double"),
+                              ("algo", 3, "string"), ("chunkBytes", 4, "uint64")],  # what ran
     "CommDestroyRequest": [("commId", 1, "uint64")],
     "CommDestroyResponse": [("success", 1, "bool")],
     "CommFinalizeRequest": [("commId", 1, "uint64")],
@@ -138,7 +139,8 @@ MESSAGES: M = {
                                ("dtype", 4, ".DataType"), ("op", 5, ".ReduceOp"),
                                ("algo", 6, "string"), ("chunkBytes", 7, "uint64"),
                                ("repeat", 8, "uint32")],
-    "DeviceAllReduceResponse": [("success", 1, "bool"), ("elapsedUs", 2, "double")],
+    "DeviceAllReduceResponse": [("success", 1, "bool"), ("elapsedUs", 2, "double"),
+                                ("algo", 3, "string"), ("chunkBytes", 4, "uint64")],
     "AbortRequest": [("commId", 1, "uint64"), ("reason", 2, "string")],
     "AbortResponse": [("success", 1, "bool")],
     "CommTeardownRequest": [("commId", 1, "uint64")],
