@@ -398,7 +398,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                     double inv_batch, c10::optional<torch::Tensor> logits,
                                     torch::Tensor dz, c10::optional<torch::Tensor> dzT,
                                     torch::Tensor stats, c10::optional<torch::Tensor> dzp,
-                                    c10::optional<torch::Tensor> dzpT, bool row_stats) {
+                                    c10::optional<torch::Tensor> dzpT, bool row_stats,
+                                    c10::optional<torch::Tensor> hs, int64_t hs_splits,
+                                    c10::optional<torch::Tensor> hs_bias, bool hs_relu, double hs_alpha) {
     TORCH_CHECK(!row_stats || stats.numel() >= 4 * B, "row_stats needs 4 floats per row");
     TORCH_CHECK(H.dim() == 2 && H.stride(1) == 1 && H.size(0) >= B && H.size(1) >= K, "H shape");
     TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.size(0) >= C && W.size(1) >= K, "W shape");
@@ -420,14 +422,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (dzpT) { TORCH_CHECK(dzp && dzpT->dim() == 2 && dzpT->stride(1) == 1 && dzpT->size(0) >= K && dzpT->size(1) >= B,
                             "dzpT shape (needs dzp)");
                 ppT = bf16p(*dzpT, "dzpT"); ldpT = dzpT->stride(0); }
+    HeadSlabs hsl{};
+    if (hs) {
+      // H is OUTPUT here: the raw split-K slices of the last hidden layer's GEMM
+      // (gemm_skinny raw=True), combined + epilogue on load, H written back
+      check_f32(*hs, "hs");
+      const int64_t stride = hs->numel() / std::max<int64_t>(1, hs_splits);
+      TORCH_CHECK(hs_splits >= 1 && stride >= (K / 64) * 4096, "hs: hs_splits slices of K/64 tiles x 4096");
+      hsl.slabs = hs->data_ptr<float>();
+      hsl.S = (int)hs_splits;
+      hsl.stride = (K / 64) * 4096;
+      hsl.alpha = (float)hs_alpha;
+      if (hs_bias) { check_f32(*hs_bias, "hs_bias"); TORCH_CHECK(hs_bias->numel() >= K, "hs_bias");
+                     hsl.bias = hs_bias->data_ptr<float>(); }
+      hsl.relu = hs_relu ? 1 : 0;
+      hsl.Hout = bf16p(H, "H");
+      hsl.ldo = H.stride(0);
+    }
     hip_ok(head_softmax_xent(bf16p(H, "H"), H.stride(0), bf16p(W, "W"), W.stride(0), b, (int)B, (int)K,
                              (int)C, labels.data_ptr<int32_t>(), (float)inv_batch, lg, ldl,
                              bf16p(dz, "dz"), dz.stride(0), t, ldt, (int)Cp, stats.data_ptr<float>(),
-                             cur_stream(), pp, ldp, ppT, ldpT, row_stats ? 1 : 0), "head_softmax_xent");
+                             cur_stream(), pp, ldp, ppT, ldpT, row_stats ? 1 : 0, hs ? &hsl : nullptr),
+           "head_softmax_xent");
   }, py::arg("H"), py::arg("W"), py::arg("bias"), py::arg("B"), py::arg("K"), py::arg("C"),
      py::arg("labels"), py::arg("inv_batch"), py::arg("logits"), py::arg("dz"), py::arg("dzT"),
      py::arg("stats"), py::arg("dzp") = py::none(), py::arg("dzpT") = py::none(),
-     py::arg("row_stats") = false);
+     py::arg("row_stats") = false, py::arg("hs") = py::none(), py::arg("hs_splits") = 0,
+     py::arg("hs_bias") = py::none(), py::arg("hs_relu") = true, py::arg("hs_alpha") = 1.0);
   m.def("rowsum_bf16", [bf16p](torch::Tensor X, int64_t N, int64_t cols, c10::optional<torch::Tensor> out,
                               c10::optional<torch::Tensor> bias, double lr) {
     TORCH_CHECK(X.dim() == 2 && X.size(0) >= N && X.size(1) >= cols, "X shape");
@@ -510,7 +531,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> of32,
                               c10::optional<torch::Tensor> obf, c10::optional<torch::Tensor> obfT,
                               int64_t splits, c10::optional<torch::Tensor> ws,
-                              c10::optional<torch::Tensor> ctr) {
+                              c10::optional<torch::Tensor> ctr, bool raw) {
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "A, B 2-D rows");
     TORCH_CHECK(A.size(0) >= M && A.size(1) >= K, "A too small");
     TORCH_CHECK(nn ? (B.size(0) >= K && B.size(1) >= N) : (B.size(0) >= N && B.size(1) >= K), "B too small");
@@ -529,7 +550,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const int S = gemm_skinny_splits((int)M, (int)N, (int)K, (int)splits);
     float* cp = nullptr;
     int* tc = nullptr;
-    if (S > 1) {
+    if (raw) {
+      // consumer-combined: every slice's partial tile into ws, no epilogue here
+      TORCH_CHECK(ws && !bias && !mask && !of32 && !obf && !obfT,
+                  "raw skinny GEMM: ws only (the consumer applies the epilogue)");
+      check_f32(*ws, "ws");
+      const int64_t tiles = ((N + 63) / 64) * ((M + 63) / 64);
+      TORCH_CHECK(ws->numel() >= (int64_t)S * tiles * 4096, "ws too small for the raw slices");
+      cp = ws->data_ptr<float>();
+    } else if (S > 1) {
       TORCH_CHECK(ws && ctr, "split-K skinny GEMM needs ws (slabs) and ctr (tile counters)");
       check_f32(*ws, "ws");
       int64_t wsw = 0, ctw = 0;
@@ -542,13 +571,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       tc = ctr->data_ptr<int32_t>();
     }
     hip_ok(gemm_skinny(bf16p(A, "A"), A.stride(0), bf16p(B, "B"), B.stride(0), (int)M, (int)N, (int)K, nn,
-                       (int)splits, cp, tc, e, cur_stream()), "gemm_skinny");
+                       (int)splits, cp, tc, e, cur_stream(), raw), "gemm_skinny");
     return S;
   }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("nn") = false,
      py::arg("alpha") = 1.0, py::arg("bias") = py::none(), py::arg("relu") = false,
      py::arg("mask") = py::none(), py::arg("of32") = py::none(), py::arg("obf") = py::none(),
      py::arg("obfT") = py::none(), py::arg("splits") = 0, py::arg("ws") = py::none(),
-     py::arg("ctr") = py::none());
+     py::arg("ctr") = py::none(), py::arg("raw") = false);
   m.def("wgrad_sgd", [bf16p](torch::Tensor Z, torch::Tensor X, int64_t M, int64_t N, int64_t K, double alpha,
                             double lr, c10::optional<torch::Tensor> W, c10::optional<torch::Tensor> Wb,
                             c10::optional<torch::Tensor> G, c10::optional<torch::Tensor> bias,
@@ -760,6 +789,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
      "float64 torch oracle)");
   m.def("mlp_persist_set_pkx_helpers", [](int h) { mlp_persist_set_pkx_helpers(h); }, py::arg("helpers"),
         "pkx dW1 helper blocks per layer-1 block: -1 default (3 from 4 replicas on), 0, 1 or 3");
+#ifdef HIPDSML_MEASURE
+  m.def("mlp_persist_set_hop", [](double us) { mlp_persist_set_hop((int)(us * 100.0 + 0.5)); }, py::arg("us"),
+        "measurement builds: every cross-replica hop of the mirror mode becomes usable `us` after "
+        "its publication (0 off)");
+#endif
   m.def("mlp_persist_set_probe", [](int mode) { mlp_persist_set_probe(mode); },
         "testing only: 0 off; 1 peers' dZ1 rows taken as arrived (lone-replica probe of the Gram "
         "forms); 2 mirror: every push loops back into this replica's own buffer in the peer's "

@@ -111,6 +111,9 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              const float* gram = nullptr, int carry = 0,
                              const float* xsw = nullptr, int64_t xsw_stride = 0);
 void mlp_persist_set_probe(int mode);  // testing only: 0 off, 1 lone-replica probe, 2 mirror
+#ifdef HIPDSML_MEASURE
+void mlp_persist_set_hop(int ticks);  // measurement builds: extra hop latency in mirror mode (100 MHz ticks)
+#endif
 // pkx dW1 helper blocks per layer-1 block: -1 the default (3 from 4 replicas on,
 // else 0; HIPDSML_PKX_HELPERS overrides it), 0, 1 or 3 (tuning / testing)
 void mlp_persist_set_pkx_helpers(int helpers);
@@ -264,6 +267,20 @@ hipError_t cast_transpose(const float* X, int64_t ldi, int M, int K, int Kp, uin
 hipError_t softmax_xent(const float* logits, int64_t ldl, const int32_t* labels, int B, int C,
                         int Cp, float inv_batch, uint16_t* dz, int64_t ldz, uint16_t* dzT,
                         int64_t ldt, float* stats, hipStream_t s);
+// The head's H from a raw split-K skinny GEMM (gemm_skinny raw_slabs): H[m][k]
+// = bf16(relu(alpha * sum_{z < S} slabs[z][k / 64][m][k % 64] + bias[k])),
+// slices summed in slice order -- bit-identical to the skinny GEMM's own
+// combine + epilogue -- and written to Hout (the weight update reads it).
+struct HeadSlabs {
+  const float* slabs;
+  int S;              // 2, 4 or 8 slices
+  int64_t stride;     // floats per slice (tiles * 4096)
+  float alpha;
+  const float* bias;  // [K] (nullable)
+  int relu;
+  uint16_t* Hout;     // [B][ldo] bf16
+  int64_t ldo;
+};
 // Classifier head fused with softmax-CE (C <= 16, K <= 4096): logits = H . W^T
 // (row_stats: loss / correct / count accumulate in stats[4m ..] per row m,
 // summed by the reader, instead of atomics on stats[0..2])
@@ -275,7 +292,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp = nullptr, int64_t ldzp = 0, uint16_t* dzpT = nullptr,
-                             int64_t ldpt = 0, int row_stats = 0);
+                             int64_t ldpt = 0, int row_stats = 0, const HeadSlabs* hs = nullptr);
 // Skinny GEMMs (kernels/gemm_skinny.hip): C[M x N] = A[M x K] . B^T for
 // B [N x K] (nn = false) or A . B for B [K x N] (nn = true: W read in its
 // stored layout through transposing LDS reads), 64 x 64 tiles, K split S ways
@@ -288,9 +305,12 @@ int gemm_skinny_splits(int M, int N, int K, int splits);
 void gemm_skinny_ws(int M, int N, int K, int splits, int64_t* ws_words, int64_t* ctr_words);
 hipError_t gemm_skinny_read_stamps(uint64_t* host_out);  // [1024][5], profiling only
 void gemm_skinny_set_stamping(bool on);
+// raw_slabs: every slice stores its fp32 partial tile into slabs[slice][tile]
+// ([64 rows][64 cols] each, tile = m block * N tiles + n block) and the launch
+// applies no epilogue: the consumer sums the slices (head_softmax_xent's Hs).
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N,
                        int K, bool nn, int splits, float* slabs, int* tile_ctr, const GemmEpi& epi,
-                       hipStream_t s);
+                       hipStream_t s, bool raw_slabs = false);
 // Weight gradient from row-major activations (kernels/wgrad_sgd.hip):
 // G = alpha * Z^T X (Z [M x N], X [M x K] bf16, rows padded to 8 columns), then
 // W -= lr * G (+ bf16 copy Wb) when W is given, else G written out; bias -= lr

@@ -786,8 +786,9 @@ __constant__ int g_head_stamp_on;  // __constant__: scalar loads, no vector wait
 #ifdef HIPDSML_MEASURE
 __constant__ int g_head_dbg;  // measurement builds: bit 0 skips the stats atomics, bit 1 the dzp phase
 #endif
-// MAXC: the class count rounded up to an instantiated size (even: class pairs)
-template <int MAXC>
+// MAXC: the class count rounded up to an instantiated size (even: class pairs);
+// SL: 0 = bf16 H, else H from SL raw split-K slices (head_row.h)
+template <int MAXC, int SL = 0>
 __global__ __launch_bounds__(256) void head_softmax_xent_k(HeadRow h) {
   __shared__ float part[MAXC][17];     // [class][wave * 4 + 16-lane row] partial sums (+1: pad)
   __shared__ uint32_t gz2[MAXC / 2];   // bf16-rounded dLogits of this row, class pairs
@@ -797,7 +798,7 @@ __global__ __launch_bounds__(256) void head_softmax_xent_k(HeadRow h) {
 #else
   h.dbg = 0;
 #endif
-  head_row<MAXC>(h, m, part, gz2, (g_head_stamp_on && m < 64) ? g_head_stamps[m] : nullptr);
+  head_row<MAXC, SL>(h, m, part, gz2, (g_head_stamp_on && m < 64) ? g_head_stamps[m] : nullptr);
 }
 
 hipError_t head_read_stamps(uint64_t* host_out) {
@@ -822,7 +823,7 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
                              float inv_batch, float* logits, int64_t ldl, uint16_t* dz, int64_t ldz,
                              uint16_t* dzT, int64_t ldt, int Cp, float* stats, hipStream_t s,
                              uint16_t* dzp, int64_t ldzp, uint16_t* dzpT, int64_t ldpt,
-                             int row_stats) {
+                             int row_stats, const HeadSlabs* hs) {
   if (dzp && ((ldzp & 7) || ((uintptr_t)dzp & 15))) return hipErrorInvalidValue;
   if (row_stats && stats && ((uintptr_t)stats & 15)) return hipErrorInvalidValue;  // float4 per row
   if (C < 1 || C > kHeadMaxC || Cp > 64 || (K & 7) || K > 256 * 8 * kHeadMaxK8 || (ldh & 7) ||
@@ -830,11 +831,38 @@ hipError_t head_softmax_xent(const uint16_t* H, int64_t ldh, const uint16_t* W, 
       (((uintptr_t)H | (uintptr_t)W) & 15))
     return hipErrorInvalidValue;
   HeadRow h{H, ldh, W, ldw, bias, K, C, Cp, labels, inv_batch, logits, ldl, dz, ldz, dzT, ldt, stats,
-            dzp, ldzp, dzpT, ldpt, row_stats, 0};
-  if (C <= 10)
-    hipLaunchKernelGGL(head_softmax_xent_k<10>, dim3(B), dim3(256), 0, s, h);
-  else
-    hipLaunchKernelGGL(head_softmax_xent_k<kHeadMaxC>, dim3(B), dim3(256), 0, s, h);
+            dzp, ldzp, dzpT, ldpt, row_stats, 0,
+            nullptr, 0, 1.f, nullptr, 0, nullptr, 0};
+  int sl = 0;
+  if (hs != nullptr) {
+    // raw split-K slices of ONE 64-row tile block: rows <= 64, K in whole tiles
+    if (B > 64 || (K & 63) || !(hs->S == 2 || hs->S == 4 || hs->S == 8) || hs->slabs == nullptr ||
+        hs->stride < (int64_t)(K / 64) * 4096 || (hs->stride & 3) || ((uintptr_t)hs->slabs & 15) ||
+        (hs->bias && ((uintptr_t)hs->bias & 15)) || hs->Hout == nullptr || (hs->ldo & 7) ||
+        ((uintptr_t)hs->Hout & 15))
+      return hipErrorInvalidValue;
+    sl = hs->S;
+    h.hs = hs->slabs;
+    h.hs_stride = hs->stride;
+    h.hs_alpha = hs->alpha;
+    h.hs_bias = hs->bias;
+    h.hs_relu = hs->relu;
+    h.hout = hs->Hout;
+    h.ldho = hs->ldo;
+  }
+#define DSML_HEAD_LAUNCH(MC)                                                                         \
+  switch (sl) {                                                                                      \
+    case 0: hipLaunchKernelGGL((head_softmax_xent_k<MC, 0>), dim3(B), dim3(256), 0, s, h); break;  \
+    case 2: hipLaunchKernelGGL((head_softmax_xent_k<MC, 2>), dim3(B), dim3(256), 0, s, h); break;  \
+    case 4: hipLaunchKernelGGL((head_softmax_xent_k<MC, 4>), dim3(B), dim3(256), 0, s, h); break;  \
+    default: hipLaunchKernelGGL((head_softmax_xent_k<MC, 8>), dim3(B), dim3(256), 0, s, h); break; \
+  }
+  if (C <= 10) {
+    DSML_HEAD_LAUNCH(10)
+  } else {
+    DSML_HEAD_LAUNCH(kHeadMaxC)
+  }
+#undef DSML_HEAD_LAUNCH
   return hipGetLastError();
 }
 

@@ -94,6 +94,8 @@ struct SkArgs {
   float* slabs;
   int* ctr;
   GemmEpi epi;
+  int raw;  // every slice stores its partial tile to slabs[z] and exits: the CONSUMER sums
+            // the S slices in slice order and applies the epilogue on load (the wide head)
 };
 
 // Profiling only (tools/skinny_stamps.py): per workgroup s_memrealtime at
@@ -268,6 +270,20 @@ __global__ __launch_bounds__(kSkThreads, 1) void gemm_skinny_k(SkArgs a) {
   }
 
   SK_STAMP(2);
+  if (a.raw) {
+    // consumer-combined split-K: this slice's tile into its slab, nothing else
+    // (no ticket, no write-acknowledge wait, no combine: kernels/head_row.h
+    // sums the slices in slice order as it loads them).  Plain stores: the
+    // kernel boundary publishes them.
+    const int tiles = gridDim.x * gridDim.z;
+    const int tile = blockIdx.z * gridDim.x + blockIdx.x;
+    float* dst = a.slabs + ((int64_t)z * tiles + tile) * 4096 + tid * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<float4*>(dst + j * 1024) = v[j];
+    SK_STAMP(3);
+    SK_STAMP(4);
+    return;
+  }
   // ---- split-K: the last slice of the tile to arrive finishes it ----
   if (S > 1) {
     const int tiles = gridDim.x * gridDim.z;
@@ -389,7 +405,7 @@ int gemm_skinny_splits(int M, int N, int K, int splits) {
 
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int M, int N,
                        int K, bool nn, int splits, float* slabs, int* tile_ctr, const GemmEpi& epi,
-                       hipStream_t s) {
+                       hipStream_t s, bool raw_slabs) {
   if (M <= 0 || N <= 0 || K < 8 || (K & 7) || (N & 7) || (lda & 7) || (ldb & 7))
     return hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B) & 15) return hipErrorInvalidValue;
@@ -401,8 +417,10 @@ hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* B, int64_
       (epi.bias && ((uintptr_t)epi.bias & 15)))
     return hipErrorInvalidValue;
   const int S = gemm_skinny_splits(M, N, K, splits);
-  if (S > 1 && (slabs == nullptr || tile_ctr == nullptr)) return hipErrorInvalidValue;
-  SkArgs a{A, lda, B, ldb, M, N, K, (K + kSkStage - 1) / kSkStage, slabs, tile_ctr, epi};
+  if (raw_slabs && (slabs == nullptr || epi.of32 || epi.obf || epi.obfT || epi.mask))
+    return hipErrorInvalidValue;  // raw: slabs only, the consumer applies the epilogue
+  if (!raw_slabs && S > 1 && (slabs == nullptr || tile_ctr == nullptr)) return hipErrorInvalidValue;
+  SkArgs a{A, lda, B, ldb, M, N, K, (K + kSkStage - 1) / kSkStage, slabs, tile_ctr, epi, raw_slabs ? 1 : 0};
   static bool attr[2] = {false, false};
   if (!attr[nn]) {
     const void* f = nn ? reinterpret_cast<const void*>(gemm_skinny_k<true>)

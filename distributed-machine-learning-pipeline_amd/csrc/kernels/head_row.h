@@ -41,6 +41,17 @@ struct HeadRow {
   int64_t ldpt;
   int row_stats;
   int dbg;  // measurement builds only: bit 0 skips the stats, bit 1 the dzp phase
+  // H from a raw split-K GEMM instead (head_row<MAXC, SL>, SL slices): H[m][k] =
+  // bf16(relu(hs_alpha * sum_z hs[z * hs_stride + (k / 64) * 4096 + m * 64 + k % 64]
+  // + hs_bias[k])), summed in slice order like gemm_skinny's own combine, and
+  // stored to hout (rows <= 64: one 64-row tile block)
+  const float* hs;
+  int64_t hs_stride;
+  float hs_alpha;
+  const float* hs_bias;
+  int hs_relu;
+  uint16_t* hout;
+  int64_t ldho;
 };
 constexpr int kHeadMaxC = 16;  // classes the head supports (instantiated for <= 10 and <= 16)
 constexpr int kHeadMaxK8 = 2;  // 16 B chunks of the row per thread: K <= 256 * 8 * 2 = 4096
@@ -59,7 +70,8 @@ __device__ __forceinline__ float hdot8(const uint4& a, const uint4& b, float c) 
 
 // Row m; part: LDS [MAXC][17] floats, gz2: LDS [MAXC / 2] words; stamps:
 // nullable [6] (profiling).  Ends with an LDS-only barrier after its LDS use.
-template <int MAXC>
+// SL > 0: H comes as SL raw split-K slices (HeadRow::hs), combined on load.
+template <int MAXC, int SL = 0>
 __device__ __forceinline__ void head_row(const HeadRow& h, int m, float (*part)[17], uint32_t* gz2,
                                          uint64_t* stamps) {
   static_assert(MAXC % 2 == 0 && MAXC <= 16, "class pairs, one 16-lane row");
@@ -100,13 +112,55 @@ __device__ __forceinline__ void head_row(const HeadRow& h, int m, float (*part)[
   // trips in the r4 head's ISA).  Rows past C load row C - 1: their logits are
   // never read and their dLogits are 0.
   uint4 hv[kHeadMaxK8], wv[kHeadMaxK8][MAXC];
+  // raw split-K slices (SL > 0): 8 consecutive floats of every slice per chunk,
+  // plus the chunk's bias (absent: the slice's own words, dropped at the use)
+  float4 sv[SL > 0 ? SL : 1][kHeadMaxK8][2], bv[kHeadMaxK8][2];
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j) {
     const int k = min((t + 256 * j) * 8, K - 8);
-    hv[j] = *reinterpret_cast<const uint4*>(hr + k);
+    if constexpr (SL == 0) {
+      hv[j] = *reinterpret_cast<const uint4*>(hr + k);
+    } else {
+      const float* sb = h.hs + (int64_t)(k >> 6) * 4096 + m * 64 + (k & 63);
+#pragma unroll
+      for (int z = 0; z < SL; ++z) {
+        sv[z][j][0] = *reinterpret_cast<const float4*>(sb + z * h.hs_stride);
+        sv[z][j][1] = *reinterpret_cast<const float4*>(sb + z * h.hs_stride + 4);
+      }
+      const float* bp = h.hs_bias ? h.hs_bias + k : sb;
+      bv[j][0] = *reinterpret_cast<const float4*>(bp);
+      bv[j][1] = *reinterpret_cast<const float4*>(bp + 4);
+    }
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
       wv[j][c] = *reinterpret_cast<const uint4*>(W + (int64_t)min(c, C - 1) * ldw + k);
+  }
+  if constexpr (SL > 0) {
+    // gemm_skinny's combine order (0 + slice 0 + slice 1 + ...), then its
+    // epilogue (alpha, bias, ReLU, bf16): the same bits as the combined GEMM
+#pragma unroll
+    for (int j = 0; j < kHeadMaxK8; ++j) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 0.f;
+#pragma unroll
+      for (int z = 0; z < SL; ++z) {
+        x[0] += sv[z][j][0].x; x[1] += sv[z][j][0].y; x[2] += sv[z][j][0].z; x[3] += sv[z][j][0].w;
+        x[4] += sv[z][j][1].x; x[5] += sv[z][j][1].y; x[6] += sv[z][j][1].z; x[7] += sv[z][j][1].w;
+      }
+      const float b8[8] = {bv[j][0].x, bv[j][0].y, bv[j][0].z, bv[j][0].w,
+                           bv[j][1].x, bv[j][1].y, bv[j][1].z, bv[j][1].w};
+      uint32_t q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float y = x[e] * h.hs_alpha + (h.hs_bias ? b8[e] : 0.f);
+        if (h.hs_relu) y = fmaxf(y, 0.f);
+        q[e] = f32_to_bf16(y);
+      }
+      hv[j] = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
+      const int k = (t + 256 * j) * 8;
+      if (k < K && h.hout) *reinterpret_cast<uint4*>(h.hout + (int64_t)m * h.ldho + k) = hv[j];
+    }
   }
 #pragma unroll
   for (int j = 0; j < kHeadMaxK8; ++j)

@@ -534,6 +534,41 @@ __device__ __forceinline__ int64_t pk_dzr_base(const PersistArgs& a, uint64_t s,
   return (int64_t)(s & 1) * a.xhalf + a.dzr_off + (int64_t)src * kDzrFloats;
 }
 
+// Measurement builds only (-DHIPDSML_MEASURE; tools/pk_probe.py --hop-us): an
+// extra one-way latency on every cross-replica hop of the MIRROR test mode.
+// Each push of peer data (a chain wave's dZ1 rows, a slot's values or flag)
+// first stamps its publish time as a tagged granule {time, step tag} per item
+// (dZ1: chain c, wave w -> item 4 c + w; slot k -> item 16 + k); a reader
+// that has found the peers' data of an item also waits until g_pk_hop ticks
+// (100 MHz) have passed since that stamp.  So the data becomes usable exactly
+// T after its publication -- hidden when it arrived early, on the critical
+// path when it did not: the cost of the xGMI hop a one-GPU run lacks.
+#ifdef HIPDSML_MEASURE
+__device__ int g_pk_hop;
+constexpr int kHopItems = 16 + kPxSlotsG;
+__device__ uint64_t g_pk_hop_st[4][kHopItems];
+__device__ __forceinline__ void hop_stamp(const PersistArgs& a, uint64_t s, int item) {
+  if (!a.mirror || g_pk_hop == 0 || (threadIdx.x & 63) != 0) return;
+  const uint64_t v = ((uint64_t)(uint32_t)(s + 1) << 32) | (uint32_t)__builtin_amdgcn_s_memrealtime();
+  __hip_atomic_store(&g_pk_hop_st[s & 3][item], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void hop_wait(const PersistArgs& a, uint64_t s, int item) {
+  const int hop = g_pk_hop;
+  if (!a.mirror || hop == 0) return;
+  uint64_t v;
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + a.timeout_ticks;
+  do {
+    v = __hip_atomic_load(&g_pk_hop_st[s & 3][item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } while ((uint32_t)(v >> 32) != (uint32_t)(s + 1) && __builtin_amdgcn_s_memrealtime() < t_end);
+  while ((uint32_t)__builtin_amdgcn_s_memrealtime() - (uint32_t)v < (uint32_t)hop &&
+         __builtin_amdgcn_s_memrealtime() < t_end)
+    __builtin_amdgcn_s_sleep(1);
+}
+#else
+__device__ __forceinline__ void hop_stamp(const PersistArgs&, uint64_t, int) {}
+__device__ __forceinline__ void hop_wait(const PersistArgs&, uint64_t, int) {}
+#endif
+
 // One wave's slot: push v into every peer, raise their flags, wait for every
 // peer's slot of step s here, then v = the rank-ordered sum over all
 // replicas.  false: a peer did not arrive in time.
@@ -544,6 +579,7 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint64_t tag = s + 1;
+  hop_stamp(a, s, 16 + slot);  // measurement builds only
   // peers unrolled to compile-time indices: a.xt.buf[d] is then a kernarg
   // (scalar) load, not a vector load + vmcnt(0) (which would wait for the
   // previous peer's pushes) + a readfirstlane waterfall per store
@@ -573,6 +609,7 @@ __device__ __forceinline__ bool px_allreduce_wave(const PersistArgs& a, uint64_t
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   asm volatile("" ::: "memory");
   if (!ok) return false;
+  hop_wait(a, s, 16 + slot);  // measurement builds only
   const float* mine = a.xt.buf[a.rep] + poff + (int64_t)slot * kPxSlot;
   // every source's slot loaded first (all in flight together), then summed in
   // rank order
@@ -708,6 +745,7 @@ __device__ __forceinline__ bool px_allreduce_tagged_wave(const PersistArgs& a, u
   const int64_t poff = (int64_t)(s & 1) * a.xhalf;
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint32_t tag = (uint32_t)(s + 1);
+  hop_stamp(a, s, 16 + slot);  // measurement builds only
 #pragma unroll
   for (int d = 0; d < kMaxPeers; ++d) {
     if (d >= a.nrep || d == a.rep) continue;
@@ -765,6 +803,7 @@ __device__ __forceinline__ bool px_allreduce_tagged_wave(const PersistArgs& a, u
   }
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   if (!ok) return false;
+  hop_wait(a, s, 16 + slot);  // measurement builds only
   float4 acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -860,6 +899,8 @@ __device__ __forceinline__ bool px_tagged_gather(const PersistArgs& a, uint64_t 
   ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
   if (!ok) return false;
 #pragma unroll
+  for (int k = 0; k < NS; ++k) hop_wait(a, s, 16 + slot0 + k);  // measurement builds only
+#pragma unroll
   for (int k = 0; k < NS; ++k) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -885,6 +926,9 @@ __device__ __forceinline__ void px_tagged_push_part(const PersistArgs& a, uint64
   const int64_t per_src = (int64_t)a.pxslots * kPxSlot;
   const uint32_t tag = (uint32_t)(s + 1);
   nu4v lo[3], hi[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (k < ns) hop_stamp(a, s, 16 + slot0 + k);  // measurement builds only
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     lo[k] = nu4v{__float_as_uint(v[k].x), tag, __float_as_uint(v[k].y), tag};
@@ -1460,7 +1504,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
 #pragma unroll
       for (int r2 = 0; r2 < kMaxPeers; ++r2)
         if (r2 < rhi && r2 != a.rep) need |= 1u << r2;
-      bool pok = true;
+      bool pok = true, peer_rows = false;
       poll.start();
       while (need != 0u) {
         nu4v v0[kMaxPeers], v1[kMaxPeers];
@@ -1485,10 +1529,12 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
             d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
             d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
             need &= ~(1u << r2);
+            peer_rows = peer_rows || r2 != a.rep;
           }
         }
         if (need != 0u && !poll.again()) { pok = false; break; }
       }
+      if (pok && peer_rows) hop_wait(a, s, 4 * (m >> 4) + (gn & 3));  // measurement builds only
       ok = __syncthreads_and(pok ? 1 : 0) != 0;
       if (!ok) break;
     }
@@ -1723,6 +1769,7 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
 #pragma unroll
       for (int r2 = 0; r2 < kMaxPeers; ++r2)
         if (r2 >= h0 && r2 < h1) need |= 1u << r2;
+      const bool peer_rows = h1 - h0 > 1 || h0 != a.rep;
       poll.start();
       while (need != 0u) {
         nu4v v0[kMaxPeers], v1[kMaxPeers];
@@ -1754,6 +1801,7 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
         }
         if (need != 0u && !poll.again()) { ok = false; break; }
       }
+      if (ok && peer_rows) hop_wait(a, s, 4 * (m >> 4) + (gn & 3));  // measurement builds only
       ok = __syncthreads_and(ok ? 1 : 0) != 0;
       if (!ok) break;
     }
@@ -2009,6 +2057,7 @@ __device__ __forceinline__ void pk_publish_dz1(const PersistArgs& a, __amdgpu_bu
       __builtin_amdgcn_raw_buffer_store_b128(pr[tt][k], rb, (int)((g0 + off[tt][k]) * 8), 0, kSc1);
   if constexpr (XM) {
     const int64_t base = pk_dzr_base(a, s, a.rep);
+    hop_stamp(a, s, 4 * (rb0 >> 4) + w);  // measurement builds: the rows' publish time
 #pragma unroll
     for (int d = 0; d < kMaxPeers; ++d) {
       if (d >= a.nrep || d == a.rep) continue;
@@ -3184,6 +3233,12 @@ void mlp_persist_set_jitter(int ticks) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_jitter), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
 }
+#ifdef HIPDSML_MEASURE
+void mlp_persist_set_hop(int ticks) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_hop), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
+}
+#endif
 void mlp_persist_set_probe(int mode) {
   g_pk_probe_mode = mode;
   const int v = mode == 1 ? 1 : 0;

@@ -116,6 +116,12 @@ class WideMlpTrainer:
         self.views = self.layout.views(self._P)
         self.gviews = self.layout.views(self.G)
         self.fused_head = d[L] <= 16 and self.pd[L - 1] <= 4096
+        # the last hidden layer's split-K GEMM hands its raw slices to the head,
+        # which sums them in slice order as it loads H (bias + ReLU on load,
+        # H written back for the weight update): no ticket / combine / epilogue
+        # tail in that GEMM (HIPDSML_WIDE_HEAD_SLABS=0: the in-GEMM combine)
+        self.head_slabs = (os.environ.get("HIPDSML_WIDE_HEAD_SLABS", "1") == "1" and self.fused_head
+                           and L >= 2 and batch <= 64 and d[L - 1] % 64 == 0)
         # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
         self.plans: Dict[str, tuple] = {}
         for l in range(L):
@@ -267,6 +273,31 @@ class WideMlpTrainer:
     def _plan(self, name: str, M: int, N: int, K: int, nn: bool) -> None:
         self.plans[name] = (M, N, K, nn, self.C.gemm_skinny_splits(M, N, K, 0))
 
+    def _slab_plan(self, l: int) -> int:
+        """Slices of layer l's forward GEMM when the head combines them (0: the
+        GEMM combines them itself)."""
+        if not self.head_slabs or l != self.L - 2 or self.xact:
+            return 0
+        M, N, K, nn, S = self.plans[f"f{l}"]
+        if self.gemm == "rows64" or K < 1024 or S not in (2, 4, 8):
+            return 0
+        return S
+
+    def _last_hidden_and_head(self, cur_prev: torch.Tensor, W_head: torch.Tensor, rows: int, y: torch.Tensor,
+                              logits, stats, dzp) -> None:
+        """H_{L-1} = relu(H_{L-2} W^T + b) as raw split-K slices, then the head
+        (kernels/head_row.h) sums them while it loads H, writes H_{L-1} back and
+        runs the classifier + softmax-CE (+ dZ_{L-1})."""
+        C, d, L = self.C, self.spec.dims, self.L
+        l = L - 2
+        M, N, K, nn, S = self.plans[f"f{l}"]
+        _, b = self.views[l]
+        _, bh = self.views[L - 1]
+        C.gemm_skinny(self.H[l], cur_prev, rows, N, K, nn=False, ws=self.Cp, raw=True)
+        C.head_softmax_xent(self.H[L - 1], W_head, bh, rows, self.pd[L - 1], d[L], y, 1.0 / rows, logits,
+                            self.dZ[L], None, stats, dzp=dzp, row_stats=True, hs=self.Cp, hs_splits=S,
+                            hs_bias=b, hs_relu=True)
+
     def _gemm(self, name: str, A: torch.Tensor, B: torch.Tensor, rows: int = 0, **epi) -> None:
         """One skinny GEMM with its epilogue fused (split-K combined in-kernel
         by the last slice of each tile to arrive); `rows` < batch for a short
@@ -288,14 +319,20 @@ class WideMlpTrainer:
         cur = [self.Wb[l][p] for l in range(L)]       # this step's weights
         nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
         self.H[0] = self._xb_rows(bi)  # this batch's bf16 rows (a view: no copy)
+        slabs = self._slab_plan(L - 2)
         for l in range(L - 1):
+            if slabs and l == L - 2:
+                break  # the head combines this layer's GEMM (below)
             _, b = self.views[l]
             A = self.Xblk[:, r0:r0 + Bt] if l == 0 and self.Xblk is not None else self.H[l]
             self._gemm(f"f{l}", A, cur[l], bias=b, relu=True, obf=self.H[l + 1])
             if self.xact:
                 self._gather(self.Hall[l + 1])
         _, b = self.views[L - 1]
-        if self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
+        if slabs:
+            self._last_hidden_and_head(cur[L - 2], cur[L - 1], Bt, self.y[r0:r0 + Bt], self.logits, self.stats,
+                                       self.dZ[L - 1])
+        elif self.fused_head:  # classifier GEMM + softmax-CE in one kernel (one block per row),
             # plus the next activation gradient dZ_{L-1} from the W / H chunks it holds
             prev = L >= 2
             C.head_softmax_xent(self.H[L - 1], cur[L - 1], b, Bt, self.pd[L - 1], d[L],
@@ -483,12 +520,17 @@ class WideMlpTrainer:
                 m = min(Bt, n - r0)
                 C.cast_transpose(X[r0:r0 + m], m, d[0], xb, None)
                 self.H[0] = xb
+                slabs = self._slab_plan(L - 2)
                 for l in range(L - 1):
+                    if slabs and l == L - 2:
+                        break
                     _, b = self.views[l]
                     self._gemm(f"f{l}", self.H[l], self.wb(l), rows=m, bias=b, relu=True,
                                obf=self.H[l + 1])
                 _, b = self.views[L - 1]
-                if self.fused_head:
+                if slabs:
+                    self._last_hidden_and_head(self.wb(L - 2), self.wb(L - 1), m, y[r0:r0 + m], None, st, None)
+                elif self.fused_head:
                     C.head_softmax_xent(self.H[L - 1], self.wb(L - 1), b, m, self.pd[L - 1], d[L],
                                         y[r0:r0 + m], 1.0 / m, None, self.dZ[L], None, st,
                                         row_stats=True)

@@ -212,3 +212,91 @@ def test_data_parallel_forms_mirrored_replicas(algo, n, helpers):
     want, _ = _ref(ds, 15)
     err = (t.P.cpu() - want).abs().max().item()
     assert err < 2e-5, err
+
+
+def _replay_group(algo, n, shards):
+    """n persistent-step instances on one GPU, instance r holding shard r, wired
+    into one local exchange group as ranks 0..n-1 (data-parallel persistent
+    step `algo`), with the all-gathered inputs / cross-replica Gram tables the
+    real job builds from the distinct shards."""
+    from hipdsml.ops.native import require_native
+    from hipdsml.parallel.xchg import make_local_group, swizzle_inputs
+
+    C = require_native()
+    trs = [MlpTrainer(SPEC, ds, batch=64, lr=0.05, ctx=DistContext(device=DEV), seed=3, persist=True,
+                      persist_place_trials=1) for ds in shards]
+    nb = trs[0].nbatches
+    plain = torch.stack([t.X[: nb * 64, :784] for t in trs]).contiguous()  # [n][rows][784], rank order
+    half, ntiles = C.MlpRunner.persist_xchg_size(n, algo)
+    xs = make_local_group(None, [0] * n, 5000.0, half_floats=half, ntiles=ntiles)
+    xall = swizzle_inputs(plain, 64) if algo == 4 else None
+    for r, t in enumerate(trs):
+        t.runner.set_world_size(n)
+        if algo >= 2:
+            t.runner.set_persist_gram(C.gram_table(plain, t.X, nb, 64, 784))
+        if xall is not None:
+            t.runner.set_persist_xall(xall, xall[0].numel())
+        t.runner.set_persist(t.pk_buf, t.pk_err, 5000.0, xs[r], algo)
+    return C, trs, xs
+
+
+def _replay_steps(C, trs, xs, r, algo, steps):
+    """Replay: replica r runs the n-rank persistent step one launch per step
+    (its pipeline state carried from launch to launch), and before each of its
+    launches every peer r' != r runs that step once as a CAPTURE: a fresh
+    (uncarried) one-step launch of the same kernel on r's current weights and
+    step counter -- the weights every replica holds at that step, since
+    replicas stay identical -- with its own shard.  The capture's pushes land
+    in r's receive buffer exactly as a real peer's would (its dZ1 rows, its
+    gradient-tile / layer-1 slots, tags and flags), computed from distinct data
+    by the real kernel; its own sums run in the probe test mode (peers taken
+    as arrived: its state is thrown away).  Then r's launch finds every peer's
+    data of the step in place and must produce n-replica SGD."""
+    t = trs[r]
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        C.mlp_persist_set_probe(1)
+        try:
+            for rp, tp in enumerate(trs):
+                if rp == r:
+                    continue
+                tp.P.copy_(t.P)
+                tp.ctr.copy_(t.ctr)
+                tp.runner.set_persist_carry(False)
+                xs[rp].fill_flags(1 << 62)  # its own flags preset (the probe's rule): it never waits
+                tp.train_steps(1)
+                tp.synchronize()
+        finally:
+            C.mlp_persist_set_probe(0)
+        torch.cuda.synchronize()
+        t.train_steps(1)
+        t.synchronize()
+
+
+@pytest.mark.parametrize("algo,n,r", [(4, 4, 0), (4, 4, 1), (4, 4, 3), (4, 8, 0), (4, 8, 1), (4, 8, 7),
+                                      (2, 4, 1), (2, 8, 7), (0, 4, 2)], ids=lambda v: str(v))
+def test_pkx_replay_distinct_peers(algo, n, r):
+    """VERDICT r5 Next #1: the N >= 4 data-parallel persistent code (pkx's
+    helper split and pusher blocks switch on from 4 replicas) on DISTINCT
+    replica data, which mirror mode (every peer an exact copy) cannot check: a
+    rank-offset or slot-permutation bug there passes mirror mode but not this.
+    Replica r's parameters after 7 steps (3-slot dZ1 rotation, both parities,
+    an epoch wrap) must match fp32 torch SGD on the global batch of n shards."""
+    shards = [synthetic_mnist(64 * 4, seed=300 + k) for k in range(n)]
+    C, trs, xs = _replay_group(algo, n, shards)
+    steps = 7
+    _replay_steps(C, trs, xs, r, algo, steps)
+    lay = MlpLayout(SPEC, 64, 4)
+    P = init_params(lay, 3, "reference")
+    for s in range(steps):
+        b = s % 4
+        g = sum(grads_ref(lay, P, ds.X[b * 64:(b + 1) * 64], ds.y[b * 64:(b + 1) * 64])[0] for ds in shards)
+        P = P - 0.05 * g / n
+    err = (trs[r].P.cpu() - P).abs().max().item()
+    assert err < 2e-5, err
+    # and the replay is not vacuous: the shards differ, so single-shard SGD is far off
+    P1 = init_params(lay, 3, "reference")
+    for s in range(steps):
+        b = s % 4
+        P1 = P1 - 0.05 * grads_ref(lay, P1, shards[r].X[b * 64:(b + 1) * 64], shards[r].y[b * 64:(b + 1) * 64])[0]
+    assert (trs[r].P.cpu() - P1).abs().max().item() > 100 * err

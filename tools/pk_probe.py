@@ -12,7 +12,15 @@ rows by their tags, which no preset can match: the probe switch of the kernel
 copies of this replica's swizzled shard as the all-gathered inputs.
 
 Prints one JSON line per N, with the exchange bytes each replica sends per
-step (to all peers) from the kernel's slot layout."""
+step (to all peers) from the kernel's slot layout.
+
+--mirror runs the kernel's MIRROR test mode instead: every push to a peer
+lands in this replica's own receive buffer in that peer's slot, with real tags
+and flags, so the replica waits for its own pushes exactly as for a peer's.
+With --hop-us T1,T2,... (measurement build: python -m hipdsml._build
+--measure) every such hop becomes usable only T us after its publication
+(kernels/mlp_persist.hip g_pk_hop): the step time at each T prices what the
+xGMI latency a one-GPU run lacks costs each form (one line per N and T)."""
 import argparse
 import json
 import os
@@ -57,7 +65,14 @@ def main() -> int:
                          "us_per_step = the fastest, place_us = all)")
     ap.add_argument("--algo", type=int, default=0,
                     help="0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx (exchange-free layer 1)")
+    ap.add_argument("--mirror", action="store_true",
+                    help="mirror test mode (pushes loop back with real tags / flags) instead of the probe")
+    ap.add_argument("--hop-us", default="",
+                    help="mirror mode, measurement build: extra one-way hop latencies to sweep (us)")
     a = ap.parse_args()
+    hops = [float(x) for x in a.hop_us.split(",")] if a.hop_us else [0.0]
+    if a.hop_us and not a.mirror:
+        ap.error("--hop-us needs --mirror")
     import torch
 
     from hipdsml.data.mnist import synthetic_mnist
@@ -78,8 +93,9 @@ def main() -> int:
         if n > 1:
             half, ntiles = C.MlpRunner.persist_xchg_size(n, a.algo)
             xs = make_local_group(None, [0] * n, 5000.0, half_floats=half, ntiles=ntiles)
-            for x in xs:
-                x.fill_flags(1 << 62)
+            if not a.mirror:
+                for x in xs:
+                    x.fill_flags(1 << 62)
             tr.runner.set_world_size(n)
             if a.algo >= 2:
                 from hipdsml.parallel.xchg import swizzle_inputs
@@ -92,6 +108,8 @@ def main() -> int:
                     xall = swizzle_inputs(Xs.reshape(n, nb * 64, 784), 64)
                     tr.runner.set_persist_xall(xall, xall[0].numel())
                 C.mlp_persist_set_probe(1)
+            if a.mirror:
+                C.mlp_persist_set_probe(2)
             tr.runner.set_persist(tr.pk_buf, tr.pk_err, 5000.0, xs[0], a.algo)
         torch.cuda.synchronize()
 
@@ -109,6 +127,19 @@ def main() -> int:
             tr.synchronize()
             return (time.perf_counter() - t0) / a.steps
 
+        if a.hop_us:
+            assert C.measure_build, "--hop-us needs the measurement build (python -m hipdsml._build --measure)"
+            for hop in hops:
+                C.mlp_persist_set_hop(hop)  # takes effect at the next launch (tags keep rising)
+                dt = timed()
+                print(json.dumps({"mode": ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo] if n > 1 else "none",
+                                  "ranks": n, "mirror": True, "hop_us": hop,
+                                  "us_per_step": round(dt * 1e6, 2)}), flush=True)
+            C.mlp_persist_set_hop(0)
+            C.mlp_persist_set_probe(0)
+            del tr, xs
+            torch.cuda.synchronize()
+            continue
         place_us = []
         cands = [tr.pk_buf]
         best_dt, best_buf = None, tr.pk_buf
@@ -145,7 +176,7 @@ def main() -> int:
                                     "stamps": stamps}) + "\n")
         C.mlp_persist_set_probe(0)
         name = ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo]
-        print(json.dumps({"mode": name if n > 1 else "none", "ranks": n,
+        print(json.dumps({"mode": name if n > 1 else "none", "ranks": n, "mirror": a.mirror,
                           "us_per_step": round(dt * 1e6, 2), "place_us": place_us,
                           "bytes_out_per_step": pk_bytes_out(n, a.algo),
                           "bytes_per_peer_per_step": pk_bytes_out(n, a.algo) // max(n - 1, 1)}),
