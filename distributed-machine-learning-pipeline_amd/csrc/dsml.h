@@ -117,6 +117,8 @@ void mlp_persist_set_hop(int ticks);  // measurement builds: extra hop latency i
 // pkx dW1 helper blocks per layer-1 block: -1 the default (3 from 4 replicas on,
 // else 0; HIPDSML_PKX_HELPERS overrides it), 0, 1 or 3 (tuning / testing)
 void mlp_persist_set_pkx_helpers(int helpers);
+// pkx: the dZ1 rows leave from the layer-1 owner blocks (1) or the chains (0); -1 the default
+void mlp_persist_set_pkx_l1push(int mode);
 // Single replica: the Gram table the persistent step reads, float[nbatches][64][64]
 // with G1T[b][m'][m] = X_{b-1}[m'] . X_b[m] + 1 (rows past the batch repeat its
 // last row; b - 1 wraps), and `carry` = 1 when the hand-off buffer still holds
@@ -340,6 +342,16 @@ struct WgLayer {
   int64_t ldwh;
   uint16_t* Wl;
   int64_t ldwl;
+  // Z from the raw split-K slices of the dgrad that produced it (gemm_skinny
+  // raw_slabs) instead of Z: Z[m][n] = bf16(zmask[m][n] > 0 ? sum_{z < zsS}
+  // zs[z * zs_stride + (n / 64) * 4096 + m * 64 + n % 64] : 0), slices summed in
+  // slice order -- the dgrad's own combine + ReLU'-mask epilogue, bit for bit.
+  // 64 x 64 tiles, M <= 64, N % 64 == 0.
+  const float* zs;
+  int zsS;
+  int64_t zs_stride;
+  const uint16_t* zmask;
+  int64_t ldzm;
 };
 // fp32 <-> split master (hi: bf16 rounded half away from zero, lo: int16 remainder)
 hipError_t hilo_split(const float* W, int N, int K, int64_t ldw, uint16_t* hi, int64_t ldh, uint16_t* lo,

@@ -420,6 +420,10 @@ static int g_pk_probe_mode = 0;
 // pkx helper count override (-1: the default by replica count; set from
 // HIPDSML_PKX_HELPERS at the first data-parallel launch)
 static int g_pkx_helpers = -2;
+// pkx dZ1 row pushes from the layer-1 owner blocks (1) or the chains (0): the
+// default, and the HIPDSML_PKX_L1PUSH override (-2: not read yet, -1: none)
+constexpr int kPkxL1PushDefault = 0;
+static int g_pkx_l1push = -2;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;
   uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
@@ -494,6 +498,8 @@ struct PersistArgs {
   int32_t mirror;   // testing only (g_pk_probe_mode 2): pushes loop back into this replica's buffer
   int32_t probe;    // testing only (g_pk_probe_mode 1): peers' tagged data taken as arrived
   int32_t pushers;  // Gram forms, tagged tile sums: the tiles' slots pushed by pusher blocks
+  int32_t l1push;   // pkx: the replica's dZ1 rows go to the peers from the layer-1 owner blocks
+                    // (block (gn, gk) sends column tile gn to peer rep + 1 + gk), not the chains
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -1496,6 +1502,14 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       const int off = (m * kD1 + n0 + 4 * qq) * 8;
       const int64_t gl = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
       const float* rbase = a.xt.buf[a.rep];
+      // pkx l1push: this block sends the replica's own rows of column tile gn
+      // to ONE peer as soon as they are here -- the 7 gk blocks of a tile
+      // cover up to 7 peers, so a replica's 64 KB a peer leave from 56 CUs
+      // instead of queueing behind each other in the 4 chains' CUs
+      int push_d = -1;
+      if constexpr (XL) {
+        if (a.l1push && gk < a.nrep - 1) push_d = __builtin_amdgcn_readfirstlane((a.rep + 1 + gk) % a.nrep);
+      }
       uint32_t need = 1u << a.rep;  // replicas whose rows this thread still waits for
       // gatherers: every replica (the correction); other pkx owners: only the
       // replicas of their own dW1 part (the helpers read theirs) -- the exchange
@@ -1528,6 +1542,13 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
             float* d = r2 == a.rep ? Dz + m * 17 + 4 * qq : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
             d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
             d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
+            if (XL && r2 == a.rep && push_d >= 0) {
+              hop_stamp(a, s, 4 * w + (gn & 3));  // measurement builds only
+              const __amdgpu_buffer_rsrc_t rp = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, push_d)
+                                                              : a.xt.buf[push_d] + pk_dzr_base(a, s, a.rep));
+              __builtin_amdgcn_raw_buffer_store_b128(v0[r2], rp, off, 0, kScSys);
+              __builtin_amdgcn_raw_buffer_store_b128(v1[r2], rp, off + 16, 0, kScSys);
+            }
             need &= ~(1u << r2);
             peer_rows = peer_rows || r2 != a.rep;
           }
@@ -2056,6 +2077,7 @@ __device__ __forceinline__ void pk_publish_dz1(const PersistArgs& a, __amdgpu_bu
     for (int k = 0; k < 2; ++k)
       __builtin_amdgcn_raw_buffer_store_b128(pr[tt][k], rb, (int)((g0 + off[tt][k]) * 8), 0, kSc1);
   if constexpr (XM) {
+    if (a.l1push) return;  // the layer-1 owner blocks send the rows on (pk_l1_gram)
     const int64_t base = pk_dzr_base(a, s, a.rep);
     hop_stamp(a, s, 4 * (rb0 >> 4) + w);  // measurement builds: the rows' publish time
 #pragma unroll
@@ -2078,6 +2100,7 @@ __device__ __forceinline__ void pk_publish_dz1(const PersistArgs& a, __amdgpu_bu
 // on the tiles' path.
 __device__ __forceinline__ void pk_drain_rows(int nrep) {
   switch (nrep) {
+    case 1: __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;  // local dZ1 stores only
     case 2: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 3: __asm__ volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 4: __asm__ volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
@@ -2465,7 +2488,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
 
     // ---- the rest of the rows (stored before the dZ1 stage): drained by every
     // wave, then flagged behind the barrier ----
-    if constexpr (XM) pk_drain_rows(a.nrep);
+    if constexpr (XM) pk_drain_rows(a.l1push ? 1 : a.nrep);  // l1push: no peer pushes here
     else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     if (tid == 0) st_gran(rb, kOffCxf + 8 + par * kNCH + c, __uint_as_float(tag), tag);
@@ -3246,6 +3269,7 @@ void mlp_persist_set_probe(int mode) {
   (void)hipDeviceSynchronize();
 }
 void mlp_persist_set_pkx_helpers(int helpers) { g_pkx_helpers = helpers < 0 ? -1 : helpers; }
+void mlp_persist_set_pkx_l1push(int mode) { g_pkx_l1push = mode < 0 ? -1 : (mode ? 1 : 0); }
 void mlp_persist_set_stamp_window(int first_step) {
   const int v = first_step < 0 ? 0 : first_step + 1;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
@@ -3384,6 +3408,13 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
     // gather never queues behind its own pushes; with fewer peers the tile's
     // spare wave pushes them itself (a staging hop would cost more)
     a.pushers = ((algo == 2 || algo == 4) && a.nrep >= 4) ? 1 : 0;
+    // pkx: the dZ1 rows leave from the layer-1 owner blocks (HIPDSML_PKX_L1PUSH
+    // overrides: 0 the chains push them, 1 the owners)
+    if (g_pkx_l1push == -2) {
+      const char* e = getenv("HIPDSML_PKX_L1PUSH");
+      g_pkx_l1push = e != nullptr && *e ? atoi(e) : -1;
+    }
+    a.l1push = algo == 4 ? (g_pkx_l1push >= 0 ? (g_pkx_l1push ? 1 : 0) : kPkxL1PushDefault) : 0;
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)
     if (algo < 2) a.carry = 0;

@@ -171,10 +171,12 @@ def test_persistent_uneven_load_is_bit_exact(spec):
     assert torch.equal(a.P, b.P)
 
 
-@pytest.mark.parametrize("algo,n,helpers", [(4, 2, -1), (4, 3, -1), (4, 4, -1), (4, 8, -1), (4, 8, 1), (4, 6, -1),
-                                            (4, 2, 1), (4, 4, 0), (2, 4, -1), (2, 8, -1), (0, 4, -1)],
+@pytest.mark.parametrize("algo,n,helpers,l1push", [(4, 2, -1, -1), (4, 3, -1, -1), (4, 4, -1, -1), (4, 8, -1, -1),
+                                                   (4, 8, 1, -1), (4, 6, -1, -1), (4, 2, 1, -1), (4, 4, 0, -1),
+                                                   (4, 8, -1, 1), (4, 8, -1, 0), (4, 3, -1, 1), (2, 4, -1, -1),
+                                                   (2, 8, -1, -1), (0, 4, -1, -1)],
                          ids=lambda v: str(v))
-def test_data_parallel_forms_mirrored_replicas(algo, n, helpers):
+def test_data_parallel_forms_mirrored_replicas(algo, n, helpers, l1push):
     """One GPU runs the n-replica persistent step (pk = 0, pkg = 2, pkx = 4)
     against n - 1 exact copies of itself: in the kernel's mirror test mode every
     push to peer d lands in this replica's OWN receive buffer, in d's source
@@ -201,6 +203,7 @@ def test_data_parallel_forms_mirrored_replicas(algo, n, helpers):
         t.runner.set_persist_xall(xall, xall[0].numel())
     C.mlp_persist_set_probe(2)
     C.mlp_persist_set_pkx_helpers(helpers)  # pkx: the dW1 split over 0 / 1 / 3 helper blocks
+    C.mlp_persist_set_pkx_l1push(l1push)
     try:
         t.runner.set_persist(t.pk_buf, t.pk_err, 5000.0, xs[0], algo)
         for k in (5, 1, 9):  # launch splits: carried state, parity and slot reuse
@@ -209,6 +212,7 @@ def test_data_parallel_forms_mirrored_replicas(algo, n, helpers):
     finally:
         C.mlp_persist_set_probe(0)
         C.mlp_persist_set_pkx_helpers(-1)
+        C.mlp_persist_set_pkx_l1push(-1)
     want, _ = _ref(ds, 15)
     err = (t.P.cpu() - want).abs().max().item()
     assert err < 2e-5, err
@@ -273,9 +277,11 @@ def _replay_steps(C, trs, xs, r, algo, steps):
         t.synchronize()
 
 
-@pytest.mark.parametrize("algo,n,r", [(4, 4, 0), (4, 4, 1), (4, 4, 3), (4, 8, 0), (4, 8, 1), (4, 8, 7),
-                                      (2, 4, 1), (2, 8, 7), (0, 4, 2)], ids=lambda v: str(v))
-def test_pkx_replay_distinct_peers(algo, n, r):
+@pytest.mark.parametrize("algo,n,r,l1push", [(4, 4, 0, -1), (4, 4, 1, -1), (4, 4, 3, -1), (4, 8, 0, -1),
+                                             (4, 8, 1, -1), (4, 8, 7, -1), (4, 8, 3, 1), (4, 4, 2, 1), (4, 2, 1, 1),
+                                             (4, 8, 5, 0), (2, 4, 1, -1), (2, 8, 7, -1), (0, 4, 2, -1)],
+                         ids=lambda v: str(v))
+def test_pkx_replay_distinct_peers(algo, n, r, l1push):
     """VERDICT r5 Next #1: the N >= 4 data-parallel persistent code (pkx's
     helper split and pusher blocks switch on from 4 replicas) on DISTINCT
     replica data, which mirror mode (every peer an exact copy) cannot check: a
@@ -285,7 +291,11 @@ def test_pkx_replay_distinct_peers(algo, n, r):
     shards = [synthetic_mnist(64 * 4, seed=300 + k) for k in range(n)]
     C, trs, xs = _replay_group(algo, n, shards)
     steps = 7
-    _replay_steps(C, trs, xs, r, algo, steps)
+    C.mlp_persist_set_pkx_l1push(l1push)  # pkx: dZ1 rows pushed by the chains (0) / layer-1 owners (1)
+    try:
+        _replay_steps(C, trs, xs, r, algo, steps)
+    finally:
+        C.mlp_persist_set_pkx_l1push(-1)
     lay = MlpLayout(SPEC, 64, 4)
     P = init_params(lay, 3, "reference")
     for s in range(steps):

@@ -65,6 +65,8 @@ def main() -> int:
                          "us_per_step = the fastest, place_us = all)")
     ap.add_argument("--algo", type=int, default=0,
                     help="0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx (exchange-free layer 1)")
+    ap.add_argument("--l1push", type=int, default=-1,
+                    help="pkx dZ1 row pushes: 1 from the layer-1 owner blocks, 0 from the chains, -1 default")
     ap.add_argument("--mirror", action="store_true",
                     help="mirror test mode (pushes loop back with real tags / flags) instead of the probe")
     ap.add_argument("--hop-us", default="",
@@ -84,6 +86,7 @@ def main() -> int:
 
     C = require_native()
     C.mlp_persist_set_pkx_helpers(a.helpers)
+    C.mlp_persist_set_pkx_l1push(a.l1push)
     dev = torch.device("cuda", 0)
     for n in [int(x) for x in a.ranks.split(",")]:
         tr = MlpTrainer(MlpSpec((784, 128, 64, 10)), synthetic_mnist(64 * 100, seed=0),
@@ -173,10 +176,11 @@ def main() -> int:
             stamps = decode(C.mlp_persist_stamps(), tr.spec)
             with open(a.stamps, "a") as f:
                 f.write(json.dumps({"mode": ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo], "ranks": n,
+                                    "mirror": a.mirror, "l1push": a.l1push,
                                     "stamps": stamps}) + "\n")
         C.mlp_persist_set_probe(0)
         name = ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo]
-        print(json.dumps({"mode": name if n > 1 else "none", "ranks": n, "mirror": a.mirror,
+        print(json.dumps({"mode": name if n > 1 else "none", "ranks": n, "mirror": a.mirror, "l1push": a.l1push,
                           "us_per_step": round(dt * 1e6, 2), "place_us": place_us,
                           "bytes_out_per_step": pk_bytes_out(n, a.algo),
                           "bytes_per_peer_per_step": pk_bytes_out(n, a.algo) // max(n - 1, 1)}),
