@@ -671,7 +671,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (auto G = opt(t[9])) { chk2(*G, "G"); check_f32(*G, "G"); a.G = G->data_ptr<float>(); a.ldg = G->stride(0); }
     if (auto b = opt(t[10])) { check_f32(*b, "bias"); TORCH_CHECK(b->numel() >= N, "bias"); a.bias = b->data_ptr<float>(); }
     if (auto bg = opt(t[11])) { check_f32(*bg, "bgrad"); TORCH_CHECK(bg->numel() >= N, "bgrad"); a.bgrad = bg->data_ptr<float>(); }
-    if (t.size() == 14) {  // split master: this step's hi words + the int16 remainders
+    if (t.size() >= 14) {  // split master: this step's hi words + the int16 remainders
       if (auto Wh = opt(t[12])) { chk2(*Wh, "Wh"); a.Wh = bf16p(*Wh, "Wh"); a.ldwh = Wh->stride(0); }
       if (auto Wl = opt(t[13])) {
         chk2(*Wl, "Wl");

@@ -140,7 +140,6 @@ __device__ __forceinline__ void wg_load_hl(const WgArgs& a, int kt, int nt, uint
 
 // 2. Z[mb.., n0..] and X[mb.., k0..] as row-major images: 2 LDS-DMA pieces per wave each
 // (zpre: the Z image is already in LDS -- a hand-off written by this launch)
-template <bool ZS = false>
 __device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb, char* lds,
                                          bool zpre = false) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -153,36 +152,9 @@ __device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb
     const int m = min(mb + r, a.M - 1);
     const int zc = min(n0 + 8 * (p ^ wg_swz(r)), (int)((a.N + 7) & ~7) - 8);
     const int xc = min(k0 + 8 * (p ^ wg_swz(r)), (int)((a.K + 7) & ~7) - 8);
-    if (ZS && !zpre) {
-      // the dgrad's raw slices summed in slice order + its ReLU'-mask epilogue
-      // (gemm_skinny's combine: 0 + slice 0 + slice 1 ...; x * 1 + 0; masked
-      // to 0; bf16), written where the LDS-DMA would have put chunk zc.  Slices
-      // one after the other (unroll 1): the whole set in flight took 168
-      // VGPRs, which would cost every tile of the launch its occupancy.
-      const float* src = a.zs + (int64_t)(zc >> 6) * 4096 + m * 64 + (zc & 63);
-      const uint4 mk = *reinterpret_cast<const uint4*>(a.zmask + (int64_t)m * a.ldzm + zc);
-      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int z = 0; z < a.zsS; ++z) {
-        const float4 s0 = *reinterpret_cast<const float4*>(src + z * a.zs_stride);
-        const float4 s1 = *reinterpret_cast<const float4*>(src + z * a.zs_stride + 4);
-        x[0] += s0.x; x[1] += s0.y; x[2] += s0.z; x[3] += s0.w;
-        x[4] += s1.x; x[5] += s1.y; x[6] += s1.z; x[7] += s1.w;
-      }
-      const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
-      uint32_t q[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t mb16 = e & 1 ? mw[e >> 1] >> 16 : mw[e >> 1] & 0xffffu;
-        const float y = x[e] * 1.0f + 0.f;
-        q[e] = bf16_to_f32(mb16) > 0.f ? f32_to_bf16(y) : f32_to_bf16(0.f);
-      }
-      *reinterpret_cast<uint4*>(imz + piece * 1024 + lane * 16) =
-          make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
-    } else if (!zpre) {
+    if (!zpre)
       __builtin_amdgcn_global_load_lds((wg_gptr)(a.Z + (int64_t)m * a.ldz + zc),
                                        (wg_lptr)(imz + piece * 1024), 16, 0, 0);
-    }
     __builtin_amdgcn_global_load_lds((wg_gptr)(a.X + (int64_t)m * a.ldx + xc),
                                      (wg_lptr)(imx + piece * 1024), 16, 0, 0);
   }
@@ -190,7 +162,6 @@ __device__ __forceinline__ void wg_stage(const WgArgs& a, int k0, int n0, int mb
 
 // 2-4. One 64 (n) x 64 (k) tile of layer `a` (k tile kt, n tile nt) whose W
 // loads are already in flight in `wold`.
-template <bool ZS = false>
 __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt, char* lds,
                                                 const uint4 (&wr)[4], bool zpre = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -211,7 +182,7 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
 
   for (int mb = 0; mb < a.M; mb += 64) {
     // ---- 2. Z[mb.., n0..] and X[mb.., k0..] row-major images ----
-    wg_stage<ZS>(a, k0, n0, mb, lds, zpre);
+    wg_stage(a, k0, n0, mb, lds, zpre);
     full_barrier();  // every piece landed (vmcnt(0) also retires the W loads: issued earlier)
 
     // ---- 3. MFMAs: wave tile 32 n x 32 k, reduction over the batch rows ----
@@ -333,10 +304,47 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
   }
 }
 
+// Z image of n tile nt (rows 0..63, wg_stage's swizzled layout) from the raw
+// split-K slices of the dgrad that produced Z (WgLayer::zs): the slices summed
+// in slice order + the dgrad's ReLU'-mask epilogue (gemm_skinny's combine:
+// 0 + slice 0 + slice 1 ...; x * 1 + 0; masked to 0; bf16), written where the
+// LDS-DMA would have put each chunk.  Slices one after the other (unroll 1):
+// all in flight took 168 VGPRs, every tile of the launch its occupancy.
+__device__ __forceinline__ void wg_stage_zs(const WgArgs& a, int nt, char* lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) {
+    const int piece = 2 * w + pc;
+    const int r = 8 * piece + (lane >> 3), p = lane & 7;
+    const int m = min(r, a.M - 1);
+    const int zc = min(nt * 64 + 8 * (p ^ wg_swz(r)), a.N - 8);
+    const float* src = a.zs + (int64_t)(zc >> 6) * 4096 + m * 64 + (zc & 63);
+    const uint4 mk = *reinterpret_cast<const uint4*>(a.zmask + (int64_t)m * a.ldzm + zc);
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int z = 0; z < a.zsS; ++z) {
+      const float4 s0 = *reinterpret_cast<const float4*>(src + z * a.zs_stride);
+      const float4 s1 = *reinterpret_cast<const float4*>(src + z * a.zs_stride + 4);
+      x[0] += s0.x; x[1] += s0.y; x[2] += s0.z; x[3] += s0.w;
+      x[4] += s1.x; x[5] += s1.y; x[6] += s1.z; x[7] += s1.w;
+    }
+    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t mb16 = e & 1 ? mw[e >> 1] >> 16 : mw[e >> 1] & 0xffffu;
+      q[e] = bf16_to_f32((uint16_t)mb16) > 0.f ? (uint32_t)f32_to_bf16(x[e] * 1.0f + 0.f) : 0u;
+    }
+    *reinterpret_cast<uint4*>(lds + piece * 1024 + lane * 16) =
+        make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
+  }
+}
+
 template <bool ZS = false>
 __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
   // the tile's W words in one register set: fp32 W (4 float4), or for the
-  // split master {hi, lo} of rows (tid >> 3) and (tid >> 3) + 32
+  // split master {hi, lo} of rows (tid >> 3) and (tid >> 3) + 32 -- issued
+  // first, so their HBM round trip overlaps the operand staging and MFMAs
   uint4 wr[4];
   if (a.Wl) {
     wg_load_hl(a, kt, nt, wr);
@@ -346,8 +354,11 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr[j] = __builtin_bit_cast(uint4, wold[j]);
   }
-  if (ZS && a.zs != nullptr) wgrad_tile_body<true>(a, kt, nt, lds, wr);
-  else wgrad_tile_body<false>(a, kt, nt, lds, wr);
+  // Z from a dgrad's raw slices: summed into the LDS image here, then the
+  // ordinary tile with its Z image already in place
+  const bool zs = ZS && a.zs != nullptr;
+  if (zs) wg_stage_zs(a, nt, lds);
+  wgrad_tile_body(a, kt, nt, lds, wr, zs);
 }
 
 __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
