@@ -652,8 +652,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       return h.cast<torch::Tensor>();
     };
     py::tuple t = it.cast<py::tuple>();
-    TORCH_CHECK(t.size() == 12 || t.size() == 14 || t.size() == 17,
-                "wgrad layer: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl[, zs, zs_splits, zmask]])");
+    TORCH_CHECK(t.size() == 12 || t.size() == 14,
+                "wgrad layer: (Z, X, M, N, K, alpha, lr, W, Wb, G, bias, bgrad[, Wh, Wl])");
     torch::Tensor Z = t[0].cast<torch::Tensor>(), X = t[1].cast<torch::Tensor>();
     const int64_t M = t[2].cast<int64_t>(), N = t[3].cast<int64_t>(), K = t[4].cast<int64_t>();
     TORCH_CHECK(Z.dim() == 2 && X.dim() == 2 && Z.stride(1) == 1 && X.stride(1) == 1, "Z, X 2-D rows");
@@ -678,16 +678,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(Wl->scalar_type() == torch::kInt16, "Wl must be int16");
         a.Wl = reinterpret_cast<uint16_t*>(Wl->data_ptr<int16_t>()); a.ldwl = Wl->stride(0);
       }
-    }
-    if (t.size() == 17 && !t[14].is_none()) {
-      // Z as the raw split-K slices of the dgrad that produced it (+ its ReLU' mask)
-      torch::Tensor zs = t[14].cast<torch::Tensor>(), zm = t[16].cast<torch::Tensor>();
-      check_f32(zs, "zs");
-      const int64_t S = t[15].cast<int64_t>();
-      TORCH_CHECK(S >= 1 && S <= 8 && N % 64 == 0 && zs.numel() >= S * (N / 64) * 4096, "zs: S slices of N/64 tiles");
-      TORCH_CHECK(zm.dim() == 2 && zm.stride(1) == 1 && zm.size(0) >= M && zm.size(1) >= N, "zmask shape");
-      a.zs = zs.data_ptr<float>(); a.zsS = (int)S; a.zs_stride = (N / 64) * 4096;
-      a.zmask = bf16p(zm, "zmask"); a.ldzm = zm.stride(0);
     }
     return a;
   };

@@ -342,16 +342,6 @@ struct WgLayer {
   int64_t ldwh;
   uint16_t* Wl;
   int64_t ldwl;
-  // Z from the raw split-K slices of the dgrad that produced it (gemm_skinny
-  // raw_slabs) instead of Z: Z[m][n] = bf16(zmask[m][n] > 0 ? sum_{z < zsS}
-  // zs[z * zs_stride + (n / 64) * 4096 + m * 64 + n % 64] : 0), slices summed in
-  // slice order -- the dgrad's own combine + ReLU'-mask epilogue, bit for bit.
-  // 64 x 64 tiles, M <= 64, N % 64 == 0.
-  const float* zs;
-  int zsS;
-  int64_t zs_stride;
-  const uint16_t* zmask;
-  int64_t ldzm;
 };
 // fp32 <-> split master (hi: bf16 rounded half away from zero, lo: int16 remainder)
 hipError_t hilo_split(const float* W, int N, int K, int64_t ldw, uint16_t* hi, int64_t ldh, uint16_t* lo,

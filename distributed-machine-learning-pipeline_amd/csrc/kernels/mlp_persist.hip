@@ -422,7 +422,10 @@ static int g_pk_probe_mode = 0;
 static int g_pkx_helpers = -2;
 // pkx dZ1 row pushes from the layer-1 owner blocks (1) or the chains (0): the
 // default, and the HIPDSML_PKX_L1PUSH override (-2: not read yet, -1: none)
-constexpr int kPkxL1PushDefault = 0;
+// (1: mirror-mode N = 8 step 17.5 -> 15.4 us, N = 4 13.3 -> 12.3 us; the
+// lone-replica probe, which never waits for the rows, 10.9 -> 11.4 us at N = 8:
+// profiles/r6_pkx_l1push_ab.json)
+constexpr int kPkxL1PushDefault = 1;
 static int g_pkx_l1push = -2;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;

@@ -304,47 +304,9 @@ __device__ __forceinline__ void wgrad_tile_body(const WgArgs& a, int kt, int nt,
   }
 }
 
-// Z image of n tile nt (rows 0..63, wg_stage's swizzled layout) from the raw
-// split-K slices of the dgrad that produced Z (WgLayer::zs): the slices summed
-// in slice order + the dgrad's ReLU'-mask epilogue (gemm_skinny's combine:
-// 0 + slice 0 + slice 1 ...; x * 1 + 0; masked to 0; bf16), written where the
-// LDS-DMA would have put each chunk.  Slices one after the other (unroll 1):
-// all in flight took 168 VGPRs, every tile of the launch its occupancy.
-__device__ __forceinline__ void wg_stage_zs(const WgArgs& a, int nt, char* lds) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int pc = 0; pc < 2; ++pc) {
-    const int piece = 2 * w + pc;
-    const int r = 8 * piece + (lane >> 3), p = lane & 7;
-    const int m = min(r, a.M - 1);
-    const int zc = min(nt * 64 + 8 * (p ^ wg_swz(r)), a.N - 8);
-    const float* src = a.zs + (int64_t)(zc >> 6) * 4096 + m * 64 + (zc & 63);
-    const uint4 mk = *reinterpret_cast<const uint4*>(a.zmask + (int64_t)m * a.ldzm + zc);
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int z = 0; z < a.zsS; ++z) {
-      const float4 s0 = *reinterpret_cast<const float4*>(src + z * a.zs_stride);
-      const float4 s1 = *reinterpret_cast<const float4*>(src + z * a.zs_stride + 4);
-      x[0] += s0.x; x[1] += s0.y; x[2] += s0.z; x[3] += s0.w;
-      x[4] += s1.x; x[5] += s1.y; x[6] += s1.z; x[7] += s1.w;
-    }
-    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
-    uint32_t q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t mb16 = e & 1 ? mw[e >> 1] >> 16 : mw[e >> 1] & 0xffffu;
-      q[e] = bf16_to_f32((uint16_t)mb16) > 0.f ? (uint32_t)f32_to_bf16(x[e] * 1.0f + 0.f) : 0u;
-    }
-    *reinterpret_cast<uint4*>(lds + piece * 1024 + lane * 16) =
-        make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
-  }
-}
-
-template <bool ZS = false>
 __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char* lds) {
   // the tile's W words in one register set: fp32 W (4 float4), or for the
-  // split master {hi, lo} of rows (tid >> 3) and (tid >> 3) + 32 -- issued
-  // first, so their HBM round trip overlaps the operand staging and MFMAs
+  // split master {hi, lo} of rows (tid >> 3) and (tid >> 3) + 32
   uint4 wr[4];
   if (a.Wl) {
     wg_load_hl(a, kt, nt, wr);
@@ -354,11 +316,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int kt, int nt, char
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr[j] = __builtin_bit_cast(uint4, wold[j]);
   }
-  // Z from a dgrad's raw slices: summed into the LDS image here, then the
-  // ordinary tile with its Z image already in place
-  const bool zs = ZS && a.zs != nullptr;
-  if (zs) wg_stage_zs(a, nt, lds);
-  wgrad_tile_body(a, kt, nt, lds, wr, zs);
+  wgrad_tile_body(a, kt, nt, lds, wr);
 }
 
 __global__ __launch_bounds__(256) void wgrad_sgd_k(WgArgs a) {
@@ -388,8 +346,6 @@ __device__ __forceinline__ void wg_tile_xcd(int t, int kts, int nts, int& kt, in
   }
 }
 
-// ZS: some layer's Z comes as a dgrad's raw split-K slices (WgLayer::zs)
-template <bool ZS>
 __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
   __shared__ __attribute__((aligned(16))) char lds[kWgLdsTot];
   const int b = blockIdx.x;
@@ -409,7 +365,7 @@ __global__ __launch_bounds__(256) void wgrad_multi_k(WgMulti m) {
   // a layer's first block must sit at a multiple of 8 for its XCD map to hold
   if ((m.start[j] & 7) == 0) wg_tile_xcd(t, kts, (a.N + 63) / 64, kt, nt);
   else { kt = t % kts; nt = t / kts; }
-  wgrad_tile<ZS>(a, kt, nt, lds);
+  wgrad_tile(a, kt, nt, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1206,18 +1162,7 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile
   // the row-block form when asked for (tile kWgRowBlkTile) or, auto, at M >= 256
   // (M = 256 / 512: 47.3 / 64.7 us against 48.0 / 73.5 for the 64 x 64 tiles,
   // profiles/r5_wide_xact_cost.json; below 256 the square tiles are faster)
-  int any_zs = 0;
-  for (int j = 0; j < n; ++j) {
-    const WgLayer& L = layers[j];
-    if (L.zs == nullptr) continue;
-    // Z from raw split-K slices: the 64 x 64 tiles, one batch block, whole tiles
-    if (L.M > 64 || (L.N & 63) || L.zsS < 1 || L.zsS > 8 || L.zmask == nullptr || (L.ldzm & 7) ||
-        (L.zs_stride & 3) || L.zs_stride < (int64_t)(L.N / 64) * 4096 || ((uintptr_t)L.zs & 15) ||
-        ((uintptr_t)L.zmask & 15) || (tile != 0 && tile != 64))
-      return hipErrorInvalidValue;
-    any_zs = 1;
-  }
-  bool rows = !any_zs && (tile == kWgRowBlkTile || (tile == 0 && kRbAuto));
+  bool rows = tile == kWgRowBlkTile || (tile == 0 && kRbAuto);
   for (int j = 0; j < n && rows; ++j)
     rows = wg_valid(layers[j]) && rowblk_fits(layers[j]) && layers[j].M == layers[0].M &&
            (tile == kWgRowBlkTile || layers[j].M >= 256);
@@ -1237,7 +1182,7 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile
     // form 34.9 / 40.2 / 54.7 / 78.6 against 39.7 / 45.5 / 55.6 / 74.9; split
     // master 31.3 / 36.7 / 48.9 / 72.8 against 38.2 / 43.4 / 53.6 / 74.7 --
     // profiles/r3_wide_xact_cost.json)
-    const int big = !any_zs && L.N >= kBgT && L.K >= kBgT &&
+    const int big = L.N >= kBgT && L.K >= kBgT &&
                     (tile == kBgT || (tile == 0 && L.M >= 512 && L.W != nullptr));
     const int T = big ? kBgT : 64;
     mb.big[j] = big;
@@ -1251,10 +1196,8 @@ hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile
   for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; mb.big[j] = mb.big[0]; }
   if (any_big)
     hipLaunchKernelGGL(wgrad_multi_big_k, dim3(t), dim3(256), 0, s, mb);
-  else if (any_zs)
-    hipLaunchKernelGGL(wgrad_multi_k<true>, dim3(t), dim3(256), 0, s, m);
   else
-    hipLaunchKernelGGL(wgrad_multi_k<false>, dim3(t), dim3(256), 0, s, m);
+    hipLaunchKernelGGL(wgrad_multi_k, dim3(t), dim3(256), 0, s, m);
   return hipGetLastError();
 }
 

@@ -122,12 +122,6 @@ class WideMlpTrainer:
         # tail in that GEMM (HIPDSML_WIDE_HEAD_SLABS=0: the in-GEMM combine)
         self.head_slabs = (os.environ.get("HIPDSML_WIDE_HEAD_SLABS", "1") == "1" and self.fused_head
                            and L >= 2 and batch <= 64 and d[L - 1] % 64 == 0)
-        # likewise the last dgrad (dZ_1, read only by layer 0's update): its
-        # raw split-K slices go straight to the update launch, which sums them
-        # (+ the ReLU' mask) as it stages its Z tiles (HIPDSML_WIDE_DGRAD_SLABS=0:
-        # the in-GEMM combine)
-        self.dgrad_slabs = (os.environ.get("HIPDSML_WIDE_DGRAD_SLABS", "1") == "1" and L >= 3
-                            and batch <= 64 and d[1] % 64 == 0)
         # split-K plans of the skinny GEMMs: name -> (M, N, K, nn, S)
         self.plans: Dict[str, tuple] = {}
         for l in range(L):
@@ -289,13 +283,6 @@ class WideMlpTrainer:
             return 0
         return S
 
-    def _dgrad1_slabs(self) -> int:
-        """Slices of the last dgrad (dZ_1) when layer 0's update combines them."""
-        if not self.dgrad_slabs or self.xact or self.ctx.world_size != 1 or "b1" not in self.plans:
-            return 0
-        M, N, K, nn, S = self.plans["b1"]
-        return S if 2 <= S <= 8 and N % 64 == 0 else 0
-
     def _last_hidden_and_head(self, cur_prev: torch.Tensor, W_head: torch.Tensor, rows: int, y: torch.Tensor,
                               logits, stats, dzp) -> None:
         """H_{L-1} = relu(H_{L-2} W^T + b) as raw split-K slices, then the head
@@ -385,21 +372,13 @@ class WideMlpTrainer:
             # every dgrad first (they read this step's bf16 weights), then ONE
             # launch updates every layer: W -= lr * dZ_{l+1}^T H_l, the next step's
             # bf16 copies, the biases (kernels/wgrad_sgd.hip, flattened tile grid)
-            zs = self._dgrad1_slabs()
             for l in range(L - 2 if self.fused_head else L - 1, 0, -1):
-                if zs and l == 1:  # raw slices: layer 0's update sums them (+ mask)
-                    M1, N1, K1, _, _ = self.plans["b1"]
-                    C.gemm_skinny(self.dZ[2], cur[1], Bt, N1, K1, nn=True, ws=self.Cp, raw=True)
-                else:
-                    self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
+                self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
             layers = []
             for l in range(L - 1, -1, -1):
                 W, b = self.views[l]
-                lay = (self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l],
-                       None, b, None, cur[l], self.Wlo[l])
-                if zs and l == 0:
-                    lay = lay + (self.Cp, zs, self.H[1])
-                layers.append(lay)
+                layers.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l],
+                               None, b, None, cur[l], self.Wlo[l]))
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1

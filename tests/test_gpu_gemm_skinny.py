@@ -241,41 +241,3 @@ def test_wgrad_rowblk_matches_square_tiles(M):
         want = W0 - lr * al * (Zr.t() @ Xr)
         assert (Wn[:, :K].cpu() - want).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
 
-
-@pytest.mark.parametrize("N,K", [(256, 128), (4096, 4096)])
-def test_wgrad_update_sums_raw_dgrad_slices(N, K):
-    """Layer 0's update with its Z operand given as the last dgrad's raw
-    split-K slices (+ the ReLU' mask), against the dgrad's own combine +
-    masked bf16 epilogue feeding the update: the same hi / lo words, the same
-    bias step."""
-    C = require_native()
-    g = torch.Generator().manual_seed(N + K)
-    M, D0 = 64, 784
-    dZ2 = (1e-2 * torch.randn(M, K, generator=g)).to(torch.bfloat16).to(DEV)
-    W1 = (torch.randn(K, N, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)   # [out K][in N]
-    H1 = torch.relu(torch.randn(M, N, generator=g)).to(torch.bfloat16).to(DEV)    # the ReLU' mask
-    X = torch.rand(M, D0, generator=g).to(torch.bfloat16).to(DEV)
-    W0 = 0.01 * torch.randn(N, D0, generator=g)
-    S = C.gemm_skinny_splits(M, N, K, 0)
-    ws_words, ctr_words = C.gemm_skinny_ws(M, N, K, 0)
-    ws = torch.zeros(max(ws_words, S * (N // 64) * 4096), device=DEV)
-    ctr = torch.zeros(max(ctr_words, 1), dtype=torch.int32, device=DEV)
-    dZ1 = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-    outs = []
-    for raw in (False, True):
-        Wh = torch.zeros(N, D0, dtype=torch.bfloat16, device=DEV)
-        Wl = torch.zeros(N, D0, dtype=torch.int16, device=DEV)
-        Wb = torch.zeros(N, D0, dtype=torch.bfloat16, device=DEV)
-        C.hilo_split(W0.to(DEV), Wh, Wl)
-        b0 = torch.zeros(N, device=DEV)
-        if raw:
-            C.gemm_skinny(dZ2, W1, M, N, K, nn=True, ws=ws, raw=True)
-            lay = (dZ1, X, M, N, D0, 1.0, 0.5, None, Wb, None, b0, None, Wh, Wl, ws, S, H1)
-        else:
-            C.gemm_skinny(dZ2, W1, M, N, K, nn=True, mask=H1, obf=dZ1, ws=ws, ctr=ctr)
-            lay = (dZ1, X, M, N, D0, 1.0, 0.5, None, Wb, None, b0, None, Wh, Wl)
-        C.wgrad_sgd_multi([lay])
-        torch.cuda.synchronize()
-        outs.append((Wb.cpu(), Wl.cpu(), b0.cpu()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
