@@ -681,8 +681,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
     return a;
   };
-  m.def("wgrad_rowblk_set_mfma32", &wgrad_rowblk_set_mfma32, py::arg("mode"),
-        "row-block update MFMA shape: 1 32x32x16, 0 16x16x32, -1 the default");
   m.def("wgrad_sgd_multi", [wg_layer](py::list layers, int tile) {
     std::vector<WgLayer> v;
     for (py::handle it : layers) v.push_back(wg_layer(it));

@@ -359,8 +359,6 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // tile: 0 auto, 64 / 128 square tiles, kWgRowBlkTile the row-block form (split
 // master, one M of 64 / 128 / 256 / 512 for every layer; auto picks it from M >= 256)
 constexpr int kWgRowBlkTile = 256;
-// row-block update: products on 32x32x16 (1) or 16x16x32 (0) MFMAs, -1 the default
-void wgrad_rowblk_set_mfma32(int mode);
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);

@@ -704,8 +704,6 @@ constexpr bool kRbPair = true;
 #endif
   // two ring blocks per wait / barrier (NBLK >= 4)
 constexpr int kRbOob = 0x7ffffff0;             // offset of a dropped word: past every bound (host check)
-constexpr bool kRbMfma32Default = false;        // the products on 32x32x16 (see wgrad_rowblk_k M32)
-static int g_rb_mfma32 = -2;                    // HIPDSML_RB_MFMA32 override (-2: not read, -1: none)
 
 struct WgRowBlk {
   WgArgs l[kWgMaxLayers];
@@ -774,15 +772,14 @@ __device__ __forceinline__ wg_u2 rb_dstr_o(uint32_t addr) {
   return v;
 }
 // Lane addresses (block 0 of the X ring) of the 8 transposing reads a wave
-// issues per 32-row block: [y][lo, hi], y = the 16-column group (16x16x32) or
-// 2 k step + 32-column tile (32x32x16); block b adds b * 4096 (immediate).
-template <bool M32>
+// issues per 32-row block: [y][lo, hi], y = the 16-column group; block b adds
+// b * 4096 (immediate).
 __device__ __forceinline__ void rb_frag_addrs(uint32_t ring, int lane, uint32_t (&fa)[4][2]) {
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
 #pragma unroll
   for (int y = 0; y < 4; ++y) {
-    const int c0 = M32 ? 32 * (y & 1) + 16 * (g & 1) : 16 * y;
-    const int r0 = M32 ? 16 * (y >> 1) + 8 * (g >> 1) + q : 8 * g + q, r1 = r0 + 4;
+    const int c0 = 16 * y;
+    const int r0 = 8 * g + q, r1 = r0 + 4;
     const int ch = (c0 >> 3) + (p >> 1);
     fa[y][0] = ring + r0 * 128 + 16 * (ch ^ wg_swz(r0)) + 8 * (p & 1);
     fa[y][1] = ring + r1 * 128 + 16 * (ch ^ wg_swz(r1)) + 8 * (p & 1);
@@ -802,24 +799,7 @@ __device__ __forceinline__ void rb_frag_issue(uint32_t img, int c0, int lane, wg
   hi = bg_dstr(img + r1 * PITCH + 16 * (ch ^ s1) + 8 * (p & 1));
 }
 
-// Operand fragment of the 32 x 32 x 16 MFMA (k step of 16 batch rows at kb):
-// lane l gets image column c0 + l % 32 at rows kb + 8 (l / 32) .. +7 -- each
-// 16-lane group reads its 16 columns (c0 or c0 + 16) of 8 rows with two
-// transposing reads, as rb_frag_issue does for the 16 x 16 x 32 form.
-template <int PITCH>
-__device__ __forceinline__ void rb_frag32_issue(uint32_t img, int c0, int kb, int lane, wg_u2& lo, wg_u2& hi) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int ch = ((c0 + 16 * (g & 1)) >> 3) + (p >> 1);
-  const int r0 = kb + 8 * (g >> 1) + q, r1 = r0 + 4;
-  const int s0 = PITCH == 128 ? wg_swz(r0) : bg_swz(r0), s1 = PITCH == 128 ? wg_swz(r1) : bg_swz(r1);
-  lo = bg_dstr(img + r0 * PITCH + 16 * (ch ^ s0) + 8 * (p & 1));
-  hi = bg_dstr(img + r1 * PITCH + 16 * (ch ^ s1) + 8 * (p & 1));
-}
-
-// M32: the products on v_mfma_f32_32x32x16_bf16 instead of 16x16x32 -- the
-// same fragment registers, LDS reads and cycles per FLOP, half the MFMA
-// instructions (4 a 32-row block and wave instead of 8)
-template <int NBLK, bool M32 = false>
+template <int NBLK>
 __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
   extern __shared__ __attribute__((aligned(16))) char rb_lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -828,7 +808,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
   const uint32_t ring = (uint32_t)(uintptr_t)(wg_lptr)rb_lds;
   const uint32_t tileb = ring + kRbRing;
   uint32_t fa[4][2];  // the 8 transposing reads' lane addresses in ring block 0
-  rb_frag_addrs<M32>(ring, lane, fa);
+  rb_frag_addrs(ring, lane, fa);
   const int U = rb.ustart[rb.n];
   const int u0 = (int)((int64_t)blockIdx.x * U / rb.groups);
   const int u1 = (int)((int64_t)(blockIdx.x + 1) * U / rb.groups);
@@ -892,13 +872,9 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           const int c = 8 * ph + cc;
           if (c < nblk) {
             wg_u2 lo0, hi0, lo1, hi1;
-            if constexpr (M32) {  // [c][k step]: W rows 32 w + l % 32, batch rows 32 c + 16 s + 8 (l / 32) ..
-              rb_frag32_issue<256>(ring + cc * 8192, 32 * w, 0, lane, lo0, hi0);
-              rb_frag32_issue<256>(ring + cc * 8192, 32 * w, 16, lane, lo1, hi1);
-            } else {              // [c][xm]: W rows 32 w + 16 xm + l % 16, batch rows 32 c + 8 (l / 16) ..
-              rb_frag_issue<256>(ring + cc * 8192, 32 * w, lane, lo0, hi0);
-              rb_frag_issue<256>(ring + cc * 8192, 32 * w + 16, lane, lo1, hi1);
-            }
+            // [c][xm]: W rows 32 w + 16 xm + l % 16, batch rows 32 c + 8 (l / 16) ..
+            rb_frag_issue<256>(ring + cc * 8192, 32 * w, lane, lo0, hi0);
+            rb_frag_issue<256>(ring + cc * 8192, 32 * w + 16, lane, lo1, hi1);
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo0), "+v"(hi0), "+v"(lo1), "+v"(hi1)::"memory");
             zf[c][0] = wg_u4{lo0.x, lo0.y, hi0.x, hi0.y};
             zf[c][1] = wg_u4{lo1.x, lo1.y, hi1.x, hi1.y};
@@ -924,17 +900,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           }
         }
       }
-      if constexpr (M32) {
-        // both k steps' fragments hold W row 32 w + l % 32: one sum, lane halves combined
-        float t = sm[0] + sm[1];
-        t += __shfl_xor(t, 32, 64);
-        const int n = n0 + 32 * w + lane;
-        if (lane < 32 && n < a.N) {
-          const float db = a.alpha * t;
-          if (a.bias) a.bias[n] -= a.lr * db;
-          if (a.bgrad) a.bgrad[n] = db;
-        }
-      } else {
 #pragma unroll
       for (int xm = 0; xm < 2; ++xm) {
         sm[xm] += __shfl_xor(sm[xm], 16, 64);
@@ -945,7 +910,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           if (a.bias) a.bias[n] -= a.lr * db;
           if (a.bgrad) a.bgrad[n] = db;
         }
-      }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's count starts from zero
     }
@@ -986,11 +950,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
       for (int xm = 0; xm < 2; ++xm)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[xm][y] = {0.f, 0.f, 0.f, 0.f};
-      f32x16 acc32[2];  // M32: the wave's two 32 x 32 column tiles
-#pragma unroll
-      for (int y2 = 0; y2 < 2; ++y2)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc32[y2][e] = 0.f;
       // The ring, software-pipelined: block b + 1's X fragments are read while
       // block b's MFMAs run (b: a compile-time index -- the waits' counts and the
       // Z^T fragment registers are static).  Block b was read (and its reads
@@ -1009,7 +968,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         auto reads2 = [&](auto b0c, int buf) __attribute__((always_inline)) {
           constexpr int b0 = decltype(b0c)::value;
 #pragma unroll
-          for (int y = 0; y < 4; ++y) {  // y: 16x16x32 column group, or 32x32x16 2 k step + tile
+          for (int y = 0; y < 4; ++y) {  // y: the 16-column group
             lo[buf][0][y] = rb_dstr_o<b0 * 4096>(fa[y][0]);
             hi[buf][0][y] = rb_dstr_o<b0 * 4096>(fa[y][1]);
             lo[buf][1][y] = rb_dstr_o<(b0 + 1) * 4096>(fa[y][0]);
@@ -1054,17 +1013,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 #pragma unroll
             for (int y = 0; y < 4; ++y) {
               const wg_u4 fx = {lo[cur][sb][y].x, lo[cur][sb][y].y, hi[cur][sb][y].x, hi[cur][sb][y].y};
-              if constexpr (M32) {
-                acc32[y & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                    __builtin_bit_cast(wg_bf16x8, zf[2 * j + sb][y >> 1]), __builtin_bit_cast(wg_bf16x8, fx),
-                    acc32[y & 1], 0, 0, 0);
-              } else {
 #pragma unroll
-                for (int xm = 0; xm < 2; ++xm)
-                  acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                      __builtin_bit_cast(wg_bf16x8, zf[2 * j + sb][xm]), __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
-                      0, 0, 0);
-              }
+              for (int xm = 0; xm < 2; ++xm)
+                acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(wg_bf16x8, zf[2 * j + sb][xm]), __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
+                    0, 0, 0);
             }
           if constexpr (2 * j + 3 < NBLK) lgkm2(nxt);
         };
@@ -1110,17 +1063,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
           const wg_u4 fx = {lo[cur][y].x, lo[cur][y].y, hi[cur][y].x, hi[cur][y].y};
-          if constexpr (M32) {
-            acc32[y & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][y >> 1]),
-                                                                  __builtin_bit_cast(wg_bf16x8, fx), acc32[y & 1],
-                                                                  0, 0, 0);
-          } else {
 #pragma unroll
-            for (int xm = 0; xm < 2; ++xm)
-              acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][xm]),
-                                                                  __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
-                                                                  0, 0, 0);
-          }
+          for (int xm = 0; xm < 2; ++xm)
+            acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][xm]),
+                                                                __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
+                                                                0, 0, 0);
         }
         if constexpr (b + 1 < NBLK) lgkm(nxt);
       };
@@ -1129,19 +1076,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
       else rb_vm<0>();
       }
       // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
-      if constexpr (M32) {
-        // 32 x 32 accumulator: register e of lane l = row 8 (e / 4) + 4 (l / 32) + e % 4, column l % 32
-        const uint32_t tb = tileb + ((32 * w + 4 * (lane >> 5)) * kRbPitch + (lane & 31)) * 4;
-        auto st = [&](auto ec, int y2) __attribute__((always_inline)) {
-          constexpr int e = decltype(ec)::value;
-          if (y2 == 0) rb_dsw32_o<((8 * (e >> 2) + (e & 3)) * kRbPitch) * 4>(tb, acc32[0][e] * a.alpha);
-          else rb_dsw32_o<((8 * (e >> 2) + (e & 3)) * kRbPitch + 32) * 4>(tb, acc32[1][e] * a.alpha);
-        };
-        auto st0 = [&](auto ec) __attribute__((always_inline)) { st(ec, 0); };
-        auto st1 = [&](auto ec) __attribute__((always_inline)) { st(ec, 1); };
-        rb_for<0, 16>(st0);
-        rb_for<0, 16>(st1);
-      } else {
+      {
         const uint32_t tb = tileb + ((32 * w + 4 * g) * kRbPitch + i) * 4;
         auto st = [&](auto kc) __attribute__((always_inline)) {  // k = 16 xm + 4 y + r
           constexpr int k = decltype(kc)::value;
@@ -1254,14 +1189,8 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const void* fs[8] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2, false>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<4, false>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<8, false>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<16, false>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<2, true>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<4, true>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<8, true>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<16, true>)};
+    const void* fs[4] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
+                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>)};
     for (const void* f : fs) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRbLds);
       if (e != hipSuccess) { cus = 0; return e; }
@@ -1274,27 +1203,14 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
 #else
   rb.dbg = 0;
 #endif
-  if (g_rb_mfma32 == -2) {  // HIPDSML_RB_MFMA32 overrides the default (1: 32x32x16, 0: 16x16x32)
-    const char* e = getenv("HIPDSML_RB_MFMA32");
-    g_rb_mfma32 = e != nullptr && *e ? (atoi(e) ? 1 : 0) : -1;
-  }
-  const bool m32 = g_rb_mfma32 >= 0 ? g_rb_mfma32 == 1 : kRbMfma32Default;
-#define DSML_RB_LAUNCH(NB)                                                                  \
-  do {                                                                                      \
-    if (m32) hipLaunchKernelGGL((wgrad_rowblk_k<NB, true>), dim3(rb.groups), dim3(256), kRbLds, s, rb); \
-    else hipLaunchKernelGGL((wgrad_rowblk_k<NB, false>), dim3(rb.groups), dim3(256), kRbLds, s, rb);    \
-  } while (0)
   switch (layers[0].M) {
-    case 64: DSML_RB_LAUNCH(2); break;
-    case 128: DSML_RB_LAUNCH(4); break;
-    case 256: DSML_RB_LAUNCH(8); break;
-    default: DSML_RB_LAUNCH(16); break;
+    case 64: hipLaunchKernelGGL(wgrad_rowblk_k<2>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    case 128: hipLaunchKernelGGL(wgrad_rowblk_k<4>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    case 256: hipLaunchKernelGGL(wgrad_rowblk_k<8>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
+    default: hipLaunchKernelGGL(wgrad_rowblk_k<16>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
   }
-#undef DSML_RB_LAUNCH
   return hipGetLastError();
 }
-
-void wgrad_rowblk_set_mfma32(int mode) { g_rb_mfma32 = mode < 0 ? -1 : (mode ? 1 : 0); }
 
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile) {
   if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT && tile != kWgRowBlkTile))

@@ -242,51 +242,3 @@ def test_wgrad_rowblk_matches_square_tiles(M):
         assert (Wn[:, :K].cpu() - want).abs().max().item() < 1e-4 * max(1.0, M ** 0.5)
 
 
-
-@pytest.mark.parametrize("M", [64, 256, 512])
-def test_wgrad_rowblk_mfma32_matches_fp32(M):
-    """The row-block update on v_mfma_f32_32x32x16_bf16 (VERDICT r5 Next #3:
-    half the MFMA instructions of the 16x16x32 form): against fp32 W - lr *
-    alpha * Z^T X and the bias step, and close to the 16x16x32 form (the two
-    MFMA shapes accumulate in different orders)."""
-    C = require_native()
-    g = torch.Generator(device="cpu").manual_seed(99 + M)
-    shapes = [(10, 1024), (200, 784), (1024, 1024), (4096, 512)]
-    runs = {}
-    for m32 in (0, 1):
-        args = []
-        for N, K in shapes:
-            pn, pk = (N + 15) // 16 * 16, (K + 15) // 16 * 16
-            g.manual_seed(7 * N + K + M)
-            Z = torch.zeros(M, pn, dtype=torch.bfloat16)
-            X = torch.zeros(M, pk, dtype=torch.bfloat16)
-            Z[:, :N] = torch.randn(M, N, generator=g).to(torch.bfloat16)
-            X[:, :K] = torch.randn(M, K, generator=g).to(torch.bfloat16)
-            W = torch.randn(N, pk, generator=g)
-            W[:, K:] = 0
-            Wh = torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV)
-            Wl = torch.zeros(N, pk, dtype=torch.int16, device=DEV)
-            C.hilo_split(W.to(DEV), Wh, Wl)
-            b = torch.randn(N, generator=g).to(DEV)
-            args.append((Z.to(DEV), X.to(DEV), M, N, K, 0.5, 0.01, None,
-                         torch.zeros(N, pk, dtype=torch.bfloat16, device=DEV), None, b, None, Wh, Wl))
-        C.wgrad_rowblk_set_mfma32(m32)
-        try:
-            C.wgrad_sgd_multi(args, tile=256)
-            torch.cuda.synchronize()
-        finally:
-            C.wgrad_rowblk_set_mfma32(-1)
-        runs[m32] = args
-    tol = 1e-4 * max(1.0, M ** 0.5)
-    for (Z, X, M_, N, K, al, lr, _, Wb, _, b, _, Wh, Wl), a16 in zip(runs[1], runs[0]):
-        Wn = torch.zeros(N, Wb.shape[1], device=DEV)
-        C.hilo_join(Wb, Wl, Wn)
-        g.manual_seed(7 * N + K + M)
-        Zr = torch.randn(M, N, generator=g).to(torch.bfloat16).float()
-        Xr = torch.randn(M, K, generator=g).to(torch.bfloat16).float()
-        W0 = torch.randn(N, (K + 15) // 16 * 16, generator=g)[:, :K]
-        b0 = torch.randn(N, generator=g)
-        want = W0 - lr * al * (Zr.t() @ Xr)
-        assert (Wn[:, :K].cpu() - want).abs().max().item() < tol
-        assert (b.cpu() - (b0 - lr * al * Zr.sum(0))).abs().max().item() < tol
-        assert (b - a16[10]).abs().max().item() < tol

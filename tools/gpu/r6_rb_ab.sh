@@ -1,5 +1,8 @@
 # Row-block global-batch update: tests, then the xact cost at N = 1/2/4/8 with
 # the 16x16x32 and 32x32x16 MFMA forms alternating, then PMC of both at N = 8.
+# Record of the A/B in profiles/r6_wide_xact_cost.json: it ran on commit
+# 34d37d2; the 32x32x16 form (HIPDSML_RB_MFMA32) was removed after it measured
+# no faster, so on later trees both arms run the 16x16x32 kernel.
 set -e
 T=${1:-r6rbab}
 R=$GRAFT_REPO_ROOT
