@@ -638,6 +638,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_set_stamping", &head_set_stamping);
 #ifdef HIPDSML_MEASURE
   m.def("head_set_debug", &head_set_debug);
+  m.def("wide_input_stamps", []() {
+    std::vector<uint64_t> v(1024 * 8);
+    hip_ok(wide_input_read_stamps(v.data()), "wide_input_read_stamps");
+    return v;
+  });
+  m.def("wide_input_set_stamping", &wide_input_set_stamping);
+  m.def("wide_input_set_dbg", &wide_input_set_dbg);
 #endif
 #ifdef HIPDSML_MEASURE
   m.attr("measure_build") = true;
@@ -686,6 +693,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (py::handle it : layers) v.push_back(wg_layer(it));
     hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
   }, py::arg("layers"), py::arg("tile") = 0);
+  m.def("wide_input_step", [bf16p](torch::Tensor slabs, int64_t S, torch::Tensor H1, c10::optional<torch::Tensor> dzo,
+                                  torch::Tensor XG, torch::Tensor XF, torch::Tensor Wh, torch::Tensor Wl,
+                                  torch::Tensor Wb, torch::Tensor bias, double alpha, double lr, torch::Tensor Hn,
+                                  int64_t M, int64_t N, int64_t K) {
+    // XG: this step's rows in gradient-fragment order, contiguous [ceil(K/16)][2][16][32];
+    // XF: the next step's rows k-blocked, contiguous [ceil(K/32)][64][32]
+    auto rows2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
+      TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
+    };
+    check_f32(slabs, "slabs");
+    check_f32(bias, "bias");
+    TORCH_CHECK(bias.numel() >= N, "bias");
+    const int64_t tiles = (N + 63) / 64;
+    TORCH_CHECK(slabs.numel() >= S * tiles * 4096, "slabs too small for S raw slices");
+    rows2(H1, M, N, "H1"); rows2(Wh, N, K, "Wh"); rows2(Wl, N, K, "Wl");
+    rows2(Wb, N, K, "Wb"); rows2(Hn, M, N, "Hn");
+    TORCH_CHECK(Wl.scalar_type() == torch::kInt16, "Wl must be int16");
+    TORCH_CHECK(XG.is_contiguous() && XG.numel() >= ((K + 15) / 16) * 1024, "XG: contiguous [K/16][2][16][32]");
+    TORCH_CHECK(XF.is_contiguous() && XF.numel() >= ((K + 31) / 32) * 2048, "XF: contiguous [K/32][64][32]");
+    WideInArgs a{};
+    a.slabs = slabs.data_ptr<float>(); a.S = (int)S; a.tiles = (int)tiles; a.zalpha = 1.f; a.zbias = 0.f;
+    a.H1 = bf16p(H1, "H1"); a.ldh1 = H1.stride(0);
+    if (dzo) { rows2(*dzo, M, N, "dzo"); a.dzo = bf16p(*dzo, "dzo"); a.lddz = dzo->stride(0); }
+    a.XG = bf16p(XG, "XG"); a.XF = bf16p(XF, "XF");
+    a.Wh = bf16p(Wh, "Wh"); a.ldwh = Wh.stride(0);
+    a.Wl = reinterpret_cast<uint16_t*>(Wl.data_ptr<int16_t>()); a.ldwl = Wl.stride(0);
+    a.Wb = bf16p(Wb, "Wb"); a.ldwb = Wb.stride(0);
+    a.bias = bias.data_ptr<float>(); a.alpha = (float)alpha; a.lr = (float)lr; a.falpha = 1.f;
+    a.Hn = bf16p(Hn, "Hn"); a.ldhn = Hn.stride(0);
+    a.M = (int)M; a.N = (int)N; a.K = (int)K; a.kq = (int)((((K + 7) / 8 + 31) / 32) * 32);
+    hip_ok(wide_input_step(a, cur_stream()), "wide_input_step");
+  }, py::arg("slabs"), py::arg("S"), py::arg("H1"), py::arg("dzo"), py::arg("XG"), py::arg("XF"), py::arg("Wh"),
+     py::arg("Wl"), py::arg("Wb"), py::arg("bias"), py::arg("alpha"), py::arg("lr"), py::arg("Hn"), py::arg("M"),
+     py::arg("N"), py::arg("K"),
+     "wide input layer: dZ_1 from raw dgrad slices, W_0 / b_0 SGD (split master), next step's H_1");
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

@@ -360,6 +360,37 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // master, one M of 64 / 128 / 256 / 512 for every layer; auto picks it from M >= 256)
 constexpr int kWgRowBlkTile = 256;
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
+// The wide step's input layer in one launch (kernels/wide_input.hip): dZ_1 from
+// the last dgrad's raw split-K slices (+ ReLU' mask), the W_0 / b_0 SGD step on
+// the split master, and the NEXT step's H_1 = relu(X' W_0'^T + b_0').  M = 64.
+struct WideInArgs {
+  const float* slabs;  // raw slices: slabs[(z * tiles + n / 64) * 4096 + m * 64 + n % 64]
+  int S, tiles;
+  float zalpha, zbias;   // the dgrad epilogue (alpha, + 0)
+  const uint16_t* H1;    // this step's H_1 (the mask), ldh1
+  int64_t ldh1;
+  uint16_t* dzo;         // dZ_1 out (nullable), lddz
+  int64_t lddz;
+  const uint16_t* XG;    // this step's 64 input rows in gradient-fragment order [K/16][2][16][32]
+  const uint16_t* XF;    // the next step's 64 input rows k-blocked [K/32][64][32]
+  const uint16_t* Wh;    // this step's hi words, ldwh
+  int64_t ldwh;
+  uint16_t* Wl;          // int16 remainders (in place), ldwl
+  int64_t ldwl;
+  uint16_t* Wb;          // the updated hi words, ldwb
+  int64_t ldwb;
+  float* bias;           // b_0 (updated in place)
+  float alpha, lr, falpha;
+  uint16_t* Hn;          // the next step's H_1, ldhn
+  int64_t ldhn;
+  int M, N, K, kq;       // kq: columns per wave, gemm_rows64_k's split ((ceil(K/8) + 31) / 32 * 32)
+};
+hipError_t wide_input_step(const WideInArgs& a, hipStream_t s);
+#ifdef HIPDSML_MEASURE
+hipError_t wide_input_read_stamps(uint64_t* host_out);  // [1024][8], measurement builds
+void wide_input_set_stamping(bool on);
+void wide_input_set_dbg(int bits);
+#endif
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 #ifdef HIPDSML_MEASURE

@@ -182,6 +182,33 @@ class WideMlpTrainer:
             del xp
         if self.xact:
             self._init_xact(batch)
+        # fused input layer (one replica): the last dgrad leaves raw split-K
+        # slices, and ONE launch (kernels/wide_input.hip) sums them into dZ_1,
+        # updates W_0 / b_0 and computes the NEXT step's H_1 with the updated
+        # rows -- the input-layer forward launch and the dgrad's combine tail
+        # leave the step.  Bit-identical to the separate kernels.  H_1 is
+        # double-buffered by step parity (this step's H_1 is still read by the
+        # update of W_1 while the next one is written); _carry is the step whose
+        # H_1 is already in its buffer (None: run the forward first).
+        self.fused_input = (os.environ.get("HIPDSML_WIDE_FUSED_INPUT", "1") == "1" and not self.ctx.is_distributed
+                            and L >= 3 and batch == 64 and d[0] % 16 == 0 and d[0] <= 1024 and d[1] % 64 == 0
+                            and self.head_slabs and self.plans["b1"][4] <= 8 and self.pd[0] == d[0])
+        self._carry: Optional[int] = None
+        self._input_first = os.environ.get("HIPDSML_WIDE_INPUT_FIRST", "0") == "1"
+        if self.fused_input:
+            self.H1buf = [self.H[1], torch.zeros_like(self.H[1])]
+            # each batch's input rows twice more, in the fused launch's fragment
+            # orders (static data, built once; 100 KB a batch each): XG for the
+            # gradient ([K/16][2][16][32]: batch rows 32h + .. at 16 columns) and
+            # XF for the forward (k-blocked [K/32][64][32]) -- every fragment load
+            # is 1 KiB contiguous
+            nb, k16, k32 = self.nbatches, _rup(d[0], 16), _rup(d[0], 32)
+            xs = torch.zeros(nb, batch, k32, **bf)
+            xs[:, :, :d[0]] = self.Xb[:nb * batch, :d[0]].view(nb, batch, d[0])
+            self.XG = (xs[:, :, :k16].view(nb, 2, 32, k16 // 16, 16).permute(0, 3, 1, 4, 2).contiguous()
+                       .view(nb, -1))
+            self.XF = xs.view(nb, batch, k32 // 32, 32).permute(0, 2, 1, 3).contiguous().view(nb, -1)
+            del xs
         self._refresh_bf16()
 
     def _init_xact(self, batch: int) -> None:
@@ -248,6 +275,7 @@ class WideMlpTrainer:
 
     def _refresh_bf16(self) -> None:
         """Split masters (both hi copies + the remainders) from the fp32 W in P."""
+        self._carry = None
         for l in range(self.L):
             W, _ = self.views[l]
             self.C.hilo_split(W, self.Wb[l][0], self.Wlo[l])
@@ -311,6 +339,11 @@ class WideMlpTrainer:
         self.C.gemm_skinny(A, B, M, N, K, nn=nn, ws=self.Cp, ctr=self.tctr, **epi)
 
     # ----------------------------------------------------------------- step --
+    def _x_operand(self, bi: int) -> torch.Tensor:
+        """The input-layer forward's A operand for batch bi (k-blocked when built)."""
+        r0 = bi * self.batch
+        return self.Xblk[:, r0:r0 + self.batch] if self.Xblk is not None else self._xb_rows(bi)
+
     def _step(self) -> None:
         C, d, L, Bt = self.C, self.spec.dims, self.L, self.batch
         bi = self.steps_done % self.nbatches
@@ -320,11 +353,15 @@ class WideMlpTrainer:
         nxt = [self.Wb[l][1 - p] for l in range(L)]   # written by this step's updates
         self.H[0] = self._xb_rows(bi)  # this batch's bf16 rows (a view: no copy)
         slabs = self._slab_plan(L - 2)
+        if self.fused_input:
+            self.H[1] = self.H1buf[p]
         for l in range(L - 1):
             if slabs and l == L - 2:
                 break  # the head combines this layer's GEMM (below)
+            if l == 0 and self.fused_input and self._carry == self.steps_done:
+                continue  # H_1 came with the previous step's input-layer launch
             _, b = self.views[l]
-            A = self.Xblk[:, r0:r0 + Bt] if l == 0 and self.Xblk is not None else self.H[l]
+            A = self._x_operand(bi) if l == 0 else self.H[l]
             self._gemm(f"f{l}", A, cur[l], bias=b, relu=True, obf=self.H[l + 1])
             if self.xact:
                 self._gather(self.Hall[l + 1])
@@ -367,6 +404,37 @@ class WideMlpTrainer:
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
             self.steps_done += 1
+            return
+        if fused_sgd and self.fused_input:
+            # dgrads (the last one as raw slices), ONE launch for the layers above
+            # the input layer, then the input layer's launch: dZ_1, W_0 / b_0 and
+            # the next batch's H_1 (kernels/wide_input.hip)
+            for l in range(L - 2, 0, -1):
+                if l == 1:
+                    M, N, K, _, S = self.plans["b1"]
+                    C.gemm_skinny(self.dZ[2], cur[1], M, N, K, nn=True, ws=self.Cp, raw=True)
+                else:
+                    self._gemm(f"b{l}", self.dZ[l + 1], cur[l], mask=self.H[l], obf=self.dZ[l])
+            layers = []
+            for l in range(L - 1, 0, -1):
+                W, b = self.views[l]
+                layers.append((self.dZ[l + 1], self.H[l], Bt, d[l + 1], d[l], 1.0, scale, None, nxt[l],
+                               None, b, None, cur[l], self.Wlo[l]))
+            bn = (bi + 1) % self.nbatches
+            _, b0 = self.views[0]
+            first = self._input_first
+            if first:
+                C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi],
+                                  self.XF[bn], cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale,
+                                  self.H1buf[1 - p], Bt, d[1], d[0])
+            for i in range(0, len(layers), 4):
+                C.wgrad_sgd_multi(layers[i:i + 4])
+            if not first:
+                C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi],
+                                  self.XF[bn], cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale,
+                                  self.H1buf[1 - p], Bt, d[1], d[0])
+            self.steps_done += 1
+            self._carry = self.steps_done
             return
         if fused_sgd:
             # every dgrad first (they read this step's bf16 weights), then ONE
@@ -452,11 +520,26 @@ class WideMlpTrainer:
         stream.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
         saved = self.steps_done
+        # the graph's first step takes H_1 from the step before it (fused input layer)
+        self._ensure_carry()
+        carry = self._carry
         with torch.cuda.graph(g, stream=stream):
             for _ in range(self.period):
                 self._step()
         self.steps_done = saved
+        self._carry = carry
         self._graph = g
+
+    def _ensure_carry(self) -> None:
+        """Fused input layer: make this step's H_1 valid (the standalone forward
+        of layer 0) when no previous step left it (first step, after evaluate /
+        a checkpoint load)."""
+        if not self.fused_input or self._carry == self.steps_done:
+            return
+        p, bi = self.steps_done % 2, self.steps_done % self.nbatches
+        _, b = self.views[0]
+        self._gemm("f0", self._x_operand(bi), self.Wb[0][p], bias=b, relu=True, obf=self.H1buf[p])
+        self._carry = self.steps_done
 
     def train_steps(self, n: int) -> None:
         with torch.cuda.device(self.device):
@@ -465,7 +548,9 @@ class WideMlpTrainer:
                         and n >= self.period):
                     if self._graph is None:
                         self._capture_epoch()
+                    self._ensure_carry()
                     self._graph.replay()
+                    self._carry = self.steps_done + self.period
                     self.steps_done += self.period
                     n -= self.period
                 else:
@@ -500,6 +585,7 @@ class WideMlpTrainer:
         self.synchronize()
         self._P.copy_(sd["params"].to(self.device))
         self.steps_done = int(sd["steps_done"])
+        self._carry = None
         self._refresh_bf16()  # the split masters from the fp32 weights
         self.synchronize()
 
@@ -512,6 +598,7 @@ class WideMlpTrainer:
         X = ds.X.to(self.device, torch.float32).contiguous()
         y = ds.y.to(self.device, torch.int32).contiguous()
         n = X.shape[0]
+        self._carry = None  # the activation buffers below are reused: H_1 is recomputed before the next step
         st = torch.zeros(Bt * 4, dtype=torch.float32, device=self.device)
         xb = torch.zeros(Bt, self.pd[0], dtype=torch.bfloat16, device=self.device)
         with torch.cuda.device(self.device):

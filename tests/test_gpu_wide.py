@@ -365,3 +365,29 @@ def test_wide_head_slab_engine_is_bit_identical(dims, monkeypatch):
     for r in runs[1:]:
         assert torch.equal(r[0], runs[0][0])
         assert r[1:] == runs[0][1:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(784, 4096, 4096, 10), (784, 2048, 1024, 10), (784, 4096, 2048, 2048, 10)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_wide_fused_input_layer_is_bit_identical(dims, graph, monkeypatch):
+    """kernels/wide_input.hip (dZ_1 from the raw dgrad slices, the W_0 / b_0
+    step and the NEXT step's H_1 in one launch) against the separate dgrad
+    combine + update tiles + input-layer forward: the same parameters,
+    statistics and evaluation, bit for bit -- across an epoch wrap (4 batches,
+    9 steps), an evaluation in the middle (the carried H_1 is invalidated and
+    recomputed) and, with graph=True, epoch-graph replays."""
+    spec = MlpSpec(dims)
+    ds = synthetic_mnist(64 * 4, seed=29)
+    runs = []
+    for fused in (0, 1):
+        monkeypatch.setenv("HIPDSML_WIDE_FUSED_INPUT", str(fused))
+        t = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=5, graph=graph)
+        assert t.fused_input == bool(fused)
+        t.train_steps(5)
+        ev = t.evaluate(ds)
+        t.train_steps(9)
+        st = t.read_stats()
+        runs.append((t.P.cpu(), st.loss_sum, st.correct, ev, t.evaluate(ds)))
+    assert torch.equal(runs[1][0], runs[0][0])
+    assert runs[1][1:] == runs[0][1:]

@@ -1,0 +1,13 @@
+# Fused input layer: launch order A/B (before / after the update of the layers above)
+set -e
+T=${1:-r6fin3}
+R=$GRAFT_REPO_ROOT
+O=gpurun_out/$T
+mkdir -p $O
+for k in 1 2; do
+  for f in 0 1; do
+    HIPDSML_WIDE_INPUT_FIRST=$f timeout -k 10 200 python bench_wide.py --steps 200 --warmup 20 > $O/ab_${f}_$k.json 2>/dev/null
+    echo "first=$f $(cut -c1-140 $O/ab_${f}_$k.json)"
+  done
+done
+cd /tmp && export TMPDIR=/tmp && HIPDSML_WIDE_INPUT_FIRST=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/wprof -o run -- python $R/bench_wide.py --steps 100 --warmup 10 > $R/$O/wprof.log 2>&1 && cd $R && python tools/rocpd_summary.py $O/wprof/run_results.db --skip 200 --csv $O/wide_kernels.csv | cut -c1-150
