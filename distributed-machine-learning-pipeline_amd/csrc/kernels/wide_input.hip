@@ -42,7 +42,7 @@ typedef uint32_t wi_u4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWiThreads = 512;
 constexpr int kWiZp = 72;    // bf16 per row of the dZ_1^T image [16 n][64 m] (+8: conflict-free b128 reads)
-constexpr int kWiScP = 36;   // floats per row of a wave's gradient tile [16 n][32 k]
+constexpr int kWiScP = 68;   // floats per row of a wave's gradient tile [16 n][64 k]
 constexpr int kWiRedP = 17;  // floats per row of a chunk's forward partial [64 m][16 n]
 
 #ifdef HIPDSML_MEASURE
@@ -79,8 +79,10 @@ __device__ __forceinline__ uint32_t wi_lo(float v, uint32_t h) { return (__float
 template <int S>
 __global__ __launch_bounds__(kWiThreads, 1) void wide_input_k(WideInArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t zt[16 * kWiZp];
-  __shared__ __attribute__((aligned(16))) float sc[8][16 * kWiScP];
-  __shared__ __attribute__((aligned(16))) float red[8][64 * kWiRedP];
+  // the waves' gradient tiles [8][16 x 68], later (behind the bias barrier) the
+  // chunks' forward partials [8][64 x 17]: the same 34 KiB
+  __shared__ __attribute__((aligned(16))) float scr[8 * 16 * kWiScP];
+  static_assert(16 * kWiScP == 64 * kWiRedP, "LDS alias");
   __shared__ float bs[4][16];
   __shared__ float bn[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -188,33 +190,40 @@ __global__ __launch_bounds__(kWiThreads, 1) void wide_input_k(WideInArgs a) {
     bs[q][c] = d;
   }
 
-  // ---- 3. per 32-column step: gradient MFMAs, update, keep the new hi words ----
+  // ---- 3. two 32-column steps at a time: gradient MFMAs, ONE trip through the
+  // wave's LDS tile, update, keep the new hi words (the forward's B fragments) ----
   uint4 bw[4];
-  float* mysc = sc[w];
+  float* mysc = scr + w * 16 * kWiScP;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int ks = kb + 32 * u;
-    bw[u] = wi_zero();
-    if (ks >= ke) continue;  // wave-uniform
-    f32x4 acc[2];
+  for (int u2 = 0; u2 < 4; u2 += 2) {
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      acc[y] = {0.f, 0.f, 0.f, 0.f};
+    for (int uu = 0; uu < 2; ++uu) {
+      const int u = u2 + uu;
+      if (kb + 32 * u >= ke) continue;  // wave-uniform
+      f32x4 acc[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) acc[y] = wi_mfma(zf[h], xf[u][y][h], acc[y]);
+      for (int y = 0; y < 2; ++y) {
+        acc[y] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[y] = wi_mfma(zf[h], xf[u][y][h], acc[y]);
+      }
+      // [16 n][64 k] tile: lane (i, g) holds rows 4g + r, column 32 uu + 16y + i
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mysc[(4 * g + r) * kWiScP + 32 * uu + 16 * y + i] = acc[y][r] * a.alpha;
     }
-    // [16 n][32 k] through LDS: lane (i, g) holds rows 4g + r, column 16y + i
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mysc[(4 * g + r) * kWiScP + 16 * y + i] = acc[y][r] * a.alpha;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float4 g0 = *reinterpret_cast<const float4*>(mysc + i * kWiScP + 8 * g);
-    const float4 g1 = *reinterpret_cast<const float4*>(mysc + i * kWiScP + 8 * g + 4);
-    const int k = ks + 8 * g;
-    if (k < ke) {
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu) {
+      const int u = u2 + uu;
+      bw[u] = wi_zero();
+      const int k = kb + 32 * u + 8 * g;
+      if (kb + 32 * u >= ke || k >= ke) continue;
+      const float4 g0 = *reinterpret_cast<const float4*>(mysc + i * kWiScP + 32 * uu + 8 * g);
+      const float4 g1 = *reinterpret_cast<const float4*>(mysc + i * kWiScP + 32 * uu + 8 * g + 4);
       const uint32_t hw[4] = {wh[u].x, wh[u].y, wh[u].z, wh[u].w}, lw[4] = {wl[u].x, wl[u].y, wl[u].z, wl[u].w};
       float v[8];
 #pragma unroll
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(kWiThreads, 1) void wide_input_k(WideInArgs a) {
                                   reinterpret_cast<wi_u4*>(a.Wl + (int64_t)(n0 + i) * a.ldwl + k));
       bw[u] = make_uint4(nh[0], nh[1], nh[2], nh[3]);
     }
-    __builtin_amdgcn_wave_barrier();  // the tile's reads are done before the next step rewrites it
+    __builtin_amdgcn_wave_barrier();  // the tile's reads are done before the next pair rewrites it
   }
   WI_STAMP(3);
   __syncthreads();  // bs complete
@@ -264,7 +273,7 @@ __global__ __launch_bounds__(kWiThreads, 1) void wide_input_k(WideInArgs a) {
     }
   }
   WI_STAMP(5);
-  float* mine = red[w];
+  float* mine = scr + w * 64 * kWiRedP;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -277,9 +286,9 @@ __global__ __launch_bounds__(kWiThreads, 1) void wide_input_k(WideInArgs a) {
     const int e = tid + kWiThreads * j;
     const int m = e >> 4, n = e & 15;
     const int o = m * kWiRedP + n;
-    float x = red[0][o];
+    float x = scr[o];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) x += red[q][o];
+    for (int q = 1; q < 8; ++q) x += scr[q * 64 * kWiRedP + o];
     x *= a.falpha;
     x += bn[n];
     x = fmaxf(x, 0.f);
