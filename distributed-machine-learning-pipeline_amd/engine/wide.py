@@ -21,6 +21,11 @@ Per step, with L layers (every kernel hand-written for gfx950 MFMA):
   dgrad     dZ_l = (dZ_{l+1} . W_l) * (H_l > 0)  gemm_skinny.hip NN (W untransposed)
   wgrad     W_l -= lr * dZ_{l+1}^T H_l, bf16 W_l refreshed, b_l step
             (kernels/wgrad_sgd.hip, straight from the row-major activations)
+  input     one replica: the last dgrad leaves raw split-K slices and ONE
+            launch (kernels/wide_input.hip) sums them into dZ_1, steps W_0 / b_0
+            and computes the NEXT step's H_1 from the updated rows (so the step
+            has no separate input-layer forward); bit-identical to the
+            separate kernels
 With several replicas, two gradient syncs:
   rccl / ring / torch   the wgrad kernel writes the gradient instead, and each
             layer's bucket is all-reduced + applied on a comm stream that
@@ -194,7 +199,6 @@ class WideMlpTrainer:
                             and L >= 3 and batch == 64 and d[0] % 16 == 0 and d[0] <= 1024 and d[1] % 64 == 0
                             and self.head_slabs and self.plans["b1"][4] <= 8 and self.pd[0] == d[0])
         self._carry: Optional[int] = None
-        self._input_first = os.environ.get("HIPDSML_WIDE_INPUT_FIRST", "0") == "1"
         if self.fused_input:
             self.H1buf = [self.H[1], torch.zeros_like(self.H[1])]
             # each batch's input rows twice more, in the fused launch's fragment
@@ -422,17 +426,10 @@ class WideMlpTrainer:
                                None, b, None, cur[l], self.Wlo[l]))
             bn = (bi + 1) % self.nbatches
             _, b0 = self.views[0]
-            first = self._input_first
-            if first:
-                C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi],
-                                  self.XF[bn], cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale,
-                                  self.H1buf[1 - p], Bt, d[1], d[0])
             for i in range(0, len(layers), 4):
                 C.wgrad_sgd_multi(layers[i:i + 4])
-            if not first:
-                C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi],
-                                  self.XF[bn], cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale,
-                                  self.H1buf[1 - p], Bt, d[1], d[0])
+            C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi], self.XF[bn],
+                              cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale, self.H1buf[1 - p], Bt, d[1], d[0])
             self.steps_done += 1
             self._carry = self.steps_done
             return
