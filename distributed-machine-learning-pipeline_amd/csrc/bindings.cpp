@@ -693,12 +693,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (py::handle it : layers) v.push_back(wg_layer(it));
     hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
   }, py::arg("layers"), py::arg("tile") = 0);
-  m.def("wide_input_step", [bf16p](torch::Tensor slabs, int64_t S, torch::Tensor H1, c10::optional<torch::Tensor> dzo,
-                                  torch::Tensor XG, torch::Tensor XF, torch::Tensor Wh, torch::Tensor Wl,
-                                  torch::Tensor Wb, torch::Tensor bias, double alpha, double lr, torch::Tensor Hn,
-                                  int64_t M, int64_t N, int64_t K) {
-    // XG: this step's rows in gradient-fragment order, contiguous [ceil(K/16)][2][16][32];
-    // XF: the next step's rows k-blocked, contiguous [ceil(K/32)][64][32]
+  // the fused input layer's operands (kernels/wide_input.hip, WideInArgs):
+  // XG this step's rows in gradient-fragment order, contiguous [ceil(K/16)][2][16][32];
+  // XF the next step's rows k-blocked, contiguous [ceil(K/32)][64][32]
+  auto wide_in_args = [bf16p](torch::Tensor slabs, int64_t S, torch::Tensor H1, c10::optional<torch::Tensor> dzo,
+                              torch::Tensor XG, torch::Tensor XF, torch::Tensor Wh, torch::Tensor Wl, torch::Tensor Wb,
+                              torch::Tensor bias, double alpha, double lr, torch::Tensor Hn, int64_t M, int64_t N,
+                              int64_t K) {
     auto rows2 = [&](const torch::Tensor& t, int64_t r, int64_t c, const char* nm) {
       TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= r && t.size(1) >= c, nm, " shape");
     };
@@ -723,11 +724,32 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.bias = bias.data_ptr<float>(); a.alpha = (float)alpha; a.lr = (float)lr; a.falpha = 1.f;
     a.Hn = bf16p(Hn, "Hn"); a.ldhn = Hn.stride(0);
     a.M = (int)M; a.N = (int)N; a.K = (int)K; a.kq = (int)((((K + 7) / 8 + 31) / 32) * 32);
+    return a;
+  };
+  m.def("wide_input_step", [wide_in_args](torch::Tensor slabs, int64_t S, torch::Tensor H1,
+                                          c10::optional<torch::Tensor> dzo, torch::Tensor XG, torch::Tensor XF,
+                                          torch::Tensor Wh, torch::Tensor Wl, torch::Tensor Wb, torch::Tensor bias,
+                                          double alpha, double lr, torch::Tensor Hn, int64_t M, int64_t N, int64_t K) {
+    const WideInArgs a = wide_in_args(slabs, S, H1, dzo, XG, XF, Wh, Wl, Wb, bias, alpha, lr, Hn, M, N, K);
     hip_ok(wide_input_step(a, cur_stream()), "wide_input_step");
   }, py::arg("slabs"), py::arg("S"), py::arg("H1"), py::arg("dzo"), py::arg("XG"), py::arg("XF"), py::arg("Wh"),
      py::arg("Wl"), py::arg("Wb"), py::arg("bias"), py::arg("alpha"), py::arg("lr"), py::arg("Hn"), py::arg("M"),
      py::arg("N"), py::arg("K"),
      "wide input layer: dZ_1 from raw dgrad slices, W_0 / b_0 SGD (split master), next step's H_1");
+  m.def("wgrad_sgd_multi_in", [wg_layer, wide_in_args](py::list layers, torch::Tensor slabs, int64_t S,
+                                                     torch::Tensor H1, c10::optional<torch::Tensor> dzo,
+                                                     torch::Tensor XG, torch::Tensor XF, torch::Tensor Wh,
+                                                     torch::Tensor Wl, torch::Tensor Wb, torch::Tensor bias,
+                                                     double alpha, double lr, torch::Tensor Hn, int64_t M, int64_t N,
+                                                     int64_t K) {
+    std::vector<WgLayer> v;
+    for (py::handle it : layers) v.push_back(wg_layer(it));
+    const WideInArgs a = wide_in_args(slabs, S, H1, dzo, XG, XF, Wh, Wl, Wb, bias, alpha, lr, Hn, M, N, K);
+    hip_ok(wgrad_sgd_multi_in(v.data(), (int)v.size(), a, cur_stream()), "wgrad_sgd_multi_in");
+  }, py::arg("layers"), py::arg("slabs"), py::arg("S"), py::arg("H1"), py::arg("dzo"), py::arg("XG"), py::arg("XF"),
+     py::arg("Wh"), py::arg("Wl"), py::arg("Wb"), py::arg("bias"), py::arg("alpha"), py::arg("lr"), py::arg("Hn"),
+     py::arg("M"), py::arg("N"), py::arg("K"),
+     "the update of the layers above the input layer (64 x 64 tiles) with the input layer's strips in the same launch");
   m.def("gemm_skinny_stamps", []() {
     std::vector<uint64_t> v(1024 * 5);
     hip_ok(gemm_skinny_read_stamps(v.data()), "gemm_skinny_read_stamps");

@@ -386,6 +386,12 @@ struct WideInArgs {
   int M, N, K, kq;       // kq: columns per wave, gemm_rows64_k's split ((ceil(K/8) + 31) / 32 * 32)
 };
 hipError_t wide_input_step(const WideInArgs& a, hipStream_t s);
+hipError_t wide_input_check(const WideInArgs& a);  // the shapes / alignment both forms assume
+// The same input-layer work as 16-row strip workgroups at the FRONT of the
+// update launch of the layers above (kernels/wgrad_sgd.hip wgrad_multi_in_k):
+// the strips' HBM phases overlap the 64 x 64 tiles' weight stream.  layers:
+// every layer but the input one, batch 64 (square tiles); bit-identical.
+hipError_t wgrad_sgd_multi_in(const WgLayer* layers, int n, const WideInArgs& in, hipStream_t s);
 #ifdef HIPDSML_MEASURE
 hipError_t wide_input_read_stamps(uint64_t* host_out);  // [1024][8], measurement builds
 void wide_input_set_stamping(bool on);

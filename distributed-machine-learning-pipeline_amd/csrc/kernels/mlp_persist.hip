@@ -1561,6 +1561,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       if (pok && peer_rows) hop_wait(a, s, 4 * (m >> 4) + (gn & 3));  // measurement builds only
       ok = __syncthreads_and(pok ? 1 : 0) != 0;
       if (!ok) break;
+      PK_STAMP(0, 6);  // every replica's dZ1 rows of the tile in LDS
     }
     // ---- gatherers: C(s+1)[chain c's 16 rows x 16 n] = -lr sum_r' G_r'
     // dZ1_r'(s)[:, tile]; wave w contracts m' = 16 w .. +15 of every replica,

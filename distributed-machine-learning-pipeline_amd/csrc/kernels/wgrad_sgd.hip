@@ -1212,6 +1212,280 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
   return hipGetLastError();
 }
 
+namespace {
+// ---------------------------------------------------------------------------
+// The wide step's input layer as strips inside the update launch (one replica,
+// batch 64): the work of kernels/wide_input.hip -- dZ_1 from the last dgrad's
+// raw slices, the W_0 / b_0 step, the NEXT step's H_1 -- re-cut for this
+// launch's 256-thread, <= 96-register, <= 32 KiB workgroups, so that 256
+// strip workgroups (16 rows of W_0 each, first in the grid) run beside the
+// 64 x 64 tiles of the layers above: their load / store phases, which left HBM
+// idle between them in a launch of their own (profiles/r6_wide_fused_input.json),
+// overlap the tiles' weight stream.  Same arithmetic and orders as wide_input.hip
+// (bit-identical): wave w takes input chunks w and w + 4 of gemm_rows64_k's
+// 8-chunk split one after the other, its chunk-w forward partial goes to LDS,
+// the chunk-(w + 4) one stays in registers until the first four are summed.
+constexpr int kWsZp = 72;                                // bf16 a row of the dZ_1^T image [16][64 + 8]
+constexpr int kWsScP = 36;                               // floats a row of a wave's gradient tile [16][32 + 4]
+constexpr int kWsRedP = 17;                              // floats a row of a chunk's forward partial [64][16 + 1]
+constexpr int kWsOffSc = 16 * kWsZp * 2;                 // 2,304
+constexpr int kWsOffP = kWsOffSc + 4 * 16 * kWsScP * 4;  // + 9,216
+constexpr int kWsLds = kWsOffP + 4 * 64 * kWsRedP * 4;   // + 17,408 = 28,928: still 5 workgroups a CU
+static_assert(kWsLds >= kWgLdsTot && kWsLds <= 32 * 1024, "LDS carve");
+
+struct WgMultiIn {
+  WgMulti m;
+  WideInArgs in;
+  int strips;  // in.N / 16 strip workgroups, then m's tiles
+};
+
+__device__ __forceinline__ uint4 ws_zero() { return make_uint4(0u, 0u, 0u, 0u); }
+__device__ __forceinline__ f32x4 ws_mfma(uint4 a, uint4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, a), __builtin_bit_cast(wg_bf16x8, b),
+                                                  c, 0, 0, 0);
+}
+
+template <int S>
+__device__ __forceinline__ void wide_strip(const WideInArgs& a, int sb, char* lds) {
+  uint16_t* zt = reinterpret_cast<uint16_t*>(lds);
+  float* sc = reinterpret_cast<float*>(lds + kWsOffSc);
+  float* P = reinterpret_cast<float*>(lds + kWsOffP);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+  const int n0 = sb * 16, K = a.K;
+
+  // ---- A. dZ_1 [64 m][16 n]: thread -> row tid >> 2, columns 4 (tid & 3) .. +3 ----
+  {
+    const int zm = tid >> 2, zn = 4 * (tid & 3);
+    const int tile = n0 >> 6, nl = (n0 & 63) + zn;
+    float4 sl[S];
+#pragma unroll
+    for (int z = 0; z < S; ++z)
+      sl[z] = *reinterpret_cast<const float4*>(a.slabs + ((int64_t)z * a.tiles + tile) * 4096 + zm * 64 + nl);
+    const uint2 mk = *reinterpret_cast<const uint2*>(a.H1 + (int64_t)zm * a.ldh1 + n0 + zn);
+    float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);  // the split-K combine's order
+#pragma unroll
+    for (int z = 0; z < S; ++z) {
+      sm.x += sl[z].x; sm.y += sl[z].y; sm.z += sl[z].z; sm.w += sl[z].w;
+    }
+    float x[4] = {sm.x * a.zalpha + a.zbias, sm.y * a.zalpha + a.zbias, sm.z * a.zalpha + a.zbias,
+                  sm.w * a.zalpha + a.zbias};
+    const uint32_t mw[4] = {mk.x << 16, mk.x & 0xffff0000u, mk.y << 16, mk.y & 0xffff0000u};
+    uint16_t q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!(__uint_as_float(mw[e]) > 0.f)) x[e] = 0.f;
+      q[e] = f32_to_bf16(x[e]);
+      zt[(zn + e) * kWsZp + zm] = q[e];
+    }
+    if (a.dzo)
+      *reinterpret_cast<uint2*>(a.dzo + (int64_t)zm * a.lddz + n0 + zn) =
+          make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+  }
+  const float bold = a.bias[n0 + (tid & 15)];
+  lds_barrier();
+  uint4 zf[2];  // A fragments: dZ_1 column n0 + i, batch rows 32h + 8g .. +7
+#pragma unroll
+  for (int h = 0; h < 2; ++h) zf[h] = *reinterpret_cast<const uint4*>(zt + i * kWsZp + 32 * h + 8 * g);
+  if (w == 0) {  // the bias gradient's four 16-row partial column sums
+    const int c = lane & 15, qq = lane >> 4;
+    float d = 0.f;
+#pragma unroll
+    for (int r = 16 * qq; r < 16 * qq + 16; ++r) d += bf16_to_f32(zt[c * kWsZp + r]);
+    sc[qq * 16 + c] = d;
+  }
+  lds_barrier();
+  if (tid < 16) {
+    const float db = a.alpha * (((sc[tid] + sc[16 + tid]) + sc[32 + tid]) + sc[48 + tid]);
+    float b = bold;
+    b -= a.lr * db;
+    a.bias[n0 + tid] = b;
+    sc[64 + tid] = b;
+  }
+  lds_barrier();
+  const float bnv = sc[64 + (tid & 15)];  // the updated bias of this thread's output column
+  lds_barrier();                          // sc is the gradient tile from here on
+
+  // ---- B. chunks w, then w + 4: per 32-column step the gradient MFMAs, the
+  // update (new hi words = the forward's B fragments), the forward MFMAs ----
+  float* mysc = sc + w * 16 * kWsScP;
+  // buffer-addressed (32-bit lane offsets: 64-bit pointers per stream spilled)
+  const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.Wh), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc(a.Wl, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwb = __builtin_amdgcn_make_buffer_rsrc(a.Wb, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxg = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.XG), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxf = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.XF), (short)0, 0x7fffffff, 0x00020000);
+  const int owh = (int)((n0 + i) * a.ldwh * 2), owl = (int)((n0 + i) * a.ldwl * 2), owb = (int)((n0 + i) * a.ldwb * 2);
+  const int oxg = 64 * i + 16 * g, oxf = 64 * i + 16 * g;
+  f32x4 af2[4];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) {
+    const int c = w + 4 * cc;
+    const int kb = a.kq * c, ke = min(K, kb + a.kq);
+    f32x4 af[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) af[t] = {0.f, 0.f, 0.f, 0.f};
+    if (kb < ke) {  // wave-uniform (chunk 7 of 784 inputs is empty)
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {
+        const int ks = kb + 32 * u;
+        const int k = ks + 8 * g;
+        const bool kvl = k < ke;
+        const int kc = kvl ? k : 0;
+        // the step's loads in one batch (W from HBM first)
+        const uint4 wh = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwh, owh + 2 * kc, 0, 0));
+        const uint4 wl = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwl, owl + 2 * kc, 0, 0));
+        uint4 xf[2][2];
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const int ky = ks + 16 * y;
+          const int kg = ky < ke ? ky >> 4 : 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            xf[y][h] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxg, oxg + kg * 2048 + 1024 * h, 0, 0));
+        }
+        const int kx = ks < ke ? ks : 0;
+        uint4 fa[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          fa[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxf, oxf + (kx >> 5) * 4096 + 1024 * t, 0, 0));
+        uint4 bw = ws_zero();
+        if (ks < ke) {  // wave-uniform
+          f32x4 acc[2];
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            acc[y] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[y] = ws_mfma(zf[h], xf[y][h], acc[y]);
+          }
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mysc[(4 * g + r) * kWsScP + 16 * y + i] = acc[y][r] * a.alpha;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const float4 g0 = *reinterpret_cast<const float4*>(mysc + i * kWsScP + 8 * g);
+          const float4 g1 = *reinterpret_cast<const float4*>(mysc + i * kWsScP + 8 * g + 4);
+          if (kvl) {
+            float wv[8];
+            hl_join8(wh, wl, wv);
+            wv[0] -= a.lr * g0.x; wv[1] -= a.lr * g0.y; wv[2] -= a.lr * g0.z; wv[3] -= a.lr * g0.w;
+            wv[4] -= a.lr * g1.x; wv[5] -= a.lr * g1.y; wv[6] -= a.lr * g1.z; wv[7] -= a.lr * g1.w;
+            uint32_t nh[4], nlw[4];
+            hl_pack8(wv, nh, nlw);
+            __builtin_amdgcn_raw_buffer_store_b128(wg_u4{nh[0], nh[1], nh[2], nh[3]}, rwb, owb + 2 * k, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(wg_u4{nlw[0], nlw[1], nlw[2], nlw[3]}, rwl, owl + 2 * k, 0, 0);
+            bw = make_uint4(nh[0], nh[1], nh[2], nh[3]);
+          }
+          __builtin_amdgcn_wave_barrier();  // the tile's reads done before the next step rewrites it
+        }
+        // gemm_rows64_k's step: zero operands past the chunk (it issues them too)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) af[t] = ws_mfma(kvl ? fa[t] : ws_zero(), kvl ? bw : ws_zero(), af[t]);
+      }
+    }
+    if (cc == 0) {
+      float* mine = P + w * 64 * kWsRedP;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mine[(16 * t + 4 * g + r) * kWsRedP + i] = af[t][r];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af2[t] = af[t];
+    }
+  }
+  lds_barrier();
+  // ---- C. the chunk partials in chunk order, the updated bias, ReLU -> bf16 ----
+  const int on = tid & 15;
+  float xs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = ((tid >> 4) + 16 * j) * kWsRedP + on;
+    float x = P[o];
+#pragma unroll
+    for (int qq = 1; qq < 4; ++qq) x += P[qq * 64 * kWsRedP + o];
+    xs[j] = x;
+  }
+  lds_barrier();
+  {
+    float* mine = P + w * 64 * kWsRedP;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mine[(16 * t + 4 * g + r) * kWsRedP + i] = af2[t][r];
+  }
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = (tid >> 4) + 16 * j;
+    const int o = m * kWsRedP + on;
+    float x = xs[j];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) x += P[qq * 64 * kWsRedP + o];
+    x *= a.falpha;
+    x += bnv;
+    x = fmaxf(x, 0.f);
+    a.Hn[(int64_t)m * a.ldhn + n0 + on] = f32_to_bf16(x);
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(256, 5) void wgrad_multi_in_k(WgMultiIn mi) {
+  __shared__ __attribute__((aligned(16))) char lds[kWsLds];
+  const int b0 = blockIdx.x;
+  if (b0 < mi.strips) {
+    wide_strip<S>(mi.in, b0, lds);
+    return;
+  }
+  const WgMulti& m = mi.m;
+  const int b = b0 - mi.strips;
+  int j = 0;
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (q < m.n && b >= m.start[q]) j = q;
+  const int t = b - m.start[j];
+  WgArgs a = m.l[0];
+  int kts = m.ktiles[0];
+#pragma unroll
+  for (int q = 1; q < kWgMaxLayers; ++q)
+    if (j == q) { a = m.l[q]; kts = m.ktiles[q]; }
+  int kt, nt;
+  if ((m.start[j] & 7) == 0) wg_tile_xcd(t, kts, (a.N + 63) / 64, kt, nt);
+  else { kt = t % kts; nt = t / kts; }
+  wgrad_tile(a, kt, nt, lds);
+}
+}  // namespace
+
+hipError_t wgrad_sgd_multi_in(const WgLayer* layers, int n, const WideInArgs& in, hipStream_t s) {
+  if (n < 1 || n > kWgMaxLayers || wide_input_check(in) != hipSuccess) return hipErrorInvalidValue;
+  WgMultiIn mi{};
+  WgMulti& m = mi.m;
+  m.n = n;
+  int t = 0;
+  for (int j = 0; j < n; ++j) {
+    const WgLayer& L = layers[j];
+    if (!wg_valid(L) || L.M != 64) return hipErrorInvalidValue;
+    m.l[j] = L;
+    m.start[j] = t;
+    m.ktiles[j] = (L.K + 63) / 64;
+    t += m.ktiles[j] * ((L.N + 63) / 64);
+  }
+  for (int j = n; j <= kWgMaxLayers; ++j) m.start[j] = t;
+  for (int j = n; j < kWgMaxLayers; ++j) { m.l[j] = layers[0]; m.ktiles[j] = m.ktiles[0]; }
+  mi.in = in;
+  mi.strips = in.N / 16;  // a multiple of 8 keeps the tiles' XCD map (block b % 8)
+  if (mi.strips & 7) return hipErrorInvalidValue;
+  const dim3 grid(mi.strips + t);
+  switch (in.S) {
+    case 1: hipLaunchKernelGGL(wgrad_multi_in_k<1>, grid, dim3(256), 0, s, mi); break;
+    case 2: hipLaunchKernelGGL(wgrad_multi_in_k<2>, grid, dim3(256), 0, s, mi); break;
+    case 4: hipLaunchKernelGGL(wgrad_multi_in_k<4>, grid, dim3(256), 0, s, mi); break;
+    default: hipLaunchKernelGGL(wgrad_multi_in_k<8>, grid, dim3(256), 0, s, mi); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile) {
   if (n < 1 || n > kWgMaxLayers || (tile != 0 && tile != 64 && tile != kBgT && tile != kWgRowBlkTile))
     return hipErrorInvalidValue;

@@ -315,7 +315,23 @@ void wide_input_set_stamping(bool on) {
 }
 #endif
 
+hipError_t wide_input_check(const WideInArgs& a) {
+  // shapes the kernels' maps assume (checked here, before any launch)
+  if (a.M != 64 || a.N <= 0 || (a.N & 15) || a.K <= 0 || (a.K & 15) || a.K > 8 * 128) return hipErrorInvalidValue;
+  if (a.kq != (((a.K + 7) / 8 + 31) / 32) * 32) return hipErrorInvalidValue;  // gemm_rows64_k's 8-wave split
+  if ((a.S != 1 && a.S != 2 && a.S != 4 && a.S != 8) || a.tiles != (a.N + 63) / 64) return hipErrorInvalidValue;
+  if (!a.slabs || !a.H1 || !a.XG || !a.XF || !a.Wh || !a.Wl || !a.Wb || !a.bias || !a.Hn)
+    return hipErrorInvalidValue;
+  if ((a.ldwh & 7) || (a.ldwl & 7) || (a.ldwb & 7) || (a.ldh1 & 3) || (a.dzo && (a.lddz & 3)))
+    return hipErrorInvalidValue;
+  const uintptr_t al = (uintptr_t)a.Wh | (uintptr_t)a.Wl | (uintptr_t)a.Wb | (uintptr_t)a.XG | (uintptr_t)a.XF;
+  if ((al & 15) || ((uintptr_t)a.slabs & 15) || ((uintptr_t)a.H1 & 7) || ((uintptr_t)a.dzo & 7))
+    return hipErrorInvalidValue;
+  return hipSuccess;
+}
+
 hipError_t wide_input_step(const WideInArgs& a, hipStream_t s) {
+  if (wide_input_check(a) != hipSuccess) return hipErrorInvalidValue;
   // shapes the kernel's maps assume (checked here, before any launch)
   if (a.M != 64 || a.N <= 0 || (a.N & 15) || a.K <= 0 || (a.K & 15) || a.K > 8 * 128) return hipErrorInvalidValue;
   if (a.kq != (((a.K + 7) / 8 + 31) / 32) * 32) return hipErrorInvalidValue;  // gemm_rows64_k's 8-wave split

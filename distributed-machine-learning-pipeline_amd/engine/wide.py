@@ -199,6 +199,7 @@ class WideMlpTrainer:
                             and L >= 3 and batch == 64 and d[0] % 16 == 0 and d[0] <= 1024 and d[1] % 64 == 0
                             and self.head_slabs and self.plans["b1"][4] <= 8 and self.pd[0] == d[0])
         self._carry: Optional[int] = None
+        self._input_beside = os.environ.get("HIPDSML_WIDE_INPUT_BESIDE", "1") == "1"
         if self.fused_input:
             self.H1buf = [self.H[1], torch.zeros_like(self.H[1])]
             # each batch's input rows twice more, in the fused launch's fragment
@@ -426,10 +427,16 @@ class WideMlpTrainer:
                                None, b, None, cur[l], self.Wlo[l]))
             bn = (bi + 1) % self.nbatches
             _, b0 = self.views[0]
-            for i in range(0, len(layers), 4):
-                C.wgrad_sgd_multi(layers[i:i + 4])
-            C.wide_input_step(self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi], self.XF[bn],
-                              cur[0], self.Wlo[0], nxt[0], b0, 1.0, scale, self.H1buf[1 - p], Bt, d[1], d[0])
+            args = (self.Cp, self.plans["b1"][4], self.H1buf[p], None, self.XG[bi], self.XF[bn], cur[0], self.Wlo[0],
+                    nxt[0], b0, 1.0, scale, self.H1buf[1 - p], Bt, d[1], d[0])
+            if self._input_beside and len(layers) <= 4:
+                # the input layer's strips first in the update launch of the layers
+                # above: their HBM phases overlap the tiles' weight stream
+                C.wgrad_sgd_multi_in(layers, *args)
+            else:
+                for i in range(0, len(layers), 4):
+                    C.wgrad_sgd_multi(layers[i:i + 4])
+                C.wide_input_step(*args)
             self.steps_done += 1
             self._carry = self.steps_done
             return

@@ -380,8 +380,11 @@ def test_wide_fused_input_layer_is_bit_identical(dims, graph, monkeypatch):
     spec = MlpSpec(dims)
     ds = synthetic_mnist(64 * 4, seed=29)
     runs = []
-    for fused in (0, 1):
+    # separate kernels; the input-layer launch of its own; its strips inside
+    # the update launch of the layers above (kernels/wgrad_sgd.hip wgrad_multi_in_k)
+    for fused, beside in ((0, 0), (1, 0), (1, 1)):
         monkeypatch.setenv("HIPDSML_WIDE_FUSED_INPUT", str(fused))
+        monkeypatch.setenv("HIPDSML_WIDE_INPUT_BESIDE", str(beside))
         t = WideMlpTrainer(spec, ds, batch=64, lr=0.05, seed=5, graph=graph)
         assert t.fused_input == bool(fused)
         t.train_steps(5)
@@ -389,5 +392,6 @@ def test_wide_fused_input_layer_is_bit_identical(dims, graph, monkeypatch):
         t.train_steps(9)
         st = t.read_stats()
         runs.append((t.P.cpu(), st.loss_sum, st.correct, ev, t.evaluate(ds)))
-    assert torch.equal(runs[1][0], runs[0][0])
-    assert runs[1][1:] == runs[0][1:]
+    for r in runs[1:]:
+        assert torch.equal(r[0], runs[0][0])
+        assert r[1:] == runs[0][1:]

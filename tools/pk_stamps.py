@@ -53,6 +53,13 @@ def decode(v, spec) -> dict:
             "l1_z1_stored_to_step_end_us": med([(st[0][s][3] - st[0][s][4]) / 100.0 for s in range(8)]),
             "z1_stored_to_chain_seen_us": med([(st[1][s + 1][1] - st[0][s][4]) / 100.0 for s in range(7)]),
         }
+        if all(st[0][s][6] for s in range(8)):
+            # data-parallel Gram forms (merged poll): layer-1 block 0 (a gatherer)
+            # before the poll -> every replica's dZ1 rows in LDS -> Z1 stored
+            out["gram"]["l1_dz1_poll_us"] = med([(st[0][s][6] - st[0][s][2]) / 100.0 for s in range(8)])
+            out["gram"]["l1_correction_publish_us"] = med([(st[0][s][4] - st[0][s][6]) / 100.0 for s in range(8)])
+            out["gram"]["chain_dz1_publish_to_l1_rows_us"] = med(
+                [(st[0][s][6] - st[1][s][4]) / 100.0 for s in range(8)])
         if all(st[0][s][5] for s in range(8)):
             # single replica: the correction block of column 0 (chains' XCD)
             out["gram"]["chain_dz1_publish_to_cb_seen_us"] = med(
