@@ -735,9 +735,9 @@ __device__ __forceinline__ void rb_for(F& f) {
 // the loop): ops issued after it are this tile's later blocks, the last tile's
 // 8 stores (tile > 0), this tile's 8 W loads and the refills of iterations
 // 0 .. B - 1 (slot b takes the next tile's block b in iteration b)
-template <int NBLK, int B, bool LATER, bool MORE>
+template <int NBLK, int B, bool LATER, bool MORE, int NW = 8>
 __device__ __forceinline__ void rb_vm_block() {
-  rb_vm<(NBLK - 2 - B) + (LATER ? 8 : 0) + 8 + ((MORE && B > 0) ? B : 0)>();
+  rb_vm<(NBLK - 2 - B) + (LATER ? NW : 0) + NW + ((MORE && B > 0) ? B : 0)>();
 }
 __device__ __forceinline__ void rb_dsw32(uint32_t addr, float v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
@@ -799,8 +799,19 @@ __device__ __forceinline__ void rb_frag_issue(uint32_t img, int c0, int lane, wg
   hi = bg_dstr(img + r1 * PITCH + 16 * (ch ^ s1) + 8 * (p & 1));
 }
 
-template <int NBLK>
-__global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
+// WAVES: 4 (wave w owns W rows 32 w .. +31 of the 128-row unit: two 16-row
+// MFMA A fragments, one wave a SIMD) or 8 (rows 16 w .. +15, one fragment, two
+// waves a SIMD: the waits of one hide behind the other's issue).  Same
+// fragments, same MFMA chain per output, same epilogue arithmetic: the two
+// forms are bit-identical.
+template <int NBLK, int WAVES>
+__device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
+  static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
+  constexpr int RW = kRbN / WAVES;       // W rows of a wave
+  constexpr int XM = RW / 16;            // its 16-row MFMA A fragments
+  constexpr int JJ = kRbN / (8 * WAVES);  // epilogue rows of a thread (er + 8 WAVES jj)
+  constexpr int NW = 2 * JJ;             // W loads (hi + lo) and stores of a thread a tile
+  constexpr int ZJ = 8 / WAVES;          // Z chunk pieces (4 rows x 256 B) a wave DMAs a chunk
   extern __shared__ __attribute__((aligned(16))) char rb_lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -842,16 +853,17 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(a.X), (short)0, (int)(a.M * a.ldx * 2), 0x00020000);
     const int nmax = (int)((a.N + 7) & ~7) - 8, kmax = (int)((a.K + 7) & ~7) - 8;
-    int zv[2];  // this lane's Z chunk offset (row r of the chunk, clamped column), bytes
+    int zv[ZJ];  // this lane's Z chunk offset (row r of the chunk, clamped column), bytes
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int r = 8 * w + 4 * jj + (lane >> 4), pc = lane & 15;
+    for (int jj = 0; jj < ZJ; ++jj) {
+      const int r = 4 * (ZJ * w + jj) + (lane >> 4), pc = lane & 15;
       zv[jj] = (int)((r * a.ldz + min(n0 + 8 * (pc ^ bg_swz(r)), nmax)) * 2);
     }
-    const int xr = 8 * w + (lane >> 3), xc = 8 * ((lane & 7) ^ wg_swz(xr));
+    // X ring pieces: 4 waves send 8 rows (1 KiB) of a block each, 8 waves 4 rows (lanes 0-31)
+    const int xr = (32 / WAVES) * w + (lane >> 3), xc = 8 * ((lane & 7) ^ wg_swz(xr & 31));
 
     // ---- Z^T fragments into registers: 32-row chunks [32][128] (256-B rows), 8 per phase ----
-    wg_u4 zf[16][2];
+    wg_u4 zf[16][XM];
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       if (8 * ph < nblk) {
@@ -860,8 +872,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           const int c = 8 * ph + cc;
           if (c < nblk) {
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (wg_lptr)(rb_lds + cc * 8192 + (8 * w + 4 * jj) * 256), 16,
+            for (int jj = 0; jj < ZJ; ++jj)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (wg_lptr)(rb_lds + cc * 8192 + 4 * (ZJ * w + jj) * 256), 16,
                                                       (DSML_MEASURE_KNOB(rb.dbg) & 2) ? kRbOob : zv[jj] + (int)(32 * c * a.ldz * 2), 0, 0, 0);
           }
         }
@@ -871,13 +883,20 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         for (int cc = 0; cc < 8; ++cc) {
           const int c = 8 * ph + cc;
           if (c < nblk) {
-            wg_u2 lo0, hi0, lo1, hi1;
-            // [c][xm]: W rows 32 w + 16 xm + l % 16, batch rows 32 c + 8 (l / 16) ..
-            rb_frag_issue<256>(ring + cc * 8192, 32 * w, lane, lo0, hi0);
-            rb_frag_issue<256>(ring + cc * 8192, 32 * w + 16, lane, lo1, hi1);
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo0), "+v"(hi0), "+v"(lo1), "+v"(hi1)::"memory");
-            zf[c][0] = wg_u4{lo0.x, lo0.y, hi0.x, hi0.y};
-            zf[c][1] = wg_u4{lo1.x, lo1.y, hi1.x, hi1.y};
+            // [c][xm]: W rows RW w + 16 xm + l % 16, batch rows 32 c + 8 (l / 16) ..
+            if constexpr (XM == 2) {
+              wg_u2 lo0, hi0, lo1, hi1;
+              rb_frag_issue<256>(ring + cc * 8192, RW * w, lane, lo0, hi0);
+              rb_frag_issue<256>(ring + cc * 8192, RW * w + 16, lane, lo1, hi1);
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo0), "+v"(hi0), "+v"(lo1), "+v"(hi1)::"memory");
+              zf[c][0] = wg_u4{lo0.x, lo0.y, hi0.x, hi0.y};
+              zf[c][XM - 1] = wg_u4{lo1.x, lo1.y, hi1.x, hi1.y};
+            } else {
+              wg_u2 lo0, hi0;
+              rb_frag_issue<256>(ring + cc * 8192, RW * w, lane, lo0, hi0);
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo0), "+v"(hi0)::"memory");
+              zf[c][0] = wg_u4{lo0.x, lo0.y, hi0.x, hi0.y};
+            }
           }
         }
         rb_barrier();  // the chunks' slots are free again
@@ -886,12 +905,14 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 
     // ---- bias gradient (the segment holding k tile 0): column sums of Z, from the fragments ----
     if (kt0 == 0 && (a.bias || a.bgrad)) {
-      float sm[2] = {0.f, 0.f};
+      float sm[XM];
+#pragma unroll
+      for (int xm = 0; xm < XM; ++xm) sm[xm] = 0.f;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         if (c < nblk) {
 #pragma unroll
-          for (int xm = 0; xm < 2; ++xm) {
+          for (int xm = 0; xm < XM; ++xm) {
             const wg_u4 v = zf[c][xm];
             sm[xm] += ((bf16_to_f32(v.x & 0xffffu) + bf16_to_f32(v.x >> 16)) +
                        (bf16_to_f32(v.y & 0xffffu) + bf16_to_f32(v.y >> 16))) +
@@ -901,10 +922,10 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         }
       }
 #pragma unroll
-      for (int xm = 0; xm < 2; ++xm) {
+      for (int xm = 0; xm < XM; ++xm) {
         sm[xm] += __shfl_xor(sm[xm], 16, 64);
         sm[xm] += __shfl_xor(sm[xm], 32, 64);
-        const int n = n0 + 32 * w + 16 * xm + i;
+        const int n = n0 + RW * w + 16 * xm + i;
         if (lane < 16 && n < a.N) {
           const float db = a.alpha * sm[xm];
           if (a.bias) a.bias[n] -= a.lr * db;
@@ -916,9 +937,13 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
 
     // ---- X ring: block b of local k tile lt -> slot b (wave w: rows 8 w .. +7) ----
     auto xdma = [&](int lt, int b) __attribute__((always_inline)) {
+      // 8 waves: lanes 0-31 only (a lane's LDS word is base + 16 lane: lanes
+      // 32-63 would land in the next wave's rows); still one op a wave a
+      // block, so the counts below are the same for every wave
       const int off = (int)(((32 * b + xr) * a.ldx + min((kt0 + lt) * 64 + xc, kmax)) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (wg_lptr)(rb_lds + b * 4096 + w * 1024), 16,
-                                               (DSML_MEASURE_KNOB(rb.dbg) & 4) ? kRbOob : off, 0, 0, 0);
+      if (WAVES == 4 || lane < 32)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (wg_lptr)(rb_lds + b * 4096 + w * (4096 / WAVES)), 16,
+                                                 (DSML_MEASURE_KNOB(rb.dbg) & 4) ? kRbOob : off, 0, 0, 0);
     };
 #pragma unroll
     for (int b = 0; b < 16; ++b)
@@ -932,22 +957,22 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.Wh), (short)0, bh, 0x00020000);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(a.Wl, (short)0, bl, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.Wb, (short)0, bw, 0x00020000);
-    const int er = tid >> 3, ec = 8 * (tid & 7);  // epilogue: rows er + 32 jj, columns ec .. +7
+    const int er = tid >> 3, ec = 8 * (tid & 7);  // epilogue: rows er + 8 WAVES jj, columns ec .. +7
     for (int lt = 0; lt < ntl; ++lt) {
       const int k0 = (kt0 + lt) * 64;
       const bool more = lt + 1 < ntl;
-      // W words of this tile: 4 hi + 4 lo loads, always issued (out of range -> 0)
-      wg_u4 whv[4], wlv[4];
+      // W words of this tile: JJ hi + JJ lo loads, always issued (out of range -> 0)
+      wg_u4 whv[JJ], wlv[JJ];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int nr = n0 + er + 32 * jj, kc = k0 + ec;
+      for (int jj = 0; jj < JJ; ++jj) {
+        const int nr = n0 + er + 8 * WAVES * jj, kc = k0 + ec;
         const bool ok = nr < a.N && kc < a.K && !(DSML_MEASURE_KNOB(rb.dbg) & 1);
         whv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? (int)((nr * a.ldwh + kc) * 2) : kRbOob, 0, 0);
         wlv[jj] = __builtin_amdgcn_raw_buffer_load_b128(rl, ok ? (int)((nr * a.ldwl + kc) * 2) : kRbOob, 0, 0);
       }
-      f32x4 acc[2][4];
+      f32x4 acc[XM][4];
 #pragma unroll
-      for (int xm = 0; xm < 2; ++xm)
+      for (int xm = 0; xm < XM; ++xm)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[xm][y] = {0.f, 0.f, 0.f, 0.f};
       // The ring, software-pipelined: block b + 1's X fragments are read while
@@ -983,8 +1008,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
                          "+v"(hi[buf][1][0]), "+v"(hi[buf][1][1]), "+v"(hi[buf][1][2]), "+v"(hi[buf][1][3])::"memory");
         };
         // blocks 0 and 1 (nothing of this loop issued yet)
-        if (lt > 0) rb_vm<(NBLK - 2) + 8 + 8>();
-        else rb_vm<(NBLK - 2) + 8>();
+        if (lt > 0) rb_vm<(NBLK - 2) + NW + NW>();
+        else rb_vm<(NBLK - 2) + NW>();
         rb_barrier();
         reads2(std::integral_constant<int, 0>{}, 0);
         lgkm2(0);
@@ -995,11 +1020,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
             // block 2j + 3 landed: refills so far 2j (this tile's slots 0 .. 2j - 1)
             constexpr int later = NBLK - 1 - (2 * j + 3);
             if (lt > 0) {
-              if (more) rb_vm<later + 8 + 8 + 2 * j>();
-              else rb_vm<later + 8 + 8>();
+              if (more) rb_vm<later + NW + NW + 2 * j>();
+              else rb_vm<later + NW + NW>();
             } else {
-              if (more) rb_vm<later + 8 + 2 * j>();
-              else rb_vm<later + 8>();
+              if (more) rb_vm<later + NW + 2 * j>();
+              else rb_vm<later + NW>();
             }
             rb_barrier();  // blocks 2j + 2, 2j + 3 landed everywhere; 2j, 2j + 1 read by all
             if (more) {
@@ -1014,7 +1039,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
             for (int y = 0; y < 4; ++y) {
               const wg_u4 fx = {lo[cur][sb][y].x, lo[cur][sb][y].y, hi[cur][sb][y].x, hi[cur][sb][y].y};
 #pragma unroll
-              for (int xm = 0; xm < 2; ++xm)
+              for (int xm = 0; xm < XM; ++xm)
                 acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                     __builtin_bit_cast(wg_bf16x8, zf[2 * j + sb][xm]), __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
                     0, 0, 0);
@@ -1040,8 +1065,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
                      : "+v"(lo[buf][0]), "+v"(lo[buf][1]), "+v"(lo[buf][2]), "+v"(lo[buf][3]), "+v"(hi[buf][0]),
                        "+v"(hi[buf][1]), "+v"(hi[buf][2]), "+v"(hi[buf][3])::"memory");
       };
-      if (lt > 0) rb_vm_block<NBLK, -1, true, false>();  // block 0 (nothing of this loop issued yet)
-      else rb_vm_block<NBLK, -1, false, false>();
+      if (lt > 0) rb_vm_block<NBLK, -1, true, false, NW>();  // block 0 (nothing of this loop issued yet)
+      else rb_vm_block<NBLK, -1, false, false, NW>();
       rb_barrier();
       reads(std::integral_constant<int, 0>{}, 0);
       lgkm(0);
@@ -1050,11 +1075,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         constexpr int cur = b & 1, nxt = cur ^ 1;
         if constexpr (b + 1 < NBLK) {
           if (lt > 0) {
-            if (more) rb_vm_block<NBLK, b, true, true>();
-            else rb_vm_block<NBLK, b, true, false>();
+            if (more) rb_vm_block<NBLK, b, true, true, NW>();
+            else rb_vm_block<NBLK, b, true, false, NW>();
           } else {
-            if (more) rb_vm_block<NBLK, b, false, true>();
-            else rb_vm_block<NBLK, b, false, false>();
+            if (more) rb_vm_block<NBLK, b, false, true, NW>();
+            else rb_vm_block<NBLK, b, false, false, NW>();
           }
           rb_barrier();  // block b + 1 landed everywhere; block b read by all
           if (more) xdma(lt + 1, b);
@@ -1064,7 +1089,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         for (int y = 0; y < 4; ++y) {
           const wg_u4 fx = {lo[cur][y].x, lo[cur][y].y, hi[cur][y].x, hi[cur][y].y};
 #pragma unroll
-          for (int xm = 0; xm < 2; ++xm)
+          for (int xm = 0; xm < XM; ++xm)
             acc[xm][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wg_bf16x8, zf[b][xm]),
                                                                 __builtin_bit_cast(wg_bf16x8, fx), acc[xm][y],
                                                                 0, 0, 0);
@@ -1077,13 +1102,13 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
       }
       // ---- epilogue: alpha * G -> LDS tile [128 n][64 k] -> split-master RMW ----
       {
-        const uint32_t tb = tileb + ((32 * w + 4 * g) * kRbPitch + i) * 4;
+        const uint32_t tb = tileb + ((RW * w + 4 * g) * kRbPitch + i) * 4;
         auto st = [&](auto kc) __attribute__((always_inline)) {  // k = 16 xm + 4 y + r
           constexpr int k = decltype(kc)::value;
           constexpr int xm = k >> 4, y = (k >> 2) & 3, rr = k & 3;
           rb_dsw32_o<((16 * xm + rr) * kRbPitch + 16 * y) * 4>(tb, acc[xm][y][rr] * a.alpha);
         };
-        rb_for<0, 32>(st);
+        rb_for<0, 16 * XM>(st);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rb_barrier();  // the tile is whole; every wave has read the last block(s)
@@ -1091,24 +1116,26 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
         if constexpr (kRbPair && NBLK >= 4) xdma(lt + 1, nblk - 2);
         xdma(lt + 1, nblk - 1);
       }
-      wg_u4 gv[4][2];
+      wg_u4 gv[JJ][2];
       {
         const uint32_t tr = tileb + (er * kRbPitch + ec) * 4;
-        gv[0][0] = rb_dsr128_o<0>(tr);
-        gv[0][1] = rb_dsr128_o<16>(tr);
-        gv[1][0] = rb_dsr128_o<32 * kRbPitch * 4>(tr);
-        gv[1][1] = rb_dsr128_o<32 * kRbPitch * 4 + 16>(tr);
-        gv[2][0] = rb_dsr128_o<64 * kRbPitch * 4>(tr);
-        gv[2][1] = rb_dsr128_o<64 * kRbPitch * 4 + 16>(tr);
-        gv[3][0] = rb_dsr128_o<96 * kRbPitch * 4>(tr);
-        gv[3][1] = rb_dsr128_o<96 * kRbPitch * 4 + 16>(tr);
+        auto rd = [&](auto jc) __attribute__((always_inline)) {
+          constexpr int jj = decltype(jc)::value;
+          gv[jj][0] = rb_dsr128_o<8 * WAVES * jj * kRbPitch * 4>(tr);
+          gv[jj][1] = rb_dsr128_o<8 * WAVES * jj * kRbPitch * 4 + 16>(tr);
+        };
+        rb_for<0, JJ>(rd);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(gv[0][0]), "+v"(gv[0][1]), "+v"(gv[1][0]), "+v"(gv[1][1]), "+v"(gv[2][0]),
-                     "+v"(gv[2][1]), "+v"(gv[3][0]), "+v"(gv[3][1])::"memory");
+      if constexpr (JJ == 4)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(gv[0][0]), "+v"(gv[0][1]), "+v"(gv[JJ - 3][0]), "+v"(gv[JJ - 3][1]), "+v"(gv[JJ - 2][0]),
+                       "+v"(gv[JJ - 2][1]), "+v"(gv[JJ - 1][0]), "+v"(gv[JJ - 1][1])::"memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(gv[0][0]), "+v"(gv[0][1]), "+v"(gv[JJ - 1][0]), "+v"(gv[JJ - 1][1])::"memory");
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int nr = n0 + er + 32 * jj, kc = k0 + ec;
+      for (int jj = 0; jj < JJ; ++jj) {
+        const int nr = n0 + er + 8 * WAVES * jj, kc = k0 + ec;
         const bool ok = nr < a.N && kc < a.K && !(DSML_MEASURE_KNOB(rb.dbg) & 1);
         float wv[8];
         hl_join8(make_uint4(whv[jj].x, whv[jj].y, whv[jj].z, whv[jj].w),
@@ -1125,7 +1152,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
           hw[e] = h0 | (h1 << 16);
           lw[e] = hl_lo(v0, h0) | (hl_lo(v1, h1) << 16);
         }
-        // always issued (the ring's counts assume 8 stores a tile): out of range -> dropped
+        // always issued (the ring's counts assume NW stores a tile): out of range -> dropped
         __builtin_amdgcn_raw_buffer_store_b128(wg_u4{hw[0], hw[1], hw[2], hw[3]}, rw,
                                                ok ? (int)((nr * a.ldwb + kc) * 2) : kRbOob, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(wg_u4{lw[0], lw[1], lw[2], lw[3]}, rl,
@@ -1134,6 +1161,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NBLK>
+__global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
+  wgrad_rowblk_body<NBLK, 4>(rb);
+}
+template <int NBLK>
+__global__ __launch_bounds__(512, 1) void wgrad_rowblk8_k(WgRowBlk rb) {
+  wgrad_rowblk_body<NBLK, 8>(rb);
 }
 
 bool wg_valid(const WgArgs& a) {
@@ -1172,6 +1208,8 @@ static bool rowblk_fits(const WgLayer& L) {
          (int64_t)L.N * L.ldwb * 2 + 16 <= kRbOob && (int64_t)L.N * L.ldwl * 2 + 16 <= kRbOob &&
          (int64_t)L.N * L.ldwh * 2 + 16 <= kRbOob;
 }
+constexpr int kRbWaves = 8;  // workgroup waves of the row-block form (HIPDSML_RB_WAVES: 4 / 8; profiles/r6_rowblk_8wave_ab.json)
+static int g_rb_waves = 0;
 static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t s) {
   WgRowBlk rb{};
   rb.n = n;
@@ -1189,8 +1227,10 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const void* fs[4] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>)};
+    const void* fs[8] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
+                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>),
+                         reinterpret_cast<const void*>(wgrad_rowblk8_k<2>), reinterpret_cast<const void*>(wgrad_rowblk8_k<4>),
+                         reinterpret_cast<const void*>(wgrad_rowblk8_k<8>), reinterpret_cast<const void*>(wgrad_rowblk8_k<16>)};
     for (const void* f : fs) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRbLds);
       if (e != hipSuccess) { cus = 0; return e; }
@@ -1203,6 +1243,19 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
 #else
   rb.dbg = 0;
 #endif
+  if (g_rb_waves == 0) {
+    const char* e = getenv("HIPDSML_RB_WAVES");
+    g_rb_waves = e != nullptr && *e ? atoi(e) : kRbWaves;
+  }
+  if (g_rb_waves == 8) {
+    switch (layers[0].M) {
+      case 64: hipLaunchKernelGGL(wgrad_rowblk8_k<2>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
+      case 128: hipLaunchKernelGGL(wgrad_rowblk8_k<4>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
+      case 256: hipLaunchKernelGGL(wgrad_rowblk8_k<8>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
+      default: hipLaunchKernelGGL(wgrad_rowblk8_k<16>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
+    }
+    return hipGetLastError();
+  }
   switch (layers[0].M) {
     case 64: hipLaunchKernelGGL(wgrad_rowblk_k<2>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
     case 128: hipLaunchKernelGGL(wgrad_rowblk_k<4>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
@@ -1211,6 +1264,8 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
   }
   return hipGetLastError();
 }
+
+void wgrad_rowblk_set_waves(int waves) { g_rb_waves = waves == 8 ? 8 : waves == 4 ? 4 : 0; }
 
 namespace {
 // ---------------------------------------------------------------------------
