@@ -645,6 +645,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("wide_input_set_stamping", &wide_input_set_stamping);
   m.def("wide_input_set_dbg", &wide_input_set_dbg);
+  m.def("wgrad_rowblk_stamps", []() {
+    std::vector<uint64_t> v(256 * 16);
+    hip_ok(wgrad_rowblk_read_stamps(v.data()), "wgrad_rowblk_read_stamps");
+    return v;
+  });
+  m.def("wgrad_rowblk_set_stamping", &wgrad_rowblk_set_stamping);
 #endif
 #ifdef HIPDSML_MEASURE
   m.attr("measure_build") = true;

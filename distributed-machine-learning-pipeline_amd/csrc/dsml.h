@@ -398,6 +398,8 @@ hipError_t wgrad_sgd_multi_in(const WgLayer* layers, int n, const WideInArgs& in
 hipError_t wide_input_read_stamps(uint64_t* host_out);  // [1024][8], measurement builds
 void wide_input_set_stamping(bool on);
 void wide_input_set_dbg(int bits);
+hipError_t wgrad_rowblk_read_stamps(uint64_t* host_out);  // [256][16], measurement builds
+void wgrad_rowblk_set_stamping(bool on);
 #endif
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);

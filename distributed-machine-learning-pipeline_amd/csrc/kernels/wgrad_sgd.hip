@@ -804,6 +804,22 @@ __device__ __forceinline__ void rb_frag_issue(uint32_t img, int c0, int lane, wg
 // waves a SIMD: the waits of one hide behind the other's issue).  Same
 // fragments, same MFMA chain per output, same epilogue arithmetic: the two
 // forms are bit-identical.
+#ifdef HIPDSML_MEASURE
+// measurement builds: per workgroup s_memrealtime at entry, the first
+// segment's Z^T in registers, the end of each of its first 12 k tiles, exit
+__device__ uint64_t g_rb_stamps[256][16];
+__device__ int g_rb_stamp_on;
+#define RB_STAMP(k)                                                                                    \
+  do {                                                                                                 \
+    if (g_rb_stamp_on && threadIdx.x == 0 && blockIdx.x < 256 && (k) < 16)                              \
+      g_rb_stamps[blockIdx.x][(k)] = __builtin_amdgcn_s_memrealtime();                                  \
+  } while (0)
+#else
+#define RB_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 template <int NBLK, int WAVES>
 __device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
@@ -823,6 +839,8 @@ __device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
   const int U = rb.ustart[rb.n];
   const int u0 = (int)((int64_t)blockIdx.x * U / rb.groups);
   const int u1 = (int)((int64_t)(blockIdx.x + 1) * U / rb.groups);
+  RB_STAMP(0);
+  int stile = 2;  // measurement builds: the next tile stamp
   for (int u = u0; u < u1;) {
     // ---- segment: units u .. of one n block of one layer ----
     int j = 0;
@@ -900,6 +918,7 @@ __device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
           }
         }
         rb_barrier();  // the chunks' slots are free again
+        if (ph == 1 || 8 * (ph + 1) >= nblk) RB_STAMP(stile == 2 ? 1 : 15);
       }
     }
 
@@ -1158,9 +1177,12 @@ __device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
         __builtin_amdgcn_raw_buffer_store_b128(wg_u4{lw[0], lw[1], lw[2], lw[3]}, rl,
                                                ok ? (int)((nr * a.ldwl + kc) * 2) : kRbOob, 0, 0);
       }
+      RB_STAMP(stile);
+      ++stile;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  RB_STAMP(14);
 }
 
 template <int NBLK>
@@ -1265,6 +1287,16 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
   return hipGetLastError();
 }
 
+#ifdef HIPDSML_MEASURE
+hipError_t wgrad_rowblk_read_stamps(uint64_t* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_rb_stamps), sizeof(uint64_t) * 256 * 16, 0, hipMemcpyDeviceToHost);
+}
+void wgrad_rowblk_set_stamping(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rb_stamp_on), &v, sizeof(int), 0, hipMemcpyHostToDevice);
+  (void)hipDeviceSynchronize();
+}
+#endif
 void wgrad_rowblk_set_waves(int waves) { g_rb_waves = waves == 8 ? 8 : waves == 4 ? 4 : 0; }
 
 namespace {
