@@ -699,8 +699,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (py::handle it : layers) v.push_back(wg_layer(it));
     hip_ok(wgrad_sgd_multi(v.data(), (int)v.size(), cur_stream(), tile), "wgrad_sgd_multi");
   }, py::arg("layers"), py::arg("tile") = 0);
-  m.def("wgrad_rowblk_set_waves", &wgrad_rowblk_set_waves, py::arg("waves"),
-        "row-block update workgroup: 4 or 8 waves (0: the default); the forms are bit-identical");
   // the fused input layer's operands (kernels/wide_input.hip, WideInArgs):
   // XG this step's rows in gradient-fragment order, contiguous [ceil(K/16)][2][16][32];
   // XF the next step's rows k-blocked, contiguous [ceil(K/32)][64][32]

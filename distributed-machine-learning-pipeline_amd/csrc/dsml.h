@@ -360,8 +360,6 @@ hipError_t hilo_sgd(const uint16_t* hic, int64_t ldc, uint16_t* lo, int64_t ldl,
 // master, one M of 64 / 128 / 256 / 512 for every layer; auto picks it from M >= 256)
 constexpr int kWgRowBlkTile = 256;
 hipError_t wgrad_sgd_multi(const WgLayer* layers, int n, hipStream_t s, int tile = 0);
-// row-block form's workgroup: 4 or 8 waves (0: the default / HIPDSML_RB_WAVES); bit-identical
-void wgrad_rowblk_set_waves(int waves);
 // The wide step's input layer in one launch (kernels/wide_input.hip): dZ_1 from
 // the last dgrad's raw split-K slices (+ ReLU' mask), the W_0 / b_0 SGD step on
 // the split master, and the NEXT step's H_1 = relu(X' W_0'^T + b_0').  M = 64.

@@ -15,6 +15,7 @@
 // every workgroup issues its W-tile loads FIRST, so that HBM round trip
 // overlaps the operand staging and the MFMAs instead of following them.
 // Reference hot loop replaced: the per-sample weight update of client.go:112-202.
+#include <algorithm>
 #include <type_traits>
 
 #include <cstdlib>
@@ -696,6 +697,7 @@ constexpr int kRbRing = 16 * 4096;             // one k tile of X: <= 16 blocks 
 constexpr int kRbPitch = 68;                   // floats per row of the fp32 epilogue tile [128][68]
 constexpr int kRbLds = kRbRing + kRbN * kRbPitch * 4;
 constexpr int kRbMaxM = 512;
+constexpr int kRbMaxGroups = 256;              // workgroups of a launch (one a CU)
 constexpr bool kRbAuto = true;                 // auto dispatch (tile 0) picks it at M >= 256
 #if defined(HIPDSML_MEASURE) && defined(HIPDSML_RB_PAIR)
 constexpr bool kRbPair = HIPDSML_RB_PAIR != 0;  // measurement builds: the single-block A/B
@@ -710,8 +712,9 @@ struct WgRowBlk {
   int ustart[kWgMaxLayers + 1];  // first unit of each layer (prefix sums); ustart[n] = all units
   int ktiles[kWgMaxLayers];
   int n;
-  int groups;  // workgroups: g owns units [g U / G, (g + 1) U / G)
+  int groups;  // workgroups: g owns units [gstart[g], gstart[g + 1])
   int dbg;     // measurement builds only (HIPDSML_RB_DBG): bit 0/1/2 drop the W / Z / X traffic
+  int gstart[kRbMaxGroups + 1];  // cost-balanced runs (wgrad_rowblk_launch)
 };
 
 // s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding:
@@ -801,9 +804,8 @@ __device__ __forceinline__ void rb_frag_issue(uint32_t img, int c0, int lane, wg
 
 // WAVES: 4 (wave w owns W rows 32 w .. +31 of the 128-row unit: two 16-row
 // MFMA A fragments, one wave a SIMD) or 8 (rows 16 w .. +15, one fragment, two
-// waves a SIMD: the waits of one hide behind the other's issue).  Same
-// fragments, same MFMA chain per output, same epilogue arithmetic: the two
-// forms are bit-identical.
+// waves a SIMD; bit-identical).  Only the 4-wave form is instantiated: with
+// cost-balanced runs the 8-wave one measured slower (profiles/r6_rowblk_balance.json).
 #ifdef HIPDSML_MEASURE
 // measurement builds: per workgroup s_memrealtime at entry, the first
 // segment's Z^T in registers, the end of each of its first 12 k tiles, exit
@@ -837,8 +839,8 @@ __device__ __forceinline__ void wgrad_rowblk_body(const WgRowBlk& rb) {
   uint32_t fa[4][2];  // the 8 transposing reads' lane addresses in ring block 0
   rb_frag_addrs(ring, lane, fa);
   const int U = rb.ustart[rb.n];
-  const int u0 = (int)((int64_t)blockIdx.x * U / rb.groups);
-  const int u1 = (int)((int64_t)(blockIdx.x + 1) * U / rb.groups);
+  const int u0 = rb.gstart[blockIdx.x], u1 = rb.gstart[blockIdx.x + 1];
+  (void)U;
   RB_STAMP(0);
   int stile = 2;  // measurement builds: the next tile stamp
   for (int u = u0; u < u1;) {
@@ -1189,10 +1191,6 @@ template <int NBLK>
 __global__ __launch_bounds__(256, 1) void wgrad_rowblk_k(WgRowBlk rb) {
   wgrad_rowblk_body<NBLK, 4>(rb);
 }
-template <int NBLK>
-__global__ __launch_bounds__(512, 1) void wgrad_rowblk8_k(WgRowBlk rb) {
-  wgrad_rowblk_body<NBLK, 8>(rb);
-}
 
 bool wg_valid(const WgArgs& a) {
   if (a.M < 1 || a.N < 1 || a.K < 8 || (a.K & 3) || (a.ldz & 7) || (a.ldx & 7) ||
@@ -1230,8 +1228,6 @@ static bool rowblk_fits(const WgLayer& L) {
          (int64_t)L.N * L.ldwb * 2 + 16 <= kRbOob && (int64_t)L.N * L.ldwl * 2 + 16 <= kRbOob &&
          (int64_t)L.N * L.ldwh * 2 + 16 <= kRbOob;
 }
-constexpr int kRbWaves = 8;  // workgroup waves of the row-block form (HIPDSML_RB_WAVES: 4 / 8; profiles/r6_rowblk_8wave_ab.json)
-static int g_rb_waves = 0;
 static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t s) {
   WgRowBlk rb{};
   rb.n = n;
@@ -1249,35 +1245,84 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const void* fs[8] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
-                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>),
-                         reinterpret_cast<const void*>(wgrad_rowblk8_k<2>), reinterpret_cast<const void*>(wgrad_rowblk8_k<4>),
-                         reinterpret_cast<const void*>(wgrad_rowblk8_k<8>), reinterpret_cast<const void*>(wgrad_rowblk8_k<16>)};
+    const void* fs[4] = {reinterpret_cast<const void*>(wgrad_rowblk_k<2>), reinterpret_cast<const void*>(wgrad_rowblk_k<4>),
+                         reinterpret_cast<const void*>(wgrad_rowblk_k<8>), reinterpret_cast<const void*>(wgrad_rowblk_k<16>)};
     for (const void* f : fs) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRbLds);
       if (e != hipSuccess) { cus = 0; return e; }
     }
   }
-  rb.groups = std::min(cus, u);
+  // Runs balanced by cost, not unit count: every segment a workgroup starts (a
+  // new n block) pays its Z^T load and a cold X ring first -- ~2.3 k tiles'
+  // worth at M = 512 (profiles/r6_rowblk_balance.json) -- so an equal split of
+  // units left the workgroups whose run crossed an n block ~10 us behind the
+  // median.  Greedy fill against a target, the target bisected to the
+  // smallest that fits the CUs.
+  const int G = std::min(std::min(cus, u), kRbMaxGroups);
+  // segment overhead in k tiles: the stamps price it at ~2.3 at M = 512, but a
+  // sweep of the model's constant put the launch's end earliest at 1.5
+  // (M = 512: 1.0 60.2 us, 1.5 48.7, 2.0 50.3, 2.3 50.5 -- profiles/r6_rowblk_balance.json)
+  const double ov = 1.5;
+  auto fill = [&](double T, int* starts) -> int {
+    int g = 0;
+    double cur = 0.0;
+    int prev_seg = -1;
+    if (starts) starts[0] = 0;
+    for (int j = 0, uu = 0; j < n; ++j) {
+      const int kts = rb.ktiles[j], nbs = (layers[j].N + kRbN - 1) / kRbN;
+      for (int nbk = 0; nbk < nbs; ++nbk) {
+        for (int kt = 0; kt < kts; ++kt, ++uu) {
+          const int seg = rb.ustart[j] + nbk * kts;  // the unit's segment id (first unit of its n block)
+          double c = 1.0 + ((cur == 0.0 || seg != prev_seg) ? ov : 0.0);
+          if (cur > 0.0 && cur + c > T) {  // close this workgroup's run
+            ++g;
+            if (starts) starts[g] = uu;
+            cur = 0.0;
+            c = 1.0 + ov;
+          }
+          cur += c;
+          prev_seg = seg;
+        }
+      }
+    }
+    ++g;
+    if (starts) starts[g] = u;
+    return g;
+  };
+  // the split depends only on the shapes: computed once per shape set (a host
+  // bisection per launch cost ~90 us of launch rate in an eager loop)
+  struct Plan {
+    int key[2 + 2 * kWgMaxLayers];
+    int groups;
+    int gstart[kRbMaxGroups + 1];
+  };
+  static Plan cache[8];
+  static int ncache = 0;
+  int key[2 + 2 * kWgMaxLayers] = {n, layers[0].M};
+  for (int j = 0; j < n; ++j) { key[2 + 2 * j] = layers[j].N; key[3 + 2 * j] = layers[j].K; }
+  const Plan* hit = nullptr;
+  for (int c = 0; c < ncache && !hit; ++c)
+    if (std::equal(key, key + 2 + 2 * kWgMaxLayers, cache[c].key)) hit = &cache[c];
+  if (hit == nullptr) {
+    double lo = 1.0, hi = (double)u * (1.0 + ov) + 1.0;
+    for (int it = 0; it < 40; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (fill(mid, nullptr) <= G) hi = mid;
+      else lo = mid;
+    }
+    Plan& pl = cache[ncache < 8 ? ncache++ : 7];
+    std::copy(key, key + 2 + 2 * kWgMaxLayers, pl.key);
+    pl.groups = fill(hi, pl.gstart);
+    hit = &pl;
+  }
+  rb.groups = hit->groups;
+  std::copy(hit->gstart, hit->gstart + hit->groups + 1, rb.gstart);
 #ifdef HIPDSML_MEASURE
   static const int rb_dbg = getenv("HIPDSML_RB_DBG") ? atoi(getenv("HIPDSML_RB_DBG")) : 0;
   rb.dbg = rb_dbg;
 #else
   rb.dbg = 0;
 #endif
-  if (g_rb_waves == 0) {
-    const char* e = getenv("HIPDSML_RB_WAVES");
-    g_rb_waves = e != nullptr && *e ? atoi(e) : kRbWaves;
-  }
-  if (g_rb_waves == 8) {
-    switch (layers[0].M) {
-      case 64: hipLaunchKernelGGL(wgrad_rowblk8_k<2>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
-      case 128: hipLaunchKernelGGL(wgrad_rowblk8_k<4>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
-      case 256: hipLaunchKernelGGL(wgrad_rowblk8_k<8>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
-      default: hipLaunchKernelGGL(wgrad_rowblk8_k<16>, dim3(rb.groups), dim3(512), kRbLds, s, rb); break;
-    }
-    return hipGetLastError();
-  }
   switch (layers[0].M) {
     case 64: hipLaunchKernelGGL(wgrad_rowblk_k<2>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
     case 128: hipLaunchKernelGGL(wgrad_rowblk_k<4>, dim3(rb.groups), dim3(256), kRbLds, s, rb); break;
@@ -1297,8 +1342,6 @@ void wgrad_rowblk_set_stamping(bool on) {
   (void)hipDeviceSynchronize();
 }
 #endif
-void wgrad_rowblk_set_waves(int waves) { g_rb_waves = waves == 8 ? 8 : waves == 4 ? 4 : 0; }
-
 namespace {
 // ---------------------------------------------------------------------------
 // The wide step's input layer as strips inside the update launch (one replica,
