@@ -123,7 +123,12 @@ template <int NL> __device__ __forceinline__ bool pk_sr_active(int b, int helper
 }
 // Replicas [pk_hlo(N, H, k), pk_hlo(N, H, k + 1)) of the global-batch dW1 go to
 // part k of a layer-1 tile (k = 0: the owner, k = h: helper h), rank order.
-__host__ __device__ constexpr int pk_hlo(int n, int helpers, int k) { return k * n / (1 + helpers); }
+// gsplit (gatherer tiles, gk < 4): the owner, which first contracts the Z1
+// correction on the chains' critical path, takes no replica; its helpers split
+// all N (part k = helper k: [(k - 1) N / H, k N / H)).
+__host__ __device__ constexpr int pk_hlo(int n, int helpers, int k, bool gsplit = false) {
+  return (gsplit && helpers > 0) ? (k == 0 ? 0 : (k - 1) * n / helpers) : k * n / (1 + helpers);
+}
 constexpr int kThreads = 256;
 static_assert(kKC % 16 == 0, "k slice must hold whole 16-wide k groups / k tiles");
 
@@ -427,6 +432,11 @@ static int g_pkx_helpers = -2;
 // profiles/r6_pkx_l1push_ab.json)
 constexpr int kPkxL1PushDefault = 1;
 static int g_pkx_l1push = -2;
+// pkx: the gatherer tiles' owners take no dW1 replica (their helpers take all):
+// lone-replica probe N = 8 11.57 -> 10.7 us, N = 4 9.96 -> 9.58, mirror mode
+// unchanged; every owner taking none was slower (profiles/r6_pkx_gather_split_ab.json)
+constexpr int kPkxGsplitDefault = 1;  // (HIPDSML_PKX_GSPLIT overrides)
+static int g_pkx_gsplit = -2;
 __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) {
   if (jit <= 0) return;
   uint32_t h = (uint32_t)blk * 2654435761u ^ (uint32_t)(it + 1) * 40503u ^ (uint32_t)salt * 0x9E3779B9u;
@@ -503,6 +513,7 @@ struct PersistArgs {
   int32_t pushers;  // Gram forms, tagged tile sums: the tiles' slots pushed by pusher blocks
   int32_t l1push;   // pkx: the replica's dZ1 rows go to the peers from the layer-1 owner blocks
                     // (block (gn, gk) sends column tile gn to peer rep + 1 + gk), not the chains
+  int32_t gsplit;   // pkx: the gatherer tiles' owners leave every dW1 replica to their helpers
 };
 
 // Receive-buffer layout per parity half: [src][slot][64 lanes][16 floats],
@@ -1444,7 +1455,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     // only -- all in flight during the waits, so the dW1 passes find them in
     // registers instead of waiting one load latency per replica
     float4 xP[3][2][4];
-    const int own_hi = XL ? pk_hlo(a.nrep, a.helpers, 1) : 0;
+    const int own_hi = XL ? pk_hlo(a.nrep, a.helpers, 1, a.gsplit && gat) : 0;
     if constexpr (XL) {
 #pragma unroll
       for (int j = 0; j < 3; ++j)
@@ -1754,7 +1765,8 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
   pk_started(a, blk, s0);
   float* Dh = lds;  // dZ1 tiles of replicas h0 .. h1 - 1: [h1 - h0][64][17]
   const int probe = g_pk_probe;
-  const int h0 = pk_hlo(a.nrep, a.helpers, h), h1 = pk_hlo(a.nrep, a.helpers, h + 1);
+  const bool gsp = a.gsplit && gk < kNCH;
+  const int h0 = pk_hlo(a.nrep, a.helpers, h, gsp), h1 = pk_hlo(a.nrep, a.helpers, h + 1, gsp);
   const int cnt = h1 - h0;
   const int kt0 = kKC / 16 * gk + w, kt1 = kKC / 16 * gk + (w < 3 ? w + 4 : w);
   auto xl_load = [&](float4 (&B)[2][4], int r, uint64_t s) __attribute__((always_inline)) {
@@ -3419,6 +3431,11 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
       g_pkx_l1push = e != nullptr && *e ? atoi(e) : -1;
     }
     a.l1push = algo == 4 ? (g_pkx_l1push >= 0 ? (g_pkx_l1push ? 1 : 0) : kPkxL1PushDefault) : 0;
+    if (g_pkx_gsplit == -2) {
+      const char* e = getenv("HIPDSML_PKX_GSPLIT");
+      g_pkx_gsplit = e != nullptr && *e ? atoi(e) : -1;
+    }
+    a.gsplit = (algo == 4 && a.helpers > 0) ? (g_pkx_gsplit >= 0 ? (g_pkx_gsplit ? 1 : 0) : kPkxGsplitDefault) : 0;
     // Gram form: the previous launch's last Z1 carries over as in the single
     // replica (every replica launches the same sequence, so all agree)
     if (algo < 2) a.carry = 0;
