@@ -206,8 +206,20 @@ struct L1GLay {
   static constexpr int G = B1 + 16;                   // data-parallel forms: the other replicas'
                                                       // dZ1 tiles [kMaxPeers - 1][64][17]
   static constexpr int RED = G + (kMaxPeers - 1) * kB * 17;  // correction partials [4 waves][64 lanes][4]
-  static constexpr int TOTAL = RED + 4 * 256;
+  static constexpr int FLG = RED + 4 * 256;                  // lds_and's per-wave words [4]
+  static constexpr int TOTAL = FLG + 4;
 };
+// Workgroup AND of `ok` that orders LDS only: unlike __syncthreads_and it does
+// not wait for the waves' outstanding global stores (the dZ1 rows a layer-1
+// block just pushed to a peer, acknowledged only after a round trip).  One
+// barrier; the words are rewritten only at the next call, behind the other
+// barriers of a step.
+__device__ __forceinline__ bool lds_and(bool ok, int* words) {
+  const bool bad = __builtin_amdgcn_ballot_w64(!ok) != 0;
+  if ((threadIdx.x & 63) == 0) words[threadIdx.x >> 6] = bad ? 1 : 0;
+  lds_barrier();
+  return (words[0] | words[1] | words[2] | words[3]) == 0;
+}
 static_assert(L1GLay::G % 4 == 0, "LDS-DMA image must be 16-B aligned");
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int NL>
@@ -219,9 +231,8 @@ static_assert(lds_floats<3>() * 4 <= 160 * 1024 && lds_floats<2>() * 4 <= 160 * 
 // ---- hand-off buffer layout (8-byte granules) --------------------------------
 // PART[2][56][4][16][16] partials [parity][slot][chain][n][row], plain fp32:
 //                   the layer-1 blocks' k-partials of Z1 (b1 added by gk == 0);
-//                   one flag per slot, parity and step (PF[2][64]).  The
-//                   data-parallel form uses parity 0 (read by the chains); the
-//                   single replica both parities (read by the gk == 0 blocks).
+//                   one flag per slot and step (PF[64]); the direct form (pk /
+//                   pk2, read by the chains).  The Gram forms' partials are PG.
 // SF[64]            started flags (tag = first step + 1): the step counter is
 //                   handed on only once every block has read it
 // DZ1[64][128]      activation gradient of layer 1, tagged granules
@@ -275,6 +286,12 @@ __device__ __forceinline__ int64_t pk_hf(uint64_t s, int h, int lb) {
 // step tag} granules (no drain, no flag: the pusher polls the data itself).
 constexpr int64_t kOffXs = kTotalG;
 constexpr int64_t kTotalX = kOffXs + 2 * 16 * 3 * 64 * 4;
+// PG[2][56][4][16][16] Gram forms: the layer-1 blocks' k-partials of Z1 as
+// tagged granules [parity][slot][chain][n][row] (tag = step + 1), polled by the
+// gatherer directly -- no store drain and flag by the producer, no flag round
+// before the data by the gatherer (PART / PF above stay the direct form's)
+constexpr int64_t kOffPg = kTotalX;
+constexpr int64_t kTotalP = kOffPg + 2 * kNPart * kNCH * 256;
 __device__ __forceinline__ int64_t pk_xs_g(uint64_t s, int g, int k, int lane) {  // granules
   return kOffXs + ((((int64_t)(s & 1) * 16 + g) * 3 + k) * 64 + lane) * 4;
 }
@@ -455,8 +472,8 @@ __device__ __forceinline__ void pk_jit(int jit, int blk, uint64_t it, int salt) 
 // default window is steps 8-15)
 #define PK_STAMP(role, ph)                                                            \
   do {                                                                                \
-    if (stamp_on && threadIdx.x == 0 && it >= g_pk_stamp_on - 1 && it < g_pk_stamp_on + 7) \
-      g_pk_stamps[(role)][it - (g_pk_stamp_on - 1)][(ph)] = __builtin_amdgcn_s_memrealtime(); \
+    if (stamp_on && threadIdx.x == 0 && it >= stamp_on - 1 && it < stamp_on + 7)          \
+      g_pk_stamps[(role)][it - (stamp_on - 1)][(ph)] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
 
 struct PersistArgs {
@@ -1090,7 +1107,7 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
   if (lb == 0) PK_EDGE(1);
 
   bool ok = true;
-  const int stamp_on = g_pk_stamp_on && lb == 0;
+  const int stamp_on = lb == 0 ? g_pk_stamp_on : 0;
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(0, 0);
     const uint64_t s = s0 + (uint64_t)it;
@@ -1250,10 +1267,16 @@ __device__ __forceinline__ void pk_layer1(const PersistArgs& a, float* lds, int 
 // Replicas of a data-parallel job keep the direct form (their W1 update sums
 // every replica's dZ1^T X).
 
-__device__ __forceinline__ int64_t pk_part_off(int par, int slot, int c) {  // floats
-  return kOffPart * 2 + (((int64_t)par * kNPart + slot) * kNCH + c) * 256;
+__device__ __forceinline__ int64_t pk_pg(int par, int slot, int c) {  // granules
+  return kOffPg + (((int64_t)par * kNPart + slot) * kNCH + c) * 256;
 }
-__device__ __forceinline__ int64_t pk_pf(int par, int slot) { return kOffPf + par * 64 + slot; }
+// One lane's 4 partial values as 4 tagged granules (two 16-B stores, no drain)
+__device__ __forceinline__ void st_part_g(__amdgpu_buffer_rsrc_t r, int64_t g, f4v z, uint32_t tag) {
+  __builtin_amdgcn_raw_buffer_store_b128(nu4v{__float_as_uint(z[0]), tag, __float_as_uint(z[1]), tag}, r,
+                                         (int)(g * 8), 0, kSc1);
+  __builtin_amdgcn_raw_buffer_store_b128(nu4v{__float_as_uint(z[2]), tag, __float_as_uint(z[3]), tag}, r,
+                                         (int)(g * 8 + 16), 0, kSc1);
+}
 
 // Gram-form X tile image: row r's 16-B chunks are XOR-swizzled within each
 // 16-float group by ((r >> 1) & 3): the forward's ds_read_b128 of 16 rows at one
@@ -1304,15 +1327,31 @@ __device__ __forceinline__ f4v pk_l1_fwd(const float* Xl, const float* Wl, const
 // flags are polled by lanes 0-6 and agreed by a ballot); false: a wait gave up.
 __device__ __forceinline__ bool pk_l1_gather_rows(__amdgpu_buffer_rsrc_t rb, f4v& z, int par, int gn, int c,
                                                   uint32_t tag, Poll& poll, int lane, int i, int q) {
-  bool ok = true;
-  if (lane < kGK && lane != c) ok = wait_flag(rb, pk_pf(par, gn + kGN * lane), tag, poll);
-  ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
-  asm volatile("" ::: "memory");
-  if (!ok) return false;
+  // the 6 others' granules polled together (PG: one round of loads per
+  // attempt, each lane re-reading only the partials still behind)
   f4v v[kGK];
+  uint32_t need = ((1u << kGK) - 1u) & ~(1u << c);
+  poll.start();
+  while (need != 0u) {
+    nu4v u0[kGK], u1[kGK];
 #pragma unroll
-  for (int g2 = 0; g2 < kGK; ++g2)
-    if (g2 != c) v[g2] = ld_f4(rb, pk_part_off(par, gn + kGN * g2, c) + i * 16 + 4 * q);
+    for (int g2 = 0; g2 < kGK; ++g2) {
+      if (need & (1u << g2)) {
+        const int off = (int)((pk_pg(par, gn + kGN * g2, c) + i * 16 + 4 * q) * 8);
+        u0[g2] = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, kSc1);
+        u1[g2] = __builtin_amdgcn_raw_buffer_load_b128(rb, off + 16, 0, kSc1);
+      }
+    }
+#pragma unroll
+    for (int g2 = 0; g2 < kGK; ++g2) {
+      if ((need & (1u << g2)) && u0[g2].y == tag && u0[g2].w == tag && u1[g2].y == tag && u1[g2].w == tag) {
+        v[g2] = f4v{__uint_as_float(u0[g2].x), __uint_as_float(u0[g2].z), __uint_as_float(u1[g2].x),
+                    __uint_as_float(u1[g2].z)};
+        need &= ~(1u << g2);
+      }
+    }
+    if (need != 0u && !poll.again()) return false;
+  }
   f4v sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int g2 = 0; g2 < kGK; ++g2) sum += g2 == c ? z : v[g2];
@@ -1396,15 +1435,13 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   const bool gat = gk < kNCH;
   const int c = gk;
   float* Red = lds + L1GLay::RED;
+  int* Flg = reinterpret_cast<int*>(lds + L1GLay::FLG);
   if (!a.carry) {
     // no state from a previous launch: step s0's Z1 directly, correction 0
     const uint32_t t0 = (uint32_t)(s0 + 1);
     const int par0 = (int)(s0 & 1);
     f4v z = pk_l1_fwd(xbuf(s0), Wl, B1, w, i, q);
-    st_f4(rb, pk_part_off(par0, lb, w) + i * 16 + 4 * q, z);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) st_gran(rb, pk_pf(par0, lb), __uint_as_float(t0), t0);
+    st_part_g(rb, pk_pg(par0, lb, w) + i * 16 + 4 * q, z, t0);
     if (gat && w == c) {
       if (!pk_l1_gather_rows(rb, z, par0, gn, c, t0, poll, lane, i, q)) {
         pk_report(a, false);
@@ -1416,7 +1453,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
   }
 
   bool ok = true;
-  const int stamp_on = g_pk_stamp_on && lb == 0;
+  const int stamp_on = lb == 0 ? g_pk_stamp_on : 0;
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(0, 0);
     const uint64_t s = s0 + (uint64_t)it;
@@ -1429,10 +1466,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     // publishes its k-partial; wave c of a gatherer keeps its own and sums the
     // six others of chain c's rows ----
     f4v zs = pk_l1_fwd(xbuf(s + 1), Wl, B1, w, i, q);
-    st_f4(rb, pk_part_off(parn, lb, w) + i * 16 + 4 * q, zs);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) st_gran(rb, pk_pf(parn, lb), __uint_as_float(tagn), tagn);
+    st_part_g(rb, pk_pg(parn, lb, w) + i * 16 + 4 * q, zs, tagn);
     // X(s+2) into the third buffer (its last reader, step s-1's backward,
     // finished before the barrier that ended that step)
     pk_glds_x_to(a, xbuf(s + 2), s + 2, lane, w, k0);
@@ -1497,6 +1531,14 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     }
     ok = __syncthreads_and(ok ? 1 : 0) != 0;  // also retires the X LDS-DMA
     if (!ok) break;
+    // the Gram fragments are in (the barrier waited for every load): said to
+    // the compiler, which otherwise cannot prove it across the poll loop below
+    // and waits vmcnt(0) -- the pushed rows' acknowledgement -- inside the
+    // correction's MFMA chain
+    // (unconditional: a path around it would merge the loads back in)
+#pragma unroll
+    for (int r2 = 0; r2 < (XM ? kMaxPeers : 1); ++r2)
+      asm volatile("" : "+v"(gv[r2][0]), "+v"(gv[r2][1]), "+v"(gv[r2][2]), "+v"(gv[r2][3]));
     if (lb == 0 && it + 1 == a.steps && tid == 0) {
       const uint64_t e = s0 + (uint64_t)a.steps;
       __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ctr), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1535,42 +1577,55 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       bool pok = true, peer_rows = false;
       poll.start();
       while (need != 0u) {
-        nu4v v0[kMaxPeers], v1[kMaxPeers];
+        nu4v v0[kMaxPeers], v1[kMaxPeers], o0, o1;
+        const bool own = (need >> a.rep) & 1u;
+        if (own) {
+          o0 = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(gl * 8), 0, kSc1);
+          o1 = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)((gl + 2) * 8), 0, kSc1);
+        }
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
-          if (need & (1u << r2)) {
-            if (r2 == a.rep) {
-              v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(gl * 8), 0, kSc1);
-              v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)((gl + 2) * 8), 0, kSc1);
-            } else {
-              const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
-              v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
-              v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
-            }
+          if ((need & (1u << r2)) && r2 != a.rep) {
+            const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
+            v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
+            v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
           }
         }
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
-          if ((need & (1u << r2)) && ((probe && r2 != a.rep) ||
-                                      (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
-            float* d = r2 == a.rep ? Dz + m * 17 + 4 * qq : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
+          if ((need & (1u << r2)) && r2 != a.rep &&
+              (probe || (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
+            float* d = DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17) + m * 17 + 4 * qq;
             d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
             d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
-            if (XL && r2 == a.rep && push_d >= 0) {
-              hop_stamp(a, s, 4 * w + (gn & 3));  // measurement builds only
-              const __amdgpu_buffer_rsrc_t rp = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, push_d)
-                                                              : a.xt.buf[push_d] + pk_dzr_base(a, s, a.rep));
-              __builtin_amdgcn_raw_buffer_store_b128(v0[r2], rp, off, 0, kScSys);
-              __builtin_amdgcn_raw_buffer_store_b128(v1[r2], rp, off + 16, 0, kScSys);
-            }
             need &= ~(1u << r2);
-            peer_rows = peer_rows || r2 != a.rep;
+            peer_rows = true;
           }
+        }
+        if (own && o0.y == tag && o0.w == tag && o1.y == tag && o1.w == tag) {
+          float* d = Dz + m * 17 + 4 * qq;
+          d[0] = __uint_as_float(o0.x); d[1] = __uint_as_float(o0.z);
+          d[2] = __uint_as_float(o1.x); d[3] = __uint_as_float(o1.z);
+          if (XL && push_d >= 0) {
+            hop_stamp(a, s, 4 * w + (gn & 3));  // measurement builds only
+            const __amdgpu_buffer_rsrc_t rp = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, push_d)
+                                                            : a.xt.buf[push_d] + pk_dzr_base(a, s, a.rep));
+            __builtin_amdgcn_raw_buffer_store_b128(o0, rp, off, 0, kScSys);
+            __builtin_amdgcn_raw_buffer_store_b128(o1, rp, off + 16, 0, kScSys);
+          }
+          need &= ~(1u << a.rep);
         }
         if (need != 0u && !poll.again()) { pok = false; break; }
       }
+      // every load of the poll is in: at most this thread's two push stores
+      // are still in flight -- said explicitly, so that the compiler's own
+      // waits below (the Gram fragments, loaded before the poll) are not a
+      // vmcnt(0) that would wait for the pushes' acknowledgement
+      __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (15 << 8));
       if (pok && peer_rows) hop_wait(a, s, 4 * (m >> 4) + (gn & 3));  // measurement builds only
-      ok = __syncthreads_and(pok ? 1 : 0) != 0;
+      // (the pushed rows' acknowledgement is not waited for here: the peers
+      // poll the granules' tags, and the chains' Z1 does not depend on it)
+      ok = lds_and(pok, Flg);
       if (!ok) break;
       PK_STAMP(0, 6);  // every replica's dZ1 rows of the tile in LDS
     }
@@ -1579,16 +1634,29 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
     // wave c adds the four partials in a fixed order and publishes Z1 ----
     if (gat) {
       f32x4 cw = {0.f, 0.f, 0.f, 0.f};
+      // every replica's B operands read up front, then one uninterrupted MFMA
+      // chain (same order): read per replica, the chain paid an LDS round trip
+      // every two MFMAs (1.1 us at N = 8)
+      float dzv[XM ? kMaxPeers : 1][4];
 #pragma unroll
       for (int r2 = 0; r2 < (XM ? kMaxPeers : 1); ++r2) {
         if (r2 < (XM ? a.nrep : 1)) {
           const float* Dr = (!XM || r2 == a.rep) ? Dz : DzX + (r2 < a.rep ? r2 : r2 - 1) * (kB * 17);
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) cw = mfma_f32_16x16x4(gv[r2][kk], Dr[(16 * w + 4 * kk + q) * 17 + i], cw);
+          for (int kk = 0; kk < 4; ++kk) dzv[r2][kk] = Dr[(16 * w + 4 * kk + q) * 17 + i];
+        }
+      }
+#pragma unroll
+      for (int r2 = 0; r2 < (XM ? kMaxPeers : 1); ++r2) {
+        if (r2 < (XM ? a.nrep : 1)) {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) cw = mfma_f32_16x16x4(gv[r2][kk], dzv[r2][kk], cw);
         }
       }
       *reinterpret_cast<f4v*>(Red + w * 256 + lane * 4) = f4v{cw[0], cw[1], cw[2], cw[3]};
-      __syncthreads();
+      PK_STAMP(0, 5);  // wave 0's contraction done
+      lds_barrier();   // (LDS only: the pushes above stay in flight)
+      PK_STAMP(0, 7);  // every wave's
       if (w == c) {
         const f4v c0 = *reinterpret_cast<const f4v*>(Red + lane * 4);
         const f4v c1 = *reinterpret_cast<const f4v*>(Red + 256 + lane * 4);
@@ -2170,7 +2238,7 @@ __device__ __forceinline__ void pk_chain(const PersistArgs& a, float* lds, int c
   if (c == 0) PK_EDGE(4);
   if (c == 0 && g_pk_stamp_on && tid == 0) g_pk_stamps[3][1][0] = local ? 1u : 0u;
 
-  const int stamp_on = g_pk_stamp_on && c == 0;
+  const int stamp_on = c == 0 ? g_pk_stamp_on : 0;
   const int jit = DP ? 0 : g_pk_jitter;
   // thread -> (column tile gn, column n, 8 rows) of this chain's H1 block
   const int pgn = tid >> 5, pn = (tid >> 1) & 15, phalf = tid & 1;
@@ -2565,7 +2633,7 @@ __device__ __forceinline__ void pk_grad(const PersistArgs& a, float* lds, int g,
   __syncthreads();
   bool ok = true;
   const bool local = pk_upper_local(a, s0, poll, ok);
-  const int stamp_on = g_pk_stamp_on && g == 0;
+  const int stamp_on = g == 0 ? g_pk_stamp_on : 0;
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(2, 0);
     const uint64_t s = s0 + (uint64_t)it;
@@ -2896,7 +2964,7 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
   // group's XCD (3 helpers: pushers on XCD 0), else they are written through
   const int hl = XM && a.pushers && pk_push_xcd0(a.helpers) ? kPushers<NL>() : 0;
   const bool xs_local = hl ? pk_upper_local(a, s0, poll, ok, kNCH + GTile<NL>::kN + hl) : false;
-  const int stamp_on = g_pk_stamp_on && g == 0;
+  const int stamp_on = g == 0 ? g_pk_stamp_on : 0;
   const int jit = g_pk_jitter;
   for (int it = 0; it < a.steps && ok; ++it) {
     PK_STAMP(2, 0);
@@ -3014,7 +3082,7 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
             }
           }
           PK_STAMP(2, 5);
-          const int dbg = stamp_on && it >= g_pk_stamp_on - 1 ? it - (g_pk_stamp_on - 1) : -1;
+          const int dbg = stamp_on && it >= stamp_on - 1 ? it - (stamp_on - 1) : -1;
           if (w < nslot) {
             float4 v[1] = {make_float4(gw[0], gw[1], gw[2], gw[3])};
             xok = px_tagged_gather<1>(a, s, v, kNL1 * 4 + 4 * g + w, w == 0 ? dbg : -1);
@@ -3305,7 +3373,7 @@ bool mlp_persist_supported(const MlpDesc& d) {
   return false;
 }
 
-int64_t mlp_persist_xbuf_granules() { return kTotalX; }
+int64_t mlp_persist_xbuf_granules() { return kTotalP; }
 
 template <int NL, int MODE>
 static hipError_t pk_launch(const PersistArgs& a, hipStream_t s) {

@@ -60,7 +60,12 @@ def decode(v, spec) -> dict:
             out["gram"]["l1_correction_publish_us"] = med([(st[0][s][4] - st[0][s][6]) / 100.0 for s in range(8)])
             out["gram"]["chain_dz1_publish_to_l1_rows_us"] = med(
                 [(st[0][s][6] - st[1][s][4]) / 100.0 for s in range(8)])
-        if all(st[0][s][5] for s in range(8)):
+            if all(st[0][s][5] and st[0][s][7] for s in range(8)):
+                # the correction split: wave 0's MFMAs -> every wave's (barrier) -> Z1 stored
+                out["gram"]["l1_corr_mfma_us"] = med([(st[0][s][5] - st[0][s][6]) / 100.0 for s in range(8)])
+                out["gram"]["l1_corr_barrier_us"] = med([(st[0][s][7] - st[0][s][5]) / 100.0 for s in range(8)])
+                out["gram"]["l1_corr_store_us"] = med([(st[0][s][4] - st[0][s][7]) / 100.0 for s in range(8)])
+        elif all(st[0][s][5] for s in range(8)):
             # single replica: the correction block of column 0 (chains' XCD)
             out["gram"]["chain_dz1_publish_to_cb_seen_us"] = med(
                 [(st[0][s][5] - st[1][s][4]) / 100.0 for s in range(8)])
