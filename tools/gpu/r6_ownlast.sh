@@ -1,4 +1,4 @@
-# pkx merged dZ1 poll: this replica's own rows loaded first (0) or after the
+# (knob HIPDSML_PK_OWNLAST since removed: no difference) pkx merged dZ1 poll: this replica's own rows loaded first (0) or after the
 # peers' (1) in each poll round; lone-replica probe at N = 2/4/8 alternating,
 # plus one stamped run each (correction split stamps)
 set -e
