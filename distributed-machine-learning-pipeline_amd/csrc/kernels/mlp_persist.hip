@@ -1557,7 +1557,10 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       const int m = tid >> 2, qq = tid & 3;
       const int off = (m * kD1 + n0 + 4 * qq) * 8;
       const int64_t gl = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
-      const float* rbase = a.xt.buf[a.rep];
+      // this step's DZR slots and the push target, computed once (inside the
+      // rounds the compiler reloaded the pointers from the kernel arguments
+      // and waited for them per replica, the poll's memory clobbers aside)
+      const float* rstep = a.xt.buf[a.rep] + pk_dzr_base(a, s, 0);
       // pkx l1push: this block sends the replica's own rows of column tile gn
       // to ONE peer as soon as they are here -- the 7 gk blocks of a tile
       // cover up to 7 peers, so a replica's 64 KB a peer leave from 56 CUs
@@ -1566,6 +1569,9 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
       if constexpr (XL) {
         if (a.l1push && gk < a.nrep - 1) push_d = __builtin_amdgcn_readfirstlane((a.rep + 1 + gk) % a.nrep);
       }
+      __amdgpu_buffer_rsrc_t rp = rb;
+      if (XL && push_d >= 0)
+        rp = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, push_d) : a.xt.buf[push_d] + pk_dzr_base(a, s, a.rep));
       uint32_t need = 1u << a.rep;  // replicas whose rows this thread still waits for
       // gatherers: every replica (the correction); other pkx owners: only the
       // replicas of their own dW1 part (the helpers read theirs) -- the exchange
@@ -1586,7 +1592,7 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
 #pragma unroll
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
           if ((need & (1u << r2)) && r2 != a.rep) {
-            const __amdgpu_buffer_rsrc_t rr = rsrc(rbase + pk_dzr_base(a, s, r2));
+            const __amdgpu_buffer_rsrc_t rr = rsrc(rstep + r2 * kDzrFloats);
             v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
             v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
           }
@@ -1608,8 +1614,6 @@ __device__ __forceinline__ void pk_layer1_gram(const PersistArgs& a, float* lds,
           d[2] = __uint_as_float(o1.x); d[3] = __uint_as_float(o1.z);
           if (XL && push_d >= 0) {
             hop_stamp(a, s, 4 * w + (gn & 3));  // measurement builds only
-            const __amdgpu_buffer_rsrc_t rp = rsrc(a.mirror ? a.xt.buf[a.rep] + pk_dzr_base(a, s, push_d)
-                                                            : a.xt.buf[push_d] + pk_dzr_base(a, s, a.rep));
             __builtin_amdgcn_raw_buffer_store_b128(o0, rp, off, 0, kScSys);
             __builtin_amdgcn_raw_buffer_store_b128(o1, rp, off + 16, 0, kScSys);
           }
@@ -1854,27 +1858,20 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       if (j < cnt) xl_load(xP[j], h0 + j, s);  // data only: in flight during the waits
-    if (probe) {
-      // lone-replica probe: the peers' rows are taken as arrived, so pace this
-      // block on the own replica's dZ1 (the owner's wait) instead of running ahead
-      const int m = tid >> 2, qq = tid & 3;
-      const int64_t gg = kOffDz1 + (int64_t)(s & 1) * (kB * kD1) + (int64_t)m * kD1 + n0 + 4 * qq;
-      poll.start();
-      for (;;) {
-        const uint4 u0 = ld_gran2(rb, gg), u1 = ld_gran2(rb, gg + 2);
-        if (u0.y == tag && u0.w == tag && u1.y == tag && u1.w == tag) break;
-        if (!poll.again()) { ok = false; break; }
-      }
-    }
     {
       // this part's dZ1 tiles: own rows from the local DZ1 region, the peers'
-      // from their DZR slots, every load of a round in flight together
+      // from their DZR slots, every load of a round in flight together.
+      // Lone-replica probe: the peers' rows are taken as arrived, so the own
+      // rows are polled in the same rounds (by their tags, whether or not
+      // they are in this part) to pace the block on this replica's dZ1, as
+      // the peers' tags pace it in a real run, instead of running ahead
       const int m = tid >> 2, qq = tid & 3;
-      uint32_t need = 0;
+      uint32_t need = probe ? 1u << a.rep : 0u;
 #pragma unroll
       for (int r2 = 0; r2 < kMaxPeers; ++r2)
         if (r2 >= h0 && r2 < h1) need |= 1u << r2;
       const bool peer_rows = h1 - h0 > 1 || h0 != a.rep;
+      const float* rstep = a.xt.buf[a.rep] + pk_dzr_base(a, s, 0);  // once, not per replica and round
       poll.start();
       while (need != 0u) {
         nu4v v0[kMaxPeers], v1[kMaxPeers];
@@ -1887,7 +1884,7 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
               v0[r2] = nu4v{u0.x, u0.y, u0.z, u0.w};
               v1[r2] = nu4v{u1.x, u1.y, u1.z, u1.w};
             } else {
-              const __amdgpu_buffer_rsrc_t rr = rsrc(a.xt.buf[a.rep] + pk_dzr_base(a, s, r2));
+              const __amdgpu_buffer_rsrc_t rr = rsrc(rstep + r2 * kDzrFloats);
               const int off = (m * kD1 + n0 + 4 * qq) * 8;
               v0[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kScSys);
               v1[r2] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, kScSys);
@@ -1898,9 +1895,11 @@ __device__ __forceinline__ void pk_l1_helper(const PersistArgs& a, float* lds, i
         for (int r2 = 0; r2 < kMaxPeers; ++r2) {
           if ((need & (1u << r2)) && ((probe && r2 != a.rep) ||
                                       (v0[r2].y == tag && v0[r2].w == tag && v1[r2].y == tag && v1[r2].w == tag))) {
-            float* d = Dh + (r2 - h0) * (kB * 17) + m * 17 + 4 * qq;
-            d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
-            d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
+            if (r2 >= h0 && r2 < h1) {
+              float* d = Dh + (r2 - h0) * (kB * 17) + m * 17 + 4 * qq;
+              d[0] = __uint_as_float(v0[r2].x); d[1] = __uint_as_float(v0[r2].z);
+              d[2] = __uint_as_float(v1[r2].x); d[3] = __uint_as_float(v1[r2].z);
+            }
             need &= ~(1u << r2);
           }
         }
