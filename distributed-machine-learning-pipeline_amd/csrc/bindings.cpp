@@ -862,6 +862,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_persist_set_pkx_l1push", [](int v) { mlp_persist_set_pkx_l1push(v); }, py::arg("mode"),
         "pkx dZ1 row pushes to the peers: 1 from the layer-1 owner blocks, 0 from the chains, -1 default");
 #ifdef HIPDSML_MEASURE
+  m.def("mlp_persist_push_stamps", []() {
+    std::vector<uint64_t> v(8 * 4);
+    hip_ok(mlp_persist_read_push_stamps(v.data()), "mlp_persist_read_push_stamps");
+    return v;
+  });
   m.def("mlp_persist_set_hop", [](double us) { mlp_persist_set_hop((int)(us * 100.0 + 0.5)); }, py::arg("us"),
         "measurement builds: every cross-replica hop of the mirror mode becomes usable `us` after "
         "its publication (0 off)");

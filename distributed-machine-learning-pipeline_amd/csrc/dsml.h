@@ -112,6 +112,7 @@ hipError_t mlp_persist_steps(const float* X, int64_t ldx, const int32_t* labels,
                              const float* xsw = nullptr, int64_t xsw_stride = 0);
 void mlp_persist_set_probe(int mode);  // testing only: 0 off, 1 lone-replica probe, 2 mirror
 #ifdef HIPDSML_MEASURE
+hipError_t mlp_persist_read_push_stamps(uint64_t* out);  // measurement builds: [8][4]
 void mlp_persist_set_hop(int ticks);  // measurement builds: extra hop latency in mirror mode (100 MHz ticks)
 #endif
 // pkx dW1 helper blocks per layer-1 block: -1 the default (3 from 4 replicas on,

@@ -3240,9 +3240,24 @@ __device__ __forceinline__ void pk_gtile(const PersistArgs& a, float* lds, int g
 // 0, 1 tile p, waves 2, 3 tile p + kPushers, each wave half the peers -- so the
 // tiles' gathers never queue behind their own pushes.  Same XCD as the tiles
 // (blockIdx 8 k): the staged slots stay in that L2.
+#ifdef HIPDSML_MEASURE
+// measurement builds (tools/pk_probe.py --push-stamps): pusher 0 wave 0 per stamped
+// step: poll entry, tile 0's staged slots seen, pushes issued, pushes acknowledged
+__device__ uint64_t g_pk_push_st[8][4];
+#define PUSH_STAMP(k)                                                                          \
+  do {                                                                                         \
+    if (p == 0 && tid == 0 && stamp_on && it >= stamp_on - 1 && it < stamp_on + 7)             \
+      g_pk_push_st[it - (stamp_on - 1)][(k)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#else
+#define PUSH_STAMP(k) do {} while (0)
+#endif
 template <int NL>
 __device__ __forceinline__ void pk_pusher(const PersistArgs& a, int p, int blk) {
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+#ifdef HIPDSML_MEASURE
+  const int stamp_on = g_pk_stamp_on;
+#endif
   const __amdgpu_buffer_rsrc_t rb = rsrc(a.xb);
   Poll poll{a.err, a.timeout_ticks, 0, 0};
   const uint64_t s0 = ld_ctr64(a.ctr + 1);
@@ -3256,6 +3271,7 @@ __device__ __forceinline__ void pk_pusher(const PersistArgs& a, int p, int blk) 
     const int par = (int)(s & 1);
     // the tile's staged slots, polled by their tags (every load of a round in flight)
     uint4 u[3][2];
+    PUSH_STAMP(0);
     poll.start();
     for (;;) {
       bool all = true;
@@ -3278,7 +3294,15 @@ __device__ __forceinline__ void pk_pusher(const PersistArgs& a, int p, int blk) 
       v[k] = k < nslot ? make_float4(__uint_as_float(u[k][0].x), __uint_as_float(u[k][0].z),
                                      __uint_as_float(u[k][1].x), __uint_as_float(u[k][1].z))
                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    PUSH_STAMP(1);
     px_tagged_push_part(a, s, v, nslot, kNL1 * 4 + 4 * g, w & 1, 2);
+    PUSH_STAMP(2);
+#ifdef HIPDSML_MEASURE
+    if (p == 0 && stamp_on) {
+      __builtin_amdgcn_s_waitcnt(0);  // measurement only: when the pushes landed
+      PUSH_STAMP(3);
+    }
+#endif
   }
   pk_report(a, ok);
 }
@@ -3340,6 +3364,9 @@ void mlp_persist_set_jitter(int ticks) {
   (void)hipDeviceSynchronize();
 }
 #ifdef HIPDSML_MEASURE
+hipError_t mlp_persist_read_push_stamps(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pk_push_st), sizeof(g_pk_push_st), 0, hipMemcpyDeviceToHost);
+}
 void mlp_persist_set_hop(int ticks) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pk_hop), &ticks, sizeof(int), 0, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();

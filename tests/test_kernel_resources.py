@@ -35,7 +35,7 @@ def test_persistent_kernels_touch_no_scratch(tmp_path):
         assert calls == 0 and spills == 0, f"{name}: {calls} calls, {spills} scratch accesses"
 
 
-MEASURE_ONLY = ("HIPDSML_RB_DBG", "HIPDSML_PK_GRID_EXTRA", "HIPDSML_RB_PAIR", "g_head_dbg", "g_wi_dbg")
+MEASURE_ONLY = ("HIPDSML_RB_DBG", "HIPDSML_PK_GRID_EXTRA", "HIPDSML_RB_PAIR", "g_head_dbg", "g_wi_dbg", "g_pk_push_st")
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")

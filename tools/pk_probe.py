@@ -67,6 +67,8 @@ def main() -> int:
                     help="0 pk, 1 pk2, 2 pkg, 3 pkg2, 4 pkx (exchange-free layer 1)")
     ap.add_argument("--l1push", type=int, default=-1,
                     help="pkx dZ1 row pushes: 1 from the layer-1 owner blocks, 0 from the chains, -1 default")
+    ap.add_argument("--push-stamps", default="",
+                    help="measurement build: also write the pusher-0 / tile-0 gather timeline (JSON lines)")
     ap.add_argument("--mirror", action="store_true",
                     help="mirror test mode (pushes loop back with real tags / flags) instead of the probe")
     ap.add_argument("--hop-us", default="",
@@ -174,6 +176,27 @@ def main() -> int:
             tr.synchronize()
             C.mlp_persist_set_stamping(False)
             stamps = decode(C.mlp_persist_stamps(), tr.spec)
+            if a.push_stamps:
+                assert C.measure_build, "--push-stamps needs the measurement build"
+                import statistics
+                raw, ps = C.mlp_persist_stamps(), C.mlp_persist_push_stamps()
+                keys = ["pusher_poll_start", "pusher_staged_seen", "pusher_pushes_issued", "pusher_pushes_acked",
+                        "gather_loads_issued", "gather_first_data", "gather_done"]
+                rel = {k: [] for k in keys}
+                for row in range(6):
+                    g0 = raw[(3 * 8 + 2 + row) * 8 + 0]
+                    gs = [raw[(3 * 8 + 2 + row) * 8 + k] for k in range(4)]
+                    pr = [ps[row * 4 + k] for k in range(4)]
+                    if not g0 or not all(gs) or not all(pr[:3]):
+                        continue
+                    for k, v in zip(keys, pr + gs[1:]):
+                        if v:
+                            rel[k].append((v - g0) / 100.0)
+                with open(a.push_stamps, "a") as f:
+                    f.write(json.dumps({"ranks": n, "mirror": a.mirror,
+                                        "us_after_tile0_gather_entry": {k: round(statistics.median(v), 2)
+                                                                        for k, v in rel.items() if v},
+                                        "rows": len(rel["gather_done"])}) + "\n")
             with open(a.stamps, "a") as f:
                 f.write(json.dumps({"mode": ["pk", "pk2", "pkg", "pkg2", "pkx"][a.algo], "ranks": n,
                                     "mirror": a.mirror, "l1push": a.l1push,
