@@ -1,3 +1,4 @@
+# (the HIPDSML_PK_PUSH_AUX knob was removed after this A/B: no effect)
 # pkx mirror mode, measurement build: the pushers' store cache policy
 # (HIPDSML_PK_PUSH_AUX 0 system scope sc0|sc1 = production, 1 sc1, 2 plain)
 # -- step time and the pusher-0 timeline at N = 4 / 8
