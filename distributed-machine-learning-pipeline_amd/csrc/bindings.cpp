@@ -823,6 +823,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_persist_supported", [](const std::vector<int64_t>& desc) {
     return mlp_persist_supported(desc_from_list(desc));
   });
+  m.def("wgrad_rowblk_plan", [](const std::vector<int>& N, const std::vector<int>& K, int groups) {
+    TORCH_CHECK(N.size() == K.size() && !N.empty() && N.size() <= 8, "wgrad_rowblk_plan: 1-8 layers");
+    TORCH_CHECK(groups >= 1 && groups <= 256, "wgrad_rowblk_plan: 1-256 groups");
+    std::vector<int> st(257);
+    const int g = wgrad_rowblk_plan(N.data(), K.data(), (int)N.size(), groups, st.data());
+    st.resize(g + 1);
+    return st;
+  }, py::arg("N"), py::arg("K"), py::arg("groups"),
+        "row-block update: cost-balanced workgroup runs (unit starts) for layers (N, K) in launch order");
   m.def("mlp_persist_xbuf_granules", []() { return mlp_persist_xbuf_granules(); });
   m.def("mlp_persist_stamps", []() {
     std::vector<uint64_t> v(4 * 8 * 8);

@@ -400,6 +400,10 @@ void wide_input_set_dbg(int bits);
 hipError_t wgrad_rowblk_read_stamps(uint64_t* host_out);  // [256][16], measurement builds
 void wgrad_rowblk_set_stamping(bool on);
 #endif
+// Row-block form (global-batch update): cost-balanced workgroup runs over the
+// units of layers (N[j], K[j]) in launch order; starts[0 .. runs], returns runs
+// (<= groups).  Host only.
+int wgrad_rowblk_plan(const int* N, const int* K, int n, int groups, int* starts);
 hipError_t head_read_stamps(uint64_t* host_out);  // [64][6], profiling only
 void head_set_stamping(bool on);
 #ifdef HIPDSML_MEASURE

@@ -1228,6 +1228,55 @@ static bool rowblk_fits(const WgLayer& L) {
          (int64_t)L.N * L.ldwb * 2 + 16 <= kRbOob && (int64_t)L.N * L.ldwl * 2 + 16 <= kRbOob &&
          (int64_t)L.N * L.ldwh * 2 + 16 <= kRbOob;
 }
+// Workgroup runs of the row-block form's units (layer j, 128-row n block, 64-deep
+// k tile; launch order), balanced by cost, not unit count: every segment a
+// workgroup starts (a new n block) pays its Z^T load and a cold X ring first
+// -- ~2.3 k tiles' worth at M = 512 (profiles/r6_rowblk_balance.json) -- so an
+// equal split of units left the workgroups whose run crossed an n block ~10 us
+// behind the median.  Greedy fill against a target, the target bisected to the
+// smallest that fits `groups` runs.  The segment overhead in k tiles: the
+// stamps price it at ~2.3 at M = 512, but a sweep of the model's constant put
+// the launch's end earliest at 1.5 (M = 512: 1.0 60.2 us, 1.5 48.7, 2.0 50.3,
+// 2.3 50.5).  Writes starts[0 .. runs] and returns the number of runs.
+int wgrad_rowblk_plan(const int* N, const int* K, int n, int groups, int* starts) {
+  int u = 0;
+  for (int j = 0; j < n; ++j) u += ((K[j] + 63) / 64) * ((N[j] + kRbN - 1) / kRbN);
+  const double ov = 1.5;
+  auto fill = [&](double T, int* st) -> int {
+    int g = 0;
+    double cur = 0.0;
+    int prev_seg = -1;
+    if (st) st[0] = 0;
+    for (int j = 0, uu = 0, us = 0; j < n; ++j) {
+      const int kts = (K[j] + 63) / 64, nbs = (N[j] + kRbN - 1) / kRbN;
+      for (int nbk = 0; nbk < nbs; ++nbk) {
+        for (int kt = 0; kt < kts; ++kt, ++uu) {
+          const int seg = us + nbk * kts;  // the unit's segment id (first unit of its n block)
+          double c = 1.0 + ((cur == 0.0 || seg != prev_seg) ? ov : 0.0);
+          if (cur > 0.0 && cur + c > T) {  // close this workgroup's run
+            ++g;
+            if (st) st[g] = uu;
+            cur = 0.0;
+            c = 1.0 + ov;
+          }
+          cur += c;
+          prev_seg = seg;
+        }
+      }
+      us += kts * nbs;
+    }
+    ++g;
+    if (st) st[g] = u;
+    return g;
+  };
+  double lo = 1.0, hi = (double)u * (1.0 + ov) + 1.0;
+  for (int it = 0; it < 40; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (fill(mid, nullptr) <= groups) hi = mid;
+    else lo = mid;
+  }
+  return fill(hi, starts);
+}
 static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t s) {
   WgRowBlk rb{};
   rb.n = n;
@@ -1252,43 +1301,8 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
       if (e != hipSuccess) { cus = 0; return e; }
     }
   }
-  // Runs balanced by cost, not unit count: every segment a workgroup starts (a
-  // new n block) pays its Z^T load and a cold X ring first -- ~2.3 k tiles'
-  // worth at M = 512 (profiles/r6_rowblk_balance.json) -- so an equal split of
-  // units left the workgroups whose run crossed an n block ~10 us behind the
-  // median.  Greedy fill against a target, the target bisected to the
-  // smallest that fits the CUs.
+  // (wgrad_rowblk_plan: runs balanced by a cost model)
   const int G = std::min(std::min(cus, u), kRbMaxGroups);
-  // segment overhead in k tiles: the stamps price it at ~2.3 at M = 512, but a
-  // sweep of the model's constant put the launch's end earliest at 1.5
-  // (M = 512: 1.0 60.2 us, 1.5 48.7, 2.0 50.3, 2.3 50.5 -- profiles/r6_rowblk_balance.json)
-  const double ov = 1.5;
-  auto fill = [&](double T, int* starts) -> int {
-    int g = 0;
-    double cur = 0.0;
-    int prev_seg = -1;
-    if (starts) starts[0] = 0;
-    for (int j = 0, uu = 0; j < n; ++j) {
-      const int kts = rb.ktiles[j], nbs = (layers[j].N + kRbN - 1) / kRbN;
-      for (int nbk = 0; nbk < nbs; ++nbk) {
-        for (int kt = 0; kt < kts; ++kt, ++uu) {
-          const int seg = rb.ustart[j] + nbk * kts;  // the unit's segment id (first unit of its n block)
-          double c = 1.0 + ((cur == 0.0 || seg != prev_seg) ? ov : 0.0);
-          if (cur > 0.0 && cur + c > T) {  // close this workgroup's run
-            ++g;
-            if (starts) starts[g] = uu;
-            cur = 0.0;
-            c = 1.0 + ov;
-          }
-          cur += c;
-          prev_seg = seg;
-        }
-      }
-    }
-    ++g;
-    if (starts) starts[g] = u;
-    return g;
-  };
   // the split depends only on the shapes: computed once per shape set (a host
   // bisection per launch cost ~90 us of launch rate in an eager loop)
   struct Plan {
@@ -1304,15 +1318,11 @@ static hipError_t wgrad_rowblk_launch(const WgLayer* layers, int n, hipStream_t 
   for (int c = 0; c < ncache && !hit; ++c)
     if (std::equal(key, key + 2 + 2 * kWgMaxLayers, cache[c].key)) hit = &cache[c];
   if (hit == nullptr) {
-    double lo = 1.0, hi = (double)u * (1.0 + ov) + 1.0;
-    for (int it = 0; it < 40; ++it) {
-      const double mid = 0.5 * (lo + hi);
-      if (fill(mid, nullptr) <= G) hi = mid;
-      else lo = mid;
-    }
+    int Ns[kWgMaxLayers], Ks[kWgMaxLayers];
+    for (int j = 0; j < n; ++j) { Ns[j] = layers[j].N; Ks[j] = layers[j].K; }
     Plan& pl = cache[ncache < 8 ? ncache++ : 7];
     std::copy(key, key + 2 + 2 * kWgMaxLayers, pl.key);
-    pl.groups = fill(hi, pl.gstart);
+    pl.groups = wgrad_rowblk_plan(Ns, Ks, n, G, pl.gstart);
     hit = &pl;
   }
   rb.groups = hit->groups;
